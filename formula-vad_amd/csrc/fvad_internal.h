@@ -1,0 +1,107 @@
+// Internal definitions shared by the host-side plan/model code and the HIP
+// kernels of the MI355X-native Formula-VAD hot path.  Not part of the C ABI
+// (that is include/fvad.h).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace fvad {
+
+// rnnoise frame geometry (Denoiser.zig:68-70 -> rnnoise_get_frame_size()).
+constexpr int kFrame = 480;
+constexpr int kWin = 960;
+constexpr int kFreq = 481;
+constexpr int kBands = 22;
+constexpr int kFeat = 42;
+constexpr int kCeps = 8;
+constexpr int kPitchBuf = 1728;  // PITCH_MAX_PERIOD + PITCH_FRAME_SIZE
+constexpr int kPitchMax = 768;
+constexpr int kPitchMin = 60;
+constexpr int kXlp = kPitchBuf / 2;  // 864
+constexpr int kMaxNeurons = 128;
+constexpr int kMaxCh = 8;
+constexpr int kMaxBandCfg = 4;
+
+// FFT B (FFT.zig) is a real FFT of fft_size; the device path supports
+// fft_size/2 = 4^k (kissfft then factors into radix-4 only), fft_size <= 4096.
+constexpr int kMaxFftB = 4096;
+
+// ---------------------------------------------------------------------------
+// Per-stream persistent state, one contiguous record per stream (the kernels
+// run one workgroup per stream, so a record is read/written coalesced).
+// Offsets are in 32-bit words.
+// ---------------------------------------------------------------------------
+namespace st {
+constexpr int kPitch = 0;                       // pitch_buf[1728] (last 480 = analysis_mem source)
+constexpr int kSyn = kPitch + kPitchBuf;        // synthesis_mem[480]
+constexpr int kCepsMem = kSyn + kFrame;         // cepstral_mem[8][22]
+constexpr int kLastG = kCepsMem + kCeps * kBands;  // lastg[22]
+constexpr int kVadGru = kLastG + kBands;        // vad_gru_state[128]
+constexpr int kNoiseGru = kVadGru + kMaxNeurons;    // noise_gru_state[128]
+constexpr int kDenGru = kNoiseGru + kMaxNeurons;    // denoise_gru_state[128]
+constexpr int kHp = kDenGru + kMaxNeurons;      // mem_hp_x[2] (float)
+constexpr int kMemId = kHp + 2;                 // int
+constexpr int kLastPeriod = kMemId + 1;         // int
+constexpr int kLastGain = kLastPeriod + 1;      // float
+constexpr int kFramesDone = kLastGain + 1;      // int: ticks processed (480-sample frames per channel)
+constexpr int kVolAcc = kFramesDone + 1;        // float: temp_fft_buffer_vol_ratio
+constexpr int kWords = ((kVolAcc + 1 + 63) / 64) * 64;
+}  // namespace st
+
+// ---------------------------------------------------------------------------
+// Read-only plan tables (built on the host by fvad_plan.cpp, uploaded once).
+// ---------------------------------------------------------------------------
+struct Plan {
+  float half_window[kFrame];     // rnnoise analysis/synthesis half window
+  float dct[kBands * kBands];    // dct_table[i*22+j]
+  float tansig[201];             // tansig_table
+  float band_frac[400];          // (float)j/band_size of bin k inside its band
+  int band_of[400];              // band index i of bin k (k < 400)
+  int eband4[kBands];            // eband5ms[i] << 2
+  float tw960[2 * kWin];         // celt twiddles (r,i)
+  int bitrev960[kWin];           // celt bit-reverse table
+  // FFT B (kissfft real FFT of size nfft_b)
+  int nfft_b;                    // real size (2048)
+  int ncfft_b;                   // nfft_b / 2
+  int stages_b;                  // log4(ncfft_b)
+  float norm_b;                  // windowNormFactor / (nfft/2)
+  float twb[2 * kMaxFftB / 2];   // kissfft substate twiddles (r,i)
+  float superb[2 * kMaxFftB / 4];  // super twiddles (r,i)
+  int permb[kMaxFftB / 2];       // kf_work leaf permutation
+  float hannb[kMaxFftB];         // hannWindowPeriodic(nfft_b)
+};
+
+// Device-side model: int8 weights stored as float (int8->float is exact).
+struct DevDense {
+  int nin, nout, act;
+  const float *w;  // [nin][nout]
+  const float *b;  // [nout]
+};
+struct DevGru {
+  int nin, nout, act;
+  const float *win;   // [nin][3*nout]
+  const float *wrec;  // [nout][3*nout]
+  const float *b;     // [3*nout]
+};
+struct DevModel {
+  DevDense in_dense, den_out, vad_out;
+  DevGru vad, noise, den;
+};
+
+constexpr int kActTanh = 0, kActSigmoid = 1, kActRelu = 2;
+
+// Host-side model (int8, text-file order).
+struct HostLayer {
+  int nin = 0, nout = 0, act = 0;
+  bool gru = false;
+  std::size_t off_w = 0, off_r = 0, off_b = 0;  // offsets into blob
+};
+struct HostModel {
+  HostLayer layers[6];  // input_dense, vad_gru, noise_gru, denoise_gru, denoise_output, vad_output
+  int8_t *blob = nullptr;
+  std::size_t blob_size = 0;
+};
+
+void build_plan(Plan *p, int nfft_b);
+
+}  // namespace fvad
