@@ -1,0 +1,397 @@
+// Batched multi-stream engine (C ABI in include/fvad.h).
+//
+// One engine owns one GPU and a partition of streams.  Device memory layout
+// (all HBM, sized for thousands of streams; 288 GB per MI355X leaves room for
+// hundreds of ticks of input per push):
+//   state   [streams][st::kWords]        persistent rnnoise + re-block state
+//   ring    [streams][channels][ring]    denoised samples awaiting FFT B
+//   pcm     [max_ticks][streams][ch][480] input staging (or resident synthetic)
+//   xbuf    [max_ticks][streams][ch][480] high-passed s16-scale frames (k_prep)
+//   ratio / outputs [max_ticks][streams] (+ channels, bands)
+// A push = k_prep (lane per stream) then k_frame (workgroup per stream) on
+// the engine's HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <algorithm>
+#include <vector>
+
+#include "../../include/fvad.h"
+#include "fvad_internal.h"
+#include "fvad_kernels.h"
+
+const fvad::HostModel *fvad_model_host(const fvad_model *m);
+
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+}  // namespace
+
+extern "C" const char *fvad_last_error(void) { return g_err.c_str(); }
+extern "C" const char *fvad_version(void) { return "fvad-mi355x 0.1 (gfx950)"; }
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) return fail(FVAD_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct fvad_engine {
+  fvad_engine_config cfg{};
+  int ring_len = 0;
+  hipStream_t stream = nullptr;
+  fvad::Plan *d_plan = nullptr;
+  float *d_weights = nullptr;
+  fvad::DevModel dmodel{};
+  float *d_state = nullptr, *d_ring = nullptr;
+  float *d_pcm = nullptr, *d_xbuf = nullptr, *d_ratio = nullptr;
+  float *d_vad = nullptr, *d_wratio = nullptr, *d_wvad = nullptr, *d_band = nullptr, *d_den = nullptr;
+  int *d_wflag = nullptr, *d_ticks = nullptr;
+  int resident_ticks = 0;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  double ms_sum[3] = {0, 0, 0};
+  int n_timed = 0;
+  bool timing_pending = false;
+  int raw_s16 = 0;  // rnnoise compat mode (s16-scaled I/O)
+};
+
+void fvad_engine_set_raw_s16(fvad_engine *e, int raw) { e->raw_s16 = raw; }
+
+extern "C" void fvad_engine_config_default(fvad_engine_config *c, int n_streams, int n_channels) {
+  std::memset(c, 0, sizeof(*c));
+  c->n_streams = n_streams;
+  c->n_channels = n_channels;
+  c->device = 0;
+  c->sample_rate = 48000;
+  c->fft_size = 2048;
+  c->max_ticks = 100;
+  c->n_bands = 1;
+  // VADMachine defaults: freqToBin(100) .. freqToBin(1500) at 48 kHz / 2048 (FFT.zig:120-131)
+  c->band_lo[0] = 4;
+  c->band_hi[0] = 64;
+  c->want_denoised = 0;
+}
+
+namespace {
+
+template <typename T>
+int dalloc(T **p, size_t count) {
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), count * sizeof(T));
+  if (e != hipSuccess) return fail(FVAD_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return FVAD_OK;
+}
+
+int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
+  std::vector<float> w(hm.blob_size);
+  for (size_t i = 0; i < hm.blob_size; i++) w[i] = (float)hm.blob[i];
+  int rc = dalloc(&e->d_weights, w.size());
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(e->d_weights, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
+  auto dense = [&](int l) {
+    const fvad::HostLayer &L = hm.layers[l];
+    fvad::DevDense d;
+    d.nin = L.nin;
+    d.nout = L.nout;
+    d.act = L.act;
+    d.w = e->d_weights + L.off_w;
+    d.b = e->d_weights + L.off_b;
+    return d;
+  };
+  auto gru = [&](int l) {
+    const fvad::HostLayer &L = hm.layers[l];
+    fvad::DevGru g;
+    g.nin = L.nin;
+    g.nout = L.nout;
+    g.act = L.act;
+    g.win = e->d_weights + L.off_w;
+    g.wrec = e->d_weights + L.off_r;
+    g.b = e->d_weights + L.off_b;
+    return g;
+  };
+  e->dmodel.in_dense = dense(0);
+  e->dmodel.vad = gru(1);
+  e->dmodel.noise = gru(2);
+  e->dmodel.den = gru(3);
+  e->dmodel.den_out = dense(4);
+  e->dmodel.vad_out = dense(5);
+  return FVAD_OK;
+}
+
+void free_all(fvad_engine *e) {
+  void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm, e->d_xbuf, e->d_ratio, e->d_vad,
+                  e->d_wratio, e->d_wvad, e->d_band, e->d_den, e->d_wflag, e->d_ticks};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  for (auto &ev : e->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+}
+
+}  // namespace
+
+extern "C" int fvad_engine_reset(fvad_engine *e) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipMemsetAsync(e->d_state, 0, sizeof(float) * fvad::st::kWords * (size_t)e->cfg.n_streams, e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_ring, 0,
+                         sizeof(float) * (size_t)e->ring_len * e->cfg.n_channels * e->cfg.n_streams, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return FVAD_OK;
+}
+
+extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_model *model, fvad_engine **out) {
+  if (!cfg || !model || !out) return fail(FVAD_EINVAL, "null argument");
+  const fvad_engine_config &c = *cfg;
+  if (c.sample_rate != 48000) return fail(FVAD_ERATE, "only 48 kHz is supported (VAD.zig:101-104)");
+  if (c.n_streams < 1 || c.n_channels < 1 || c.n_channels > FVAD_MAX_CHANNELS)
+    return fail(FVAD_EINVAL, "n_streams >= 1 and 1 <= n_channels <= 8 required");
+  if (c.fft_size != 2048 && c.fft_size != 512)
+    return fail(FVAD_EINVAL, "fft_size must be 2048 or 512 on the device path");
+  if (c.max_ticks < 1) return fail(FVAD_EINVAL, "max_ticks must be >= 1");
+  if (c.n_bands < 1 || c.n_bands > FVAD_MAX_BANDS) return fail(FVAD_EINVAL, "1 <= n_bands <= 4");
+  int lo = 1 << 30, hi = -1;
+  for (int b = 0; b < c.n_bands; b++) {
+    if (c.band_lo[b] < 0 || c.band_hi[b] < c.band_lo[b] || c.band_hi[b] > c.fft_size / 2)
+      return fail(FVAD_EINVAL, "invalid band range");
+    lo = std::min(lo, c.band_lo[b]);
+    hi = std::max(hi, c.band_hi[b]);
+  }
+  if (hi - lo + 1 > 256) return fail(FVAD_EINVAL, "reported bins must span <= 256");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FVAD_EDEVICE, "no HIP device available");
+  if (c.device < 0 || c.device >= ndev) return fail(FVAD_EDEVICE, "device ordinal out of range");
+
+  fvad_engine *e = new fvad_engine();
+  e->cfg = c;
+  e->ring_len = c.fft_size + fvad::kFrame;
+  auto bail = [&](int rc) {
+    free_all(e);
+    delete e;
+    return rc;
+  };
+  if (hipSetDevice(c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
+  for (auto &ev : e->ev)
+    if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipEventCreate failed"));
+  fvad::Plan *plan = new fvad::Plan();
+  fvad::build_plan(plan, c.fft_size);
+  int rc = dalloc(&e->d_plan, 1);
+  if (!rc && hipMemcpy(e->d_plan, plan, sizeof(fvad::Plan), hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(FVAD_EDEVICE, "plan upload failed");
+  delete plan;
+  if (rc) return bail(rc);
+  if ((rc = upload_model(e, *fvad_model_host(model)))) return bail(rc);
+  const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
+  const size_t frames = T * B * C * fvad::kFrame;
+  if ((rc = dalloc(&e->d_state, B * fvad::st::kWords)) || (rc = dalloc(&e->d_ring, B * C * e->ring_len)) ||
+      (rc = dalloc(&e->d_pcm, frames)) || (rc = dalloc(&e->d_xbuf, frames)) || (rc = dalloc(&e->d_ratio, T * B)) ||
+      (rc = dalloc(&e->d_vad, T * B)) || (rc = dalloc(&e->d_wratio, T * B)) || (rc = dalloc(&e->d_wvad, T * B)) ||
+      (rc = dalloc(&e->d_wflag, T * B)) || (rc = dalloc(&e->d_band, T * B * C * c.n_bands)) ||
+      (rc = dalloc(&e->d_ticks, B)) || (c.want_denoised && (rc = dalloc(&e->d_den, frames))))
+    return bail(rc);
+  if ((rc = fvad_engine_reset(e))) return bail(rc);
+  *out = e;
+  return FVAD_OK;
+}
+
+extern "C" void fvad_engine_destroy(fvad_engine *e) {
+  if (!e) return;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  free_all(e);
+  delete e;
+}
+
+namespace {
+
+int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
+  const fvad_engine_config &c = e->cfg;
+  fvad::PrepArgs pa;
+  pa.n_streams = c.n_streams;
+  pa.n_channels = c.n_channels;
+  pa.n_ticks = n_ticks;
+  pa.ticks_valid = use_ticks ? e->d_ticks : nullptr;
+  pa.pcm = e->d_pcm;
+  pa.xbuf = e->d_xbuf;
+  pa.ratio = e->d_ratio;
+  pa.state = e->d_state;
+  pa.raw_s16 = e->raw_s16;
+  fvad::FrameArgs fa;
+  fa.n_streams = c.n_streams;
+  fa.n_channels = c.n_channels;
+  fa.n_ticks = n_ticks;
+  fa.ticks_valid = pa.ticks_valid;
+  fa.xbuf = e->d_xbuf;
+  fa.ratio = e->d_ratio;
+  fa.state = e->d_state;
+  fa.ring = e->d_ring;
+  fa.ring_len = e->ring_len;
+  fa.plan = e->d_plan;
+  fa.model = e->dmodel;
+  fa.n_bands = c.n_bands;
+  int lo = 1 << 30, hi = -1;
+  for (int b = 0; b < fvad::kMaxBandCfg; b++) {
+    fa.band_lo[b] = b < c.n_bands ? c.band_lo[b] : 0;
+    fa.band_hi[b] = b < c.n_bands ? c.band_hi[b] : -1;
+    if (b < c.n_bands) {
+      lo = std::min(lo, c.band_lo[b]);
+      hi = std::max(hi, c.band_hi[b]);
+    }
+  }
+  fa.bin_lo_all = lo;
+  fa.bin_hi_all = hi;
+  fa.out_vad = e->d_vad;
+  fa.out_win_ratio = e->d_wratio;
+  fa.out_win_vad = e->d_wvad;
+  fa.out_band = e->d_band;
+  fa.out_den = e->d_den;
+  fa.out_win_flag = e->d_wflag;
+  fa.raw_s16 = e->raw_s16;
+  if (timed) HIP_TRY(hipEventRecord(e->ev[0], e->stream));
+  HIP_TRY(fvad::launch_prep(pa, e->stream));
+  if (timed) HIP_TRY(hipEventRecord(e->ev[1], e->stream));
+  HIP_TRY(fvad::launch_frame(fa, e->stream));
+  if (timed) {
+    HIP_TRY(hipEventRecord(e->ev[2], e->stream));
+    e->timing_pending = true;
+  }
+  return FVAD_OK;
+}
+
+int collect_timing(fvad_engine *e) {
+  if (!e->timing_pending) return FVAD_OK;
+  HIP_TRY(hipEventSynchronize(e->ev[2]));
+  float a = 0, b = 0;
+  HIP_TRY(hipEventElapsedTime(&a, e->ev[0], e->ev[1]));
+  HIP_TRY(hipEventElapsedTime(&b, e->ev[1], e->ev[2]));
+  e->ms_sum[0] += a;
+  e->ms_sum[1] += b;
+  e->ms_sum[2] += a + b;
+  e->n_timed++;
+  e->timing_pending = false;
+  return FVAD_OK;
+}
+
+int fetch(fvad_engine *e, int n_ticks, fvad_outputs *o) {
+  if (!o) return FVAD_OK;
+  const fvad_engine_config &c = e->cfg;
+  const size_t TB = (size_t)n_ticks * c.n_streams;
+  auto cp = [&](void *dst, const void *src, size_t bytes) -> int {
+    if (!dst) return FVAD_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
+    return FVAD_OK;
+  };
+  int rc;
+  if ((rc = cp(o->vad, e->d_vad, TB * 4)) || (rc = cp(o->ratio, e->d_ratio, TB * 4)) ||
+      (rc = cp(o->win_flag, e->d_wflag, TB * 4)) || (rc = cp(o->win_ratio, e->d_wratio, TB * 4)) ||
+      (rc = cp(o->win_vad, e->d_wvad, TB * 4)) || (rc = cp(o->band, e->d_band, TB * c.n_channels * c.n_bands * 4)))
+    return rc;
+  if (o->denoised) {
+    if (!e->d_den) return fail(FVAD_EINVAL, "engine created without want_denoised");
+    if ((rc = cp(o->denoised, e->d_den, TB * c.n_channels * fvad::kFrame * 4))) return rc;
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return FVAD_OK;
+}
+
+}  // namespace
+
+extern "C" int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
+                                fvad_outputs *out) {
+  if (!e || !pcm) return fail(FVAD_EINVAL, "null argument");
+  const fvad_engine_config &c = e->cfg;
+  if (n_ticks < 0 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range [0, max_ticks]");
+  if (n_ticks == 0) return FVAD_OK;
+  HIP_TRY(hipSetDevice(c.device));
+  const size_t bytes = (size_t)n_ticks * c.n_streams * c.n_channels * fvad::kFrame * sizeof(float);
+  HIP_TRY(hipMemcpyAsync(e->d_pcm, pcm, bytes, hipMemcpyHostToDevice, e->stream));
+  if (ticks_valid) {
+    for (int s = 0; s < c.n_streams; s++)
+      if (ticks_valid[s] < 0 || ticks_valid[s] > n_ticks) return fail(FVAD_EINVAL, "ticks_valid out of range");
+    HIP_TRY(hipMemcpyAsync(e->d_ticks, ticks_valid, sizeof(int32_t) * c.n_streams, hipMemcpyHostToDevice, e->stream));
+  }
+  e->resident_ticks = 0;
+  int rc = launch(e, n_ticks, ticks_valid != nullptr, false);
+  if (rc) return rc;
+  return fetch(e, n_ticks, out);
+}
+
+extern "C" int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t base) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  const fvad_engine_config &c = e->cfg;
+  if (n_ticks < 1 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range");
+  HIP_TRY(hipSetDevice(c.device));
+  const size_t n = (size_t)n_ticks * fvad::kFrame;
+  const size_t B = c.n_streams, C = c.n_channels;
+  std::vector<float> host((size_t)n_ticks * B * C * fvad::kFrame);
+  unsigned nthr = std::thread::hardware_concurrency();
+  if (nthr < 1) nthr = 1;
+  if (nthr > 16) nthr = 16;
+  std::vector<std::thread> pool;
+  for (unsigned w = 0; w < nthr; w++) {
+    pool.emplace_back([&, w]() {
+      std::vector<float> one(C * n);
+      for (size_t s = w; s < B; s += nthr) {
+        fvad_synth_stream(base + (uint32_t)s, n, (int)C, one.data(), nullptr, 0);
+        for (int t = 0; t < n_ticks; t++)
+          for (size_t ch = 0; ch < C; ch++)
+            std::memcpy(&host[(((size_t)t * B + s) * C + ch) * fvad::kFrame],
+                        &one[ch * n + (size_t)t * fvad::kFrame], fvad::kFrame * sizeof(float));
+      }
+    });
+  }
+  for (auto &th : pool) th.join();
+  HIP_TRY(hipMemcpy(e->d_pcm, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+  e->resident_ticks = n_ticks;
+  return FVAD_OK;
+}
+
+extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  if (n_ticks < 1 || n_ticks > e->resident_ticks) return fail(FVAD_EINVAL, "n_ticks exceeds resident input");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  int rc = collect_timing(e);
+  if (rc) return rc;
+  return launch(e, n_ticks, false, true);
+}
+
+extern "C" int fvad_engine_sync(fvad_engine *e) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return collect_timing(e);
+}
+
+extern "C" int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_runs) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  int rc = fvad_engine_sync(e);
+  if (rc) return rc;
+  for (int i = 0; i < 3; i++) ms_avg[i] = e->n_timed ? e->ms_sum[i] / e->n_timed : 0.0;
+  if (n_runs) *n_runs = e->n_timed;
+  return FVAD_OK;
+}
+
+extern "C" int fvad_engine_clear_times(fvad_engine *e) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  int rc = fvad_engine_sync(e);
+  if (rc) return rc;
+  e->ms_sum[0] = e->ms_sum[1] = e->ms_sum[2] = 0;
+  e->n_timed = 0;
+  return FVAD_OK;
+}
+
+extern "C" int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  if (n_ticks < 1 || n_ticks > e->cfg.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  return fetch(e, n_ticks, out);
+}

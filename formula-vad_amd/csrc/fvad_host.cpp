@@ -1,0 +1,603 @@
+// Host mirror of the reference's pipeline-side API, above the C ABI:
+//   RollingAverage            (structures/RollingAverage.zig:1-56)
+//   VADMachine                (AudioPipeline/VADMachine.zig:18-310)
+//   AudioPipeline.pushSamples (AudioPipeline.zig:86-120) + VAD frame dispatch
+//                             (VAD.zig:214-251) on a 1-stream engine
+//   multi-stream simulator core (replaces simulator.zig:217-228's thread per
+//                             instance with a lock-step tick loop per GPU)
+//   Evaluator / statistics / formats (Evaluator.zig:90-156,
+//                             Evaluator/statistics.zig:85-284, formats.zig:7-36)
+// The per-frame DSP runs on the GPU (fvad_engine_*); what stays here is the
+// per-window decision logic (cheap: 23.4 windows/s/stream) and the judge.
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fvad.h"
+#include "fvad_internal.h"
+
+namespace {
+
+// ---------------- RollingAverage ----------------
+struct RollingAverage {
+  std::vector<double> data;
+  bool has_last = false;
+  double last_avg = 0;
+  size_t write_idx = 0, written_count = 0;
+  RollingAverage(size_t count, bool has_init, double init) : data(count, 0.0) {
+    if (has_init) {
+      for (size_t i = 0; i < count; i++) data[i] = init;
+      written_count = count;
+      avg();
+    }
+  }
+  double avg() {
+    double a = 0.0;
+    const double scalar = 1.0 / (double)written_count;
+    for (size_t i = 0; i < written_count; i++) a += data[i] * scalar;
+    last_avg = a;
+    has_last = true;
+    return a;
+  }
+  double push(float sample) {
+    data[write_idx] = (double)sample;
+    write_idx = (write_idx + 1) % data.size();
+    if (written_count < data.size()) written_count++;
+    return avg();
+  }
+};
+
+size_t freq_to_bin(int sample_rate, int nfft, float freq) {
+  const float bin_width = (float)sample_rate / (float)nfft;
+  return (size_t)std::round(freq / bin_width);  // Zig @round: half away from zero
+}
+
+// ---------------- VADMachine ----------------
+struct VADMachine {
+  enum State { kClosed, kOpening, kOpen, kClosing };
+  fvad_vadm_config cfg;
+  int sample_rate, fft_size;
+  State state = kClosed;
+  RollingAverage long_term, short_term, ratio;
+  uint64_t speech_start = 0, speech_end = 0;
+  float rnn_vad = 0;
+  size_t rnn_vad_count = 0;
+  float vol_ratio = 0;
+  size_t vol_ratio_count = 0;
+  std::vector<fvad_segment> segments;
+  int band_slot = 0;  // which engine band this machine reads
+  size_t min_bin, max_bin;
+
+  static size_t len_of(float eval_per_sec, float sec) { return (size_t)(eval_per_sec * sec); }
+  VADMachine(const fvad_vadm_config &c, int sr, int fft)
+      : cfg(c),
+        sample_rate(sr),
+        fft_size(fft),
+        long_term(std::max<size_t>(1, len_of((float)sr / (float)fft, c.long_term_speech_avg_sec)),
+                  c.has_initial_long_term_avg != 0, c.initial_long_term_avg),
+        short_term(std::max<size_t>(1, len_of((float)sr / (float)fft, c.short_term_speech_avg_sec)), false, 0),
+        ratio(std::max<size_t>(1, len_of((float)sr / (float)fft, c.channel_vol_ratio_avg_sec)), false, 0) {
+    segments.reserve(100);
+    min_bin = freq_to_bin(sr, fft, c.speech_min_freq);
+    max_bin = freq_to_bin(sr, fft, c.speech_max_freq);
+  }
+  uint64_t rec_start(uint64_t from) const {
+    const uint64_t sb = (uint64_t)((float)sample_rate * 2);
+    return sb > from ? 0 : from - sb;
+  }
+  uint64_t rec_end(uint64_t to) const { return to + (uint64_t)((float)sample_rate * 2); }
+  void track(float vad, float vr, State from, State to) {
+    if (from == kClosed && to == kOpening) {
+      rnn_vad = vad;
+      rnn_vad_count = 1;
+      vol_ratio = vr;
+      vol_ratio_count = 1;
+    } else if (from == kOpening || from == kOpen) {
+      rnn_vad += vad;
+      rnn_vad_count += 1;
+      vol_ratio += vr;
+      vol_ratio_count += 1;
+    }
+  }
+  void on_speech_end() {
+    const uint64_t len = speech_end - speech_start;
+    const float len_rt = (float)len / (float)sample_rate;
+    if (len_rt >= cfg.min_vad_duration_sec) {
+      fvad_segment s;
+      s.sample_from = rec_start(speech_start);
+      s.sample_to = rec_end(speech_end);
+      s.debug_rnn_vad = rnn_vad / (float)rnn_vad_count;
+      s.debug_avg_speech_vol_ratio = vol_ratio / (float)vol_ratio_count;
+      segments.push_back(s);
+    }
+  }
+  // VADMachine.run: channel band sums of this window, window vad (has_vad) and ratio
+  void run(uint64_t index, const float *band_per_channel, int n_ch, int band_stride, float vad, float vr) {
+    float min_v = 999, max_v = 0;
+    for (int c = 0; c < n_ch; c++) {
+      const float v = band_per_channel[c * band_stride];
+      if (v < min_v) min_v = v;
+      if (v > max_v) max_v = v;
+    }
+    const float sr = (float)sample_rate;
+    const size_t min_open = (size_t)(sr * cfg.min_consecutive_sec_to_open);
+    const size_t max_gap = (size_t)(sr * cfg.max_speech_gap_sec);
+    const double st_avg = short_term.push(min_v);
+    const double r_avg = ratio.push(vr);
+    double base;
+    if (long_term.has_last)
+      base = long_term.last_avg;
+    else if (cfg.has_initial_long_term_avg)
+      base = cfg.initial_long_term_avg;
+    else
+      base = st_avg;
+    const double threshold = base * (double)cfg.speech_threshold_factor;
+    const bool met = st_avg > threshold && r_avg > (double)cfg.channel_vol_ratio_threshold;
+    if (!met) long_term.push(min_v);
+    switch (state) {
+      case kClosed:
+        if (met) {
+          state = kOpening;
+          speech_start = index;
+        }
+        track(vad, vr, kClosed, state);
+        break;
+      case kOpening:
+        if (met && index - speech_start >= min_open)
+          state = kOpen;
+        else if (!met)
+          state = kClosed;
+        track(vad, vr, kOpening, state);
+        break;
+      case kOpen:
+        if (!met) {
+          state = kClosing;
+          speech_end = index;
+        }
+        track(vad, vr, kOpen, state);
+        break;
+      case kClosing:
+        if (met)
+          state = kOpen;
+        else if (index - speech_end >= max_gap) {
+          state = kClosed;
+          on_speech_end();
+        }
+        track(vad, vr, kClosing, state);
+        break;
+    }
+  }
+};
+
+// Engine band slots for a set of machine configs (unique bin ranges).
+int assign_bands(std::vector<VADMachine> &ms, fvad_engine_config &ec) {
+  ec.n_bands = 0;
+  for (auto &m : ms) {
+    int slot = -1;
+    for (int b = 0; b < ec.n_bands; b++)
+      if (ec.band_lo[b] == (int)m.min_bin && ec.band_hi[b] == (int)m.max_bin) slot = b;
+    if (slot < 0) {
+      if (ec.n_bands == FVAD_MAX_BANDS) return FVAD_EINVAL;
+      slot = ec.n_bands++;
+      ec.band_lo[slot] = (int)m.min_bin;
+      ec.band_hi[slot] = (int)m.max_bin;
+    }
+    m.band_slot = slot;
+  }
+  return FVAD_OK;
+}
+
+}  // namespace
+
+extern "C" void fvad_vadm_config_default(fvad_vadm_config *c) {
+  c->speech_min_freq = 100;
+  c->speech_max_freq = 1500;
+  c->long_term_speech_avg_sec = 180;
+  c->has_initial_long_term_avg = 1;
+  c->initial_long_term_avg = 0.005;
+  c->short_term_speech_avg_sec = 0.2f;
+  c->speech_threshold_factor = 18;
+  c->channel_vol_ratio_avg_sec = 0.5f;
+  c->channel_vol_ratio_threshold = 0.5f;
+  c->min_consecutive_sec_to_open = 0.2f;
+  c->max_speech_gap_sec = 2;
+  c->min_vad_duration_sec = 0.7f;
+}
+
+// ---------------------------------------------------------------------------
+// Tick driver shared by the single-stream pipeline and the multi-stream core:
+// consumes engine outputs of n_ticks and feeds each stream's machines.
+// ---------------------------------------------------------------------------
+namespace {
+struct StreamMachines {
+  std::vector<VADMachine> machines;  // [0] = main
+  uint64_t windows_done = 0;
+};
+
+struct TickBuffers {
+  std::vector<float> vad, ratio, win_ratio, win_vad, band;
+  std::vector<int32_t> win_flag;
+  void resize(size_t tb, int C, int nb) {
+    vad.resize(tb);
+    ratio.resize(tb);
+    win_ratio.resize(tb);
+    win_vad.resize(tb);
+    win_flag.resize(tb);
+    band.resize(tb * C * nb);
+  }
+  fvad_outputs outputs() {
+    fvad_outputs o;
+    std::memset(&o, 0, sizeof(o));
+    o.vad = vad.data();
+    o.ratio = ratio.data();
+    o.win_flag = win_flag.data();
+    o.win_ratio = win_ratio.data();
+    o.win_vad = win_vad.data();
+    o.band = band.data();
+    return o;
+  }
+};
+
+void consume(std::vector<StreamMachines *> &sm, const TickBuffers &tb, int n_ticks, int n_streams, int C, int nb,
+             int fft_size, const int32_t *ticks_valid) {
+  for (int s = 0; s < n_streams; s++) {
+    const int nt = ticks_valid ? ticks_valid[s] : n_ticks;
+    for (int t = 0; t < nt; t++) {
+      const size_t o = (size_t)t * n_streams + s;
+      if (!tb.win_flag[o]) continue;
+      const uint64_t index = sm[s]->windows_done * (uint64_t)fft_size;
+      for (auto &m : sm[s]->machines)
+        m.run(index, &tb.band[(o * C) * nb + m.band_slot], C, nb, tb.win_vad[o], tb.win_ratio[o]);
+      sm[s]->windows_done++;
+    }
+  }
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// AudioPipeline (single stream)
+// ---------------------------------------------------------------------------
+struct fvad_pipeline {
+  int n_channels;
+  fvad_engine *engine = nullptr;
+  fvad_engine_config ec;
+  StreamMachines sm;
+  std::vector<std::vector<float>> pending;  // samples not yet forming a full 480 frame
+  uint64_t total_write_count = 0;
+  TickBuffers tb;
+  std::vector<float> pcm;
+};
+
+extern "C" int fvad_pipeline_create(int sample_rate, int n_channels, const fvad_model *model, int device,
+                                    const fvad_vadm_config *main_cfg, const fvad_vadm_config *alt_cfgs, int n_alt,
+                                    fvad_pipeline **out) {
+  if (!model || !out || n_channels < 1 || n_channels > FVAD_MAX_CHANNELS || n_alt < 0) return FVAD_EINVAL;
+  if (sample_rate != 48000) return FVAD_ERATE;
+  fvad_pipeline *p = new fvad_pipeline();
+  p->n_channels = n_channels;
+  fvad_vadm_config def;
+  fvad_vadm_config_default(&def);
+  p->sm.machines.emplace_back(main_cfg ? *main_cfg : def, sample_rate, 2048);
+  for (int i = 0; i < n_alt; i++) p->sm.machines.emplace_back(alt_cfgs[i], sample_rate, 2048);
+  fvad_engine_config_default(&p->ec, 1, n_channels);
+  p->ec.device = device;
+  p->ec.max_ticks = 100;
+  int rc = assign_bands(p->sm.machines, p->ec);
+  if (!rc) rc = fvad_engine_create(&p->ec, model, &p->engine);
+  if (rc) {
+    delete p;
+    return rc;
+  }
+  p->pending.assign(n_channels, {});
+  p->tb.resize(p->ec.max_ticks, n_channels, p->ec.n_bands);
+  p->pcm.resize((size_t)p->ec.max_ticks * n_channels * fvad::kFrame);
+  *out = p;
+  return FVAD_OK;
+}
+
+extern "C" void fvad_pipeline_destroy(fvad_pipeline *p) {
+  if (!p) return;
+  fvad_engine_destroy(p->engine);
+  delete p;
+}
+
+extern "C" int fvad_pipeline_push(fvad_pipeline *p, const float *const *pcm, size_t n, uint64_t *first_index) {
+  if (!p || (!pcm && n)) return FVAD_EINVAL;
+  if (first_index) *first_index = p->total_write_count;
+  const int C = p->n_channels;
+  for (int c = 0; c < C; c++) p->pending[c].insert(p->pending[c].end(), pcm[c], pcm[c] + n);
+  p->total_write_count += n;
+  size_t avail = p->pending[0].size() / fvad::kFrame;
+  size_t consumed = 0;
+  std::vector<StreamMachines *> sm{&p->sm};
+  while (avail > 0) {
+    const int nt = (int)std::min<size_t>(avail, (size_t)p->ec.max_ticks);
+    for (int t = 0; t < nt; t++)
+      for (int c = 0; c < C; c++)
+        std::memcpy(&p->pcm[((size_t)t * C + c) * fvad::kFrame], &p->pending[c][consumed + (size_t)t * fvad::kFrame],
+                    fvad::kFrame * sizeof(float));
+    fvad_outputs o = p->tb.outputs();
+    int rc = fvad_engine_push(p->engine, p->pcm.data(), nt, nullptr, &o);
+    if (rc) return rc;
+    consume(sm, p->tb, nt, 1, C, p->ec.n_bands, p->ec.fft_size, nullptr);
+    consumed += (size_t)nt * fvad::kFrame;
+    avail -= nt;
+  }
+  for (int c = 0; c < C; c++) p->pending[c].erase(p->pending[c].begin(), p->pending[c].begin() + consumed);
+  return FVAD_OK;
+}
+
+extern "C" size_t fvad_pipeline_segments(const fvad_pipeline *p, int alt, fvad_segment *out, size_t cap) {
+  const size_t idx = alt < 0 ? 0 : (size_t)alt + 1;
+  if (!p || idx >= p->sm.machines.size()) return 0;
+  const auto &segs = p->sm.machines[idx].segments;
+  for (size_t i = 0; i < segs.size() && i < cap; i++) out[i] = segs[i];
+  return segs.size();
+}
+
+// ---------------------------------------------------------------------------
+// Multi-stream simulator core: streams partitioned contiguously over devices,
+// one host thread and one engine per device, lock-step ticks (no collectives).
+// ---------------------------------------------------------------------------
+struct fvad_multi {
+  int n_streams, n_channels, ticks_per_push;
+  struct Part {
+    int device, s0, s1;
+    fvad_engine *engine = nullptr;
+    fvad_engine_config ec;
+  };
+  std::vector<Part> parts;
+  std::vector<StreamMachines> sm;
+  fvad_vadm_config cfg;
+};
+
+extern "C" int fvad_multi_create(int n_streams, int n_channels, const fvad_model *model, const int *devices,
+                                 int n_devices, const fvad_vadm_config *cfg, int ticks_per_push, fvad_multi **out) {
+  if (!model || !out || n_streams < 1 || n_devices < 1 || !devices || ticks_per_push < 1) return FVAD_EINVAL;
+  fvad_multi *m = new fvad_multi();
+  m->n_streams = n_streams;
+  m->n_channels = n_channels;
+  m->ticks_per_push = ticks_per_push;
+  if (cfg)
+    m->cfg = *cfg;
+  else
+    fvad_vadm_config_default(&m->cfg);
+  for (int s = 0; s < n_streams; s++) {
+    StreamMachines x;
+    x.machines.emplace_back(m->cfg, 48000, 2048);
+    m->sm.push_back(std::move(x));
+  }
+  const int nd = std::min(n_devices, n_streams);
+  for (int d = 0; d < nd; d++) {
+    fvad_multi::Part p;
+    p.device = devices[d];
+    p.s0 = (int)((long)n_streams * d / nd);
+    p.s1 = (int)((long)n_streams * (d + 1) / nd);
+    fvad_engine_config_default(&p.ec, p.s1 - p.s0, n_channels);
+    p.ec.device = p.device;
+    p.ec.max_ticks = ticks_per_push;
+    std::vector<VADMachine> tmp{m->sm[p.s0].machines[0]};
+    assign_bands(tmp, p.ec);
+    for (int s = p.s0; s < p.s1; s++) m->sm[s].machines[0].band_slot = tmp[0].band_slot;
+    const int rc = fvad_engine_create(&p.ec, model, &p.engine);
+    if (rc) {
+      fvad_multi_destroy(m);
+      return rc;
+    }
+    m->parts.push_back(p);
+  }
+  *out = m;
+  return FVAD_OK;
+}
+
+extern "C" void fvad_multi_destroy(fvad_multi *m) {
+  if (!m) return;
+  for (auto &p : m->parts) fvad_engine_destroy(p.engine);
+  delete m;
+}
+
+extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size_t *len) {
+  if (!m || !pcm || !len) return FVAD_EINVAL;
+  const int C = m->n_channels;
+  std::vector<int> rcs(m->parts.size(), FVAD_OK);
+  std::vector<std::thread> th;
+  for (size_t pi = 0; pi < m->parts.size(); pi++) {
+    th.emplace_back([&, pi]() {
+      fvad_multi::Part &p = m->parts[pi];
+      const int B = p.s1 - p.s0, T = p.ec.max_ticks;
+      size_t max_frames = 0;
+      for (int s = p.s0; s < p.s1; s++) max_frames = std::max(max_frames, len[s] / fvad::kFrame);
+      std::vector<float> buf((size_t)T * B * C * fvad::kFrame, 0.0f);
+      std::vector<int32_t> valid(B);
+      TickBuffers tb;
+      tb.resize((size_t)T * B, C, p.ec.n_bands);
+      std::vector<StreamMachines *> sm;
+      for (int s = p.s0; s < p.s1; s++) sm.push_back(&m->sm[s]);
+      for (size_t f0 = 0; f0 < max_frames; f0 += T) {
+        const int nt = (int)std::min<size_t>(T, max_frames - f0);
+        for (int b = 0; b < B; b++) {
+          const int s = p.s0 + b;
+          const size_t frames_s = len[s] / fvad::kFrame;
+          valid[b] = (int)(frames_s > f0 ? std::min<size_t>(nt, frames_s - f0) : 0);
+          for (int t = 0; t < valid[b]; t++)
+            for (int c = 0; c < C; c++)
+              std::memcpy(&buf[(((size_t)t * B + b) * C + c) * fvad::kFrame],
+                          pcm[s] + (size_t)c * len[s] + (f0 + t) * fvad::kFrame, fvad::kFrame * sizeof(float));
+        }
+        fvad_outputs o = tb.outputs();
+        const int rc = fvad_engine_push(p.engine, buf.data(), nt, valid.data(), &o);
+        if (rc) {
+          rcs[pi] = rc;
+          return;
+        }
+        consume(sm, tb, nt, B, C, p.ec.n_bands, p.ec.fft_size, valid.data());
+      }
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int rc : rcs)
+    if (rc) return rc;
+  return FVAD_OK;
+}
+
+extern "C" size_t fvad_multi_segments(const fvad_multi *m, int stream, fvad_segment *out, size_t cap) {
+  if (!m || stream < 0 || stream >= m->n_streams) return 0;
+  const auto &segs = m->sm[stream].machines[0].segments;
+  for (size_t i = 0; i < segs.size() && i < cap; i++) out[i] = segs[i];
+  return segs.size();
+}
+
+// ---------------------------------------------------------------------------
+// Evaluator / statistics / formats
+// ---------------------------------------------------------------------------
+namespace {
+struct Seg {
+  float from, to;
+  std::vector<size_t> opp;
+};
+float overlap_with(float af, float at, float bf, float bt) {
+  const float max_from = af > bf ? af : bf;
+  const float min_to = at < bt ? at : bt;
+  return min_to - max_from;
+}
+void sort_by_start(std::vector<Seg> &v) {
+  std::stable_sort(v.begin(), v.end(), [](const Seg &a, const Seg &b) { return a.from < b.from; });
+}
+float false_positive(const Seg &v, const std::vector<Seg> &refs, const fvad_stat_config &c) {
+  // extrudeSegments (statistics.zig:191-218) + calcOverlapMany
+  const size_t n = v.opp.size();
+  std::vector<float> f(n), t(n);
+  for (size_t i = 0; i < n; i++) {
+    f[i] = refs[v.opp[i]].from;
+    t[i] = refs[v.opp[i]].to;
+  }
+  if (n > 0) {
+    f[0] -= c.extrude_start;
+    t[n - 1] += c.extrude_end;
+    for (size_t i = 0; i + 1 < n; i++)
+      if (f[i + 1] - t[i] <= c.fill_gaps) t[i] = f[i + 1];
+  }
+  float ov = 0.0f;
+  for (size_t i = 0; i < n; i++) {
+    const float o = overlap_with(v.from, v.to, f[i], t[i]);
+    ov += 0.0f > o ? 0.0f : o;
+  }
+  return (v.to - v.from) - ov;
+}
+float f_score(float beta, float p, float r) {
+  const float b2 = beta * beta;  // std.math.pow(f32, beta, 2)
+  return (1 + b2) * (p * r) / (b2 * p + r);
+}
+}  // namespace
+
+extern "C" int fvad_eval_stats(const float *vad, size_t nv, const float *ref, size_t nr, const fvad_stat_config *cfg,
+                               fvad_single_stats *out) {
+  if ((!vad && nv) || (!ref && nr) || !cfg || !out) return FVAD_EINVAL;
+  std::vector<Seg> vs(nv), rs(nr);
+  for (size_t i = 0; i < nv; i++) vs[i] = {vad[2 * i], vad[2 * i + 1], {}};
+  for (size_t i = 0; i < nr; i++) rs[i] = {ref[2 * i], ref[2 * i + 1], {}};
+  sort_by_start(vs);
+  sort_by_start(rs);
+  for (auto &v : vs)
+    for (size_t j = 0; j < rs.size(); j++)
+      if (overlap_with(v.from, v.to, rs[j].from, rs[j].to) > 0.0f) v.opp.push_back(j);
+  for (auto &r : rs)
+    for (size_t j = 0; j < vs.size(); j++)
+      if (overlap_with(r.from, r.to, vs[j].from, vs[j].to) > 0.0f) r.opp.push_back(j);
+  fvad_single_stats s;
+  std::memset(&s, 0, sizeof(s));
+  for (const auto &v : vs) {
+    s.false_positives_sec += false_positive(v, rs, *cfg);
+    const float tp = (v.to - v.from) - false_positive(v, rs, *cfg);
+    s.true_positives_sec += tp;
+    s.total_positives_sec += tp;
+  }
+  for (const auto &r : rs) {
+    if ((r.to - r.from) < cfg->ignore_shorter_than_sec) continue;
+    float ov = 0.0f;
+    for (size_t j : r.opp) {
+      const float o = overlap_with(r.from, r.to, vs[j].from, vs[j].to);
+      ov += 0.0f > o ? 0.0f : o;
+    }
+    const float fn = (r.to - r.from) - ov;
+    s.false_negatives_sec += fn;
+    s.total_positives_sec += fn;
+  }
+  s.true_positive_rate = s.true_positives_sec / s.total_positives_sec;
+  s.false_negative_rate = s.false_negatives_sec / s.total_positives_sec;
+  s.false_discovery_rate = s.false_positives_sec / (s.false_positives_sec + s.true_positives_sec);
+  s.precision = s.true_positives_sec / (s.true_positives_sec + s.false_positives_sec);
+  s.f_score_beta = 0.7f;
+  s.f_score = f_score(s.f_score_beta, s.precision, s.true_positive_rate);
+  s.fm_index = std::sqrt(s.precision * s.true_positive_rate);
+  *out = s;
+  return FVAD_OK;
+}
+
+extern "C" void fvad_eval_aggregate(const fvad_single_stats *st, size_t n, fvad_aggregate_stats *a) {
+  std::memset(a, 0, sizeof(*a));
+  fvad_agg_stat *aggs[4] = {&a->true_positive_rate, &a->false_negative_rate, &a->false_discovery_rate, &a->precision};
+  for (auto *x : aggs) {
+    x->min = 2;
+    x->max = -2;
+  }
+  float sums[4] = {0, 0, 0, 0};
+  for (size_t i = 0; i < n; i++) {
+    const fvad_single_stats &s = st[i];
+    a->total_positives_sec += s.total_positives_sec;
+    a->true_positives_sec += s.true_positives_sec;
+    a->false_positives_sec += s.false_positives_sec;
+    a->false_negatives_sec += s.false_negatives_sec;
+    const float vals[4] = {s.true_positive_rate, s.false_negative_rate, s.false_discovery_rate, s.precision};
+    for (int k = 0; k < 4; k++) {
+      sums[k] += vals[k];
+      if (vals[k] < aggs[k]->min) aggs[k]->min = vals[k];
+      if (vals[k] > aggs[k]->max) aggs[k]->max = vals[k];
+    }
+  }
+  const float nf = (float)n;
+  a->true_positive_rate.overall = a->true_positives_sec / a->total_positives_sec;
+  a->false_negative_rate.overall = a->false_negatives_sec / a->total_positives_sec;
+  a->false_discovery_rate.overall = a->false_positives_sec / (a->false_positives_sec + a->true_positives_sec);
+  a->precision.overall = a->true_positives_sec / (a->true_positives_sec + a->false_positives_sec);
+  for (int k = 0; k < 4; k++) aggs[k]->avg = sums[k] / nf;
+  a->f_score_beta = 0.7f;
+  a->f_score = f_score(a->f_score_beta, a->precision.overall, a->true_positive_rate.overall);
+  a->fm_index = std::sqrt(a->precision.overall * a->true_positive_rate.overall);
+}
+
+extern "C" long fvad_parse_audacity(const char *txt, size_t len, float *out, size_t cap) {
+  // formats.parseAudacitySegments: split the raw text on '\n' (CRs are NOT
+  // stripped, formats.zig:11-14), each line on '\t'; lines with < 2 fields are
+  // skipped, an unparsable from/to field is an error.
+  long n = 0;
+  size_t pos = 0;
+  while (pos <= len) {
+    size_t e = pos;
+    while (e < len && txt[e] != '\n') e++;
+    size_t t1 = pos;
+    while (t1 < e && txt[t1] != '\t') t1++;
+    if (t1 < e) {
+      size_t t2 = t1 + 1;
+      while (t2 < e && txt[t2] != '\t') t2++;
+      const std::string a(txt + pos, t1 - pos), b(txt + t1 + 1, t2 - t1 - 1);
+      if (a.empty() || b.empty()) return FVAD_EFORMAT;
+      char *end = nullptr;
+      const float from = std::strtof(a.c_str(), &end);
+      if (*end) return FVAD_EFORMAT;
+      const float to = std::strtof(b.c_str(), &end);
+      if (*end) return FVAD_EFORMAT;
+      if ((size_t)n < cap && out) {
+        out[2 * n] = from;
+        out[2 * n + 1] = to;
+      }
+      n++;
+    }
+    pos = e + 1;
+  }
+  return n;
+}

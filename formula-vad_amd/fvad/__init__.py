@@ -1,0 +1,428 @@
+"""Python bindings (ctypes) for libfvad.so — the MI355X-native Formula-VAD hot path.
+
+Mirrors the reference's API surface for this path:
+  * Denoiser        (src/Denoiser.zig)        -> rnnoise_* C ABI on the GPU
+  * KissFFTR        (src/FFT.zig kissfft use) -> kiss_fftr_* C ABI on the GPU
+  * Engine          batched multi-stream hot path (fvad_engine_*)
+  * AudioPipeline   (src/AudioPipeline.zig pushSamples + VAD + VADMachine)
+  * Multi           multi-stream simulator core (simulator.zig runAll)
+  * evaluate/aggregate/parse_audacity (src/Evaluator/*)
+
+All compute goes through the HIP kernels in libfvad.so; there is no CPU
+fallback — operations raise FvadError when the library or the GPU is missing.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfvad.so")
+
+FVAD_OK = 0
+F32P = C.POINTER(C.c_float)
+I32P = C.POINTER(C.c_int32)
+MAX_BANDS = 4
+FRAME = 480
+
+
+class FvadError(RuntimeError):
+    pass
+
+
+class EngineConfig(C.Structure):
+    _fields_ = [("n_streams", C.c_int), ("n_channels", C.c_int), ("device", C.c_int), ("sample_rate", C.c_int),
+                ("fft_size", C.c_int), ("max_ticks", C.c_int), ("n_bands", C.c_int),
+                ("band_lo", C.c_int * MAX_BANDS), ("band_hi", C.c_int * MAX_BANDS), ("want_denoised", C.c_int)]
+
+
+class Outputs(C.Structure):
+    _fields_ = [("vad", F32P), ("ratio", F32P), ("win_flag", I32P), ("win_ratio", F32P), ("win_vad", F32P),
+                ("band", F32P), ("denoised", F32P)]
+
+
+class VadmConfig(C.Structure):
+    _fields_ = [("speech_min_freq", C.c_float), ("speech_max_freq", C.c_float),
+                ("long_term_speech_avg_sec", C.c_float), ("has_initial_long_term_avg", C.c_int),
+                ("initial_long_term_avg", C.c_double), ("short_term_speech_avg_sec", C.c_float),
+                ("speech_threshold_factor", C.c_float), ("channel_vol_ratio_avg_sec", C.c_float),
+                ("channel_vol_ratio_threshold", C.c_float), ("min_consecutive_sec_to_open", C.c_float),
+                ("max_speech_gap_sec", C.c_float), ("min_vad_duration_sec", C.c_float)]
+
+    @classmethod
+    def default(cls):
+        c = cls()
+        lib().fvad_vadm_config_default(C.byref(c))
+        return c
+
+
+class Segment(C.Structure):
+    _fields_ = [("sample_from", C.c_uint64), ("sample_to", C.c_uint64), ("debug_rnn_vad", C.c_float),
+                ("debug_avg_speech_vol_ratio", C.c_float)]
+
+
+class StatConfig(C.Structure):
+    _fields_ = [("ignore_shorter_than_sec", C.c_float), ("extrude_start", C.c_float), ("extrude_end", C.c_float),
+                ("fill_gaps", C.c_float)]
+
+
+_STAT_FIELDS = ("total_positives_sec", "true_positives_sec", "false_positives_sec", "false_negatives_sec",
+                "true_positive_rate", "false_negative_rate", "false_discovery_rate", "precision", "fm_index",
+                "f_score", "f_score_beta")
+
+
+class SingleStats(C.Structure):
+    _fields_ = [(n, C.c_float) for n in _STAT_FIELDS]
+
+
+class AggStat(C.Structure):
+    _fields_ = [("overall", C.c_float), ("min", C.c_float), ("max", C.c_float), ("avg", C.c_float)]
+
+
+class AggregateStats(C.Structure):
+    _fields_ = [("total_positives_sec", C.c_float), ("true_positives_sec", C.c_float),
+                ("false_positives_sec", C.c_float), ("false_negatives_sec", C.c_float),
+                ("true_positive_rate", AggStat), ("false_negative_rate", AggStat),
+                ("false_discovery_rate", AggStat), ("precision", AggStat), ("fm_index", C.c_float),
+                ("f_score", C.c_float), ("f_score_beta", C.c_float)]
+
+
+class KissCpx(C.Structure):
+    _fields_ = [("r", C.c_float), ("i", C.c_float)]
+
+
+# Every symbol include/fvad.h declares: (name, restype, argtypes)
+SYMBOLS = [
+    ("fvad_last_error", C.c_char_p, []),
+    ("fvad_version", C.c_char_p, []),
+    ("rnnoise_create", C.c_void_p, [C.c_void_p]),
+    ("rnnoise_destroy", None, [C.c_void_p]),
+    ("rnnoise_process_frame", C.c_float, [C.c_void_p, F32P, F32P]),
+    ("rnnoise_get_frame_size", C.c_int, []),
+    ("fvad_set_default_model", None, [C.c_void_p]),
+    ("kiss_fftr_alloc", C.c_void_p, [C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_size_t)]),
+    ("kiss_fftr", None, [C.c_void_p, F32P, C.c_void_p]),
+    ("fvad_model_synthetic", C.c_int, [C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("fvad_model_load_text", C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
+    ("fvad_model_free", None, [C.c_void_p]),
+    ("fvad_model_blob", C.c_size_t, [C.c_void_p, C.c_void_p]),
+    ("fvad_engine_config_default", None, [C.c_void_p, C.c_int, C.c_int]),
+    ("fvad_engine_create", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fvad_engine_destroy", None, [C.c_void_p]),
+    ("fvad_engine_reset", C.c_int, [C.c_void_p]),
+    ("fvad_engine_push", C.c_int, [C.c_void_p, F32P, C.c_int, I32P, C.c_void_p]),
+    ("fvad_engine_load_synthetic", C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
+    ("fvad_engine_run_resident", C.c_int, [C.c_void_p, C.c_int]),
+    ("fvad_engine_sync", C.c_int, [C.c_void_p]),
+    ("fvad_engine_kernel_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+    ("fvad_engine_clear_times", C.c_int, [C.c_void_p]),
+    ("fvad_engine_fetch", C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    ("fvad_vadm_config_default", None, [C.c_void_p]),
+    ("fvad_pipeline_create", C.c_int, [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                       C.POINTER(C.c_void_p)]),
+    ("fvad_pipeline_destroy", None, [C.c_void_p]),
+    ("fvad_pipeline_push", C.c_int, [C.c_void_p, C.POINTER(F32P), C.c_size_t, C.POINTER(C.c_uint64)]),
+    ("fvad_pipeline_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    ("fvad_multi_create", C.c_int, [C.c_int, C.c_int, C.c_void_p, I32P, C.c_int, C.c_void_p, C.c_int,
+                                    C.POINTER(C.c_void_p)]),
+    ("fvad_multi_destroy", None, [C.c_void_p]),
+    ("fvad_multi_run", C.c_int, [C.c_void_p, C.POINTER(F32P), C.POINTER(C.c_size_t)]),
+    ("fvad_multi_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    ("fvad_eval_stats", C.c_int, [F32P, C.c_size_t, F32P, C.c_size_t, C.c_void_p, C.c_void_p]),
+    ("fvad_eval_aggregate", None, [C.c_void_p, C.c_size_t, C.c_void_p]),
+    ("fvad_parse_audacity", C.c_long, [C.c_char_p, C.c_size_t, F32P, C.c_size_t]),
+    ("fvad_synth_stream", C.c_long, [C.c_uint32, C.c_size_t, C.c_int, F32P, F32P, C.c_size_t]),
+    ("fvad_simulator_main", C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libfvad.so (built in-tree by `make -C formula-vad_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FvadError("libfvad.so not built: run `make -C formula-vad_amd` (%s)" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SYMBOLS:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error():
+    return lib().fvad_last_error().decode()
+
+
+def _check(rc, what):
+    if rc != FVAD_OK:
+        raise FvadError("%s failed (%d): %s" % (what, rc, last_error()))
+
+
+def fptr(a):
+    return a.ctypes.data_as(F32P)
+
+
+class Model:
+    def __init__(self, seed=None, path=None):
+        h = C.c_void_p()
+        if path is not None:
+            _check(lib().fvad_model_load_text(path.encode(), C.byref(h)), "fvad_model_load_text")
+        else:
+            _check(lib().fvad_model_synthetic(0 if seed is None else seed, C.byref(h)), "fvad_model_synthetic")
+        self.h = h
+
+    def blob(self):
+        n = lib().fvad_model_blob(self.h, None)
+        b = np.zeros(n, np.int8)
+        lib().fvad_model_blob(self.h, b.ctypes.data_as(C.c_void_p))
+        return b
+
+    def __del__(self):
+        try:
+            lib().fvad_model_free(self.h)
+        except Exception:
+            pass
+
+
+def synth_stream(stream_id, n_samples, n_channels=2, label_cap=4096):
+    """Synthetic 48 kHz onboard audio (planar [ch][n]) and its speech labels (seconds)."""
+    out = np.zeros((n_channels, n_samples), np.float32)
+    lab = np.zeros(2 * label_cap, np.float32)
+    n = lib().fvad_synth_stream(stream_id, n_samples, n_channels, fptr(out), fptr(lab), label_cap)
+    return out, lab[: 2 * min(n, label_cap)].reshape(-1, 2).copy()
+
+
+class Engine:
+    """Batched hot path for a partition of streams on one GPU."""
+
+    def __init__(self, model, n_streams, n_channels=2, device=0, max_ticks=100, fft_size=2048, bands=((4, 64),),
+                 want_denoised=False):
+        cfg = EngineConfig()
+        lib().fvad_engine_config_default(C.byref(cfg), n_streams, n_channels)
+        cfg.device = device
+        cfg.max_ticks = max_ticks
+        cfg.fft_size = fft_size
+        cfg.n_bands = len(bands)
+        for i, (lo, hi) in enumerate(bands):
+            cfg.band_lo[i] = lo
+            cfg.band_hi[i] = hi
+        cfg.want_denoised = int(want_denoised)
+        self.cfg = cfg
+        self.model = model
+        h = C.c_void_p()
+        _check(lib().fvad_engine_create(C.byref(cfg), model.h, C.byref(h)), "fvad_engine_create")
+        self.h = h
+        self.B, self.C, self.nb = n_streams, n_channels, len(bands)
+
+    def _alloc_out(self, n_ticks, denoised):
+        T, B, Ch, nb = n_ticks, self.B, self.C, self.nb
+        o = {"vad": np.zeros((T, B), np.float32), "ratio": np.zeros((T, B), np.float32),
+             "win_flag": np.zeros((T, B), np.int32), "win_ratio": np.zeros((T, B), np.float32),
+             "win_vad": np.zeros((T, B), np.float32), "band": np.zeros((T, B, Ch, nb), np.float32)}
+        if denoised:
+            o["denoised"] = np.zeros((T, B, Ch, FRAME), np.float32)
+        s = Outputs(fptr(o["vad"]), fptr(o["ratio"]), o["win_flag"].ctypes.data_as(I32P), fptr(o["win_ratio"]),
+                    fptr(o["win_vad"]), fptr(o["band"]), fptr(o["denoised"]) if denoised else None)
+        return o, s
+
+    def push(self, pcm, ticks_valid=None, denoised=False):
+        """pcm: [ticks][streams][channels][480] normalised f32."""
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        T = pcm.shape[0]
+        assert pcm.shape[1:] == (self.B, self.C, FRAME), pcm.shape
+        o, s = self._alloc_out(T, denoised)
+        tv = None
+        if ticks_valid is not None:
+            tv = np.ascontiguousarray(ticks_valid, np.int32)
+        _check(lib().fvad_engine_push(self.h, fptr(pcm), T, tv.ctypes.data_as(I32P) if tv is not None else None,
+                                      C.byref(s)), "fvad_engine_push")
+        return o
+
+    def reset(self):
+        _check(lib().fvad_engine_reset(self.h), "fvad_engine_reset")
+
+    def load_synthetic(self, n_ticks, base=0):
+        _check(lib().fvad_engine_load_synthetic(self.h, n_ticks, base), "fvad_engine_load_synthetic")
+
+    def run_resident(self, n_ticks):
+        _check(lib().fvad_engine_run_resident(self.h, n_ticks), "fvad_engine_run_resident")
+
+    def sync(self):
+        _check(lib().fvad_engine_sync(self.h), "fvad_engine_sync")
+
+    def kernel_times(self):
+        ms = (C.c_double * 3)()
+        n = C.c_int()
+        _check(lib().fvad_engine_kernel_times(self.h, ms, C.byref(n)), "fvad_engine_kernel_times")
+        return {"prep_ms": ms[0], "frame_ms": ms[1], "total_ms": ms[2], "runs": n.value}
+
+    def clear_times(self):
+        _check(lib().fvad_engine_clear_times(self.h), "fvad_engine_clear_times")
+
+    def fetch(self, n_ticks, denoised=False):
+        o, s = self._alloc_out(n_ticks, denoised)
+        _check(lib().fvad_engine_fetch(self.h, n_ticks, C.byref(s)), "fvad_engine_fetch")
+        return o
+
+    def __del__(self):
+        try:
+            lib().fvad_engine_destroy(self.h)
+        except Exception:
+            pass
+
+
+class Denoiser:
+    """src/Denoiser.zig over the rnnoise_* C ABI (GPU, batch of one)."""
+
+    def __init__(self, model=None):
+        self.model = model
+        self.h = lib().rnnoise_create(model.h if model is not None else None)
+        if not self.h:
+            raise FvadError("rnnoise_create failed: %s" % last_error())
+
+    @staticmethod
+    def get_frame_size():
+        return lib().rnnoise_get_frame_size()
+
+    def process_s16(self, frame):
+        frame = np.ascontiguousarray(frame, np.float32)
+        if frame.shape != (FRAME,):
+            raise ValueError("InvalidFrameSize")
+        out = np.zeros(FRAME, np.float32)
+        vad = lib().rnnoise_process_frame(self.h, fptr(out), fptr(frame))
+        return out, vad
+
+    def denoise(self, samples):
+        """Denoiser.denoise: normalised [-1,1] in, normalised out, returns (out, vad)."""
+        samples = np.asarray(samples, np.float32)
+        if samples.shape != (FRAME,):
+            raise ValueError("InvalidFrameSize")
+        scaled = samples * np.float32(32767)
+        out, vad = self.process_s16(scaled)
+        return out * (np.float32(1.0) / np.float32(32767)), vad
+
+    def __del__(self):
+        try:
+            lib().rnnoise_destroy(self.h)
+        except Exception:
+            pass
+
+
+def kiss_fftr(x):
+    """kiss_fftr over the GPU compat shim; returns complex64[n/2+1]."""
+    x = np.ascontiguousarray(x, np.float32)
+    n = len(x)
+    lenmem = C.c_size_t(1)
+    if lib().kiss_fftr_alloc(n, 0, None, C.byref(lenmem)) is not None:
+        raise FvadError("size probe must fail")
+    if lenmem.value == 0:
+        raise ValueError("unsupported nfft %d" % n)
+    mem = C.create_string_buffer(lenmem.value)
+    cfg = lib().kiss_fftr_alloc(n, 0, mem, C.byref(lenmem))
+    if not cfg:
+        raise FvadError("kiss_fftr_alloc failed")
+    out = np.zeros(2 * (n // 2 + 1), np.float32)
+    lib().kiss_fftr(cfg, fptr(x), out.ctypes.data_as(C.c_void_p))
+    return out[0::2] + 1j * out[1::2]
+
+
+class AudioPipeline:
+    """src/AudioPipeline.zig for one stream (pushSamples -> VAD -> VADMachine)."""
+
+    def __init__(self, model, n_channels=2, sample_rate=48000, device=0, main_cfg=None, alt_cfgs=()):
+        self.model = model
+        main = main_cfg if main_cfg is not None else VadmConfig.default()
+        alts = (VadmConfig * max(1, len(alt_cfgs)))(*alt_cfgs) if alt_cfgs else None
+        self._keep = (main, alts)
+        self.n_alt = len(alt_cfgs)
+        h = C.c_void_p()
+        _check(lib().fvad_pipeline_create(sample_rate, n_channels, model.h, device, C.byref(main), alts,
+                                          self.n_alt, C.byref(h)), "fvad_pipeline_create")
+        self.h = h
+
+    def push_samples(self, channel_pcm):
+        chans = [np.ascontiguousarray(c, np.float32) for c in channel_pcm]
+        arr = (F32P * len(chans))(*[fptr(c) for c in chans])
+        first = C.c_uint64()
+        _check(lib().fvad_pipeline_push(self.h, arr, len(chans[0]), C.byref(first)), "fvad_pipeline_push")
+        return first.value
+
+    def segments(self, alt=-1):
+        n = lib().fvad_pipeline_segments(self.h, alt, None, 0)
+        buf = (Segment * max(1, n))()
+        lib().fvad_pipeline_segments(self.h, alt, buf, n)
+        return [(s.sample_from, s.sample_to, s.debug_rnn_vad, s.debug_avg_speech_vol_ratio) for s in buf[:n]]
+
+    def __del__(self):
+        try:
+            lib().fvad_pipeline_destroy(self.h)
+        except Exception:
+            pass
+
+
+class Multi:
+    """Multi-stream simulator core: lock-step ticks, streams partitioned over devices."""
+
+    def __init__(self, model, n_streams, n_channels=2, devices=(0,), cfg=None, ticks_per_push=50):
+        self.model = model
+        self.n = n_streams
+        d = np.ascontiguousarray(devices, np.int32)
+        c = cfg if cfg is not None else VadmConfig.default()
+        self._keep = (d, c)
+        h = C.c_void_p()
+        _check(lib().fvad_multi_create(n_streams, n_channels, model.h, d.ctypes.data_as(I32P), len(d), C.byref(c),
+                                       ticks_per_push, C.byref(h)), "fvad_multi_create")
+        self.h = h
+
+    def run(self, streams):
+        """streams: list of planar float32 arrays [ch][len]."""
+        arrs = [np.ascontiguousarray(s, np.float32) for s in streams]
+        ptrs = (F32P * len(arrs))(*[fptr(a) for a in arrs])
+        lens = (C.c_size_t * len(arrs))(*[a.shape[1] for a in arrs])
+        _check(lib().fvad_multi_run(self.h, ptrs, lens), "fvad_multi_run")
+
+    def segments(self, stream):
+        n = lib().fvad_multi_segments(self.h, stream, None, 0)
+        buf = (Segment * max(1, n))()
+        lib().fvad_multi_segments(self.h, stream, buf, n)
+        return [(s.sample_from, s.sample_to, s.debug_rnn_vad, s.debug_avg_speech_vol_ratio) for s in buf[:n]]
+
+    def __del__(self):
+        try:
+            lib().fvad_multi_destroy(self.h)
+        except Exception:
+            pass
+
+
+def evaluate(vad_segs, ref_segs, ignore_shorter_than_sec=0.0, extrude_start=0.0, extrude_end=0.0, fill_gaps=0.0):
+    v = np.ascontiguousarray(np.asarray(vad_segs, np.float32).reshape(-1, 2))
+    r = np.ascontiguousarray(np.asarray(ref_segs, np.float32).reshape(-1, 2))
+    cfg = StatConfig(ignore_shorter_than_sec, extrude_start, extrude_end, fill_gaps)
+    out = SingleStats()
+    _check(lib().fvad_eval_stats(fptr(v), len(v), fptr(r), len(r), C.byref(cfg), C.byref(out)), "fvad_eval_stats")
+    return {n: getattr(out, n) for n in _STAT_FIELDS}
+
+
+def aggregate(stats_list):
+    arr = (SingleStats * max(1, len(stats_list)))()
+    for i, s in enumerate(stats_list):
+        for n in _STAT_FIELDS:
+            setattr(arr[i], n, s[n])
+    out = AggregateStats()
+    lib().fvad_eval_aggregate(arr, len(stats_list), C.byref(out))
+    return out
+
+
+def parse_audacity(txt):
+    b = txt.encode() if isinstance(txt, str) else txt
+    n = lib().fvad_parse_audacity(b, len(b), None, 0)
+    if n < 0:
+        raise ValueError("malformed Audacity label text")
+    out = np.zeros(2 * max(1, n), np.float32)
+    lib().fvad_parse_audacity(b, len(b), fptr(out), n)
+    return out[: 2 * n].reshape(-1, 2)

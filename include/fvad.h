@@ -1,0 +1,232 @@
+/*
+ * fvad.h — C ABI of the MI355X-native Formula-VAD hot path (libfvad.so).
+ *
+ * Plain C types only (pointers, sizes, ints, floats): a Zig host can
+ * @cImport this header exactly as the reference @cImports rnnoise.h and
+ * kiss_fftr.h today (src/Denoiser.zig:12-14, src/FFT.zig:5-9).
+ *
+ * Three layers:
+ *   1. compatibility shims with the signatures and semantics the reference
+ *      binds today (rnnoise_*, kiss_fftr*) — batch-of-1 calls into the HIP
+ *      kernels;
+ *   2. the batched engine (fvad_engine_*): thousands of concurrent 48 kHz
+ *      streams per GPU, one tick = 480 samples per channel per stream;
+ *   3. the host mirror of the reference pipeline / evaluator API
+ *      (fvad_pipeline_*, fvad_vadm_*, fvad_eval_*), C++ above this ABI.
+ *
+ * Every entry point returns an int status (FVAD_OK = 0, negative = error)
+ * unless noted; fvad_last_error() gives the message of the last failure on the
+ * calling thread.  Ownership: the library owns device buffers and handles; the
+ * caller owns every host array it passes.
+ */
+#ifndef FVAD_H
+#define FVAD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FVAD_OK 0
+#define FVAD_EINVAL (-1)   /* invalid argument / size (Denoiser.zig:48-54, FFT.zig:29-31,71-81) */
+#define FVAD_EDEVICE (-2)  /* HIP runtime / device error, or no device */
+#define FVAD_ENOMEM (-3)   /* host or device allocation failed */
+#define FVAD_EIO (-4)      /* file could not be opened */
+#define FVAD_EFORMAT (-5)  /* malformed model / plan / label file */
+#define FVAD_ERATE (-6)    /* sample rate != 48000 (VAD.zig:101-104) */
+
+const char *fvad_last_error(void);
+const char *fvad_version(void);
+
+/* ------------------------------------------------------------------ */
+/* 1a. rnnoise compatibility (replaces lib/rnnoise as bound by          */
+/*     src/Denoiser.zig:12-14,23,36,60,69)                              */
+/* ------------------------------------------------------------------ */
+typedef struct fvad_model fvad_model;
+typedef struct DenoiseState DenoiseState;
+typedef struct fvad_model RNNModel;
+
+/* rnnoise_create(RNNModel *model) — Denoiser.zig:23.  model == NULL selects
+ * the process-wide default model (fvad_set_default_model, else the synthetic
+ * model with seed 0, since rnn_data.c is not available).  Returns NULL on
+ * failure (as upstream; Denoiser.zig:46 checks for it). */
+DenoiseState *rnnoise_create(RNNModel *model);
+/* rnnoise_destroy — Denoiser.zig:36 */
+void rnnoise_destroy(DenoiseState *st);
+/* rnnoise_process_frame — Denoiser.zig:60.  in/out: 480 floats in s16 scale;
+ * returns the VAD probability.  Runs the HIP frame kernel (batch of 1). */
+float rnnoise_process_frame(DenoiseState *st, float *out, const float *in);
+/* rnnoise_get_frame_size — Denoiser.zig:69 (returns 480) */
+int rnnoise_get_frame_size(void);
+void fvad_set_default_model(const fvad_model *model);
+
+/* ------------------------------------------------------------------ */
+/* 1b. kissfft compatibility (replaces lib/kissfft as bound by           */
+/*     src/FFT.zig:5-9,90,179-208)                                       */
+/* ------------------------------------------------------------------ */
+typedef struct { float r; float i; } kiss_fft_cpx;
+typedef struct kiss_fftr_state *kiss_fftr_cfg;
+/* kiss_fftr_alloc — FFT.zig:183,199.  Same lenmem protocol: with mem == NULL
+ * or *lenmem too small it returns NULL and writes the required size into
+ * *lenmem; otherwise the config lives in the caller's memory.  Forward only;
+ * nfft must be even and nfft/2 a power of 4 (the reference uses 2048). */
+kiss_fftr_cfg kiss_fftr_alloc(int nfft, int inverse_fft, void *mem, size_t *lenmem);
+/* kiss_fftr — FFT.zig:90.  timedata: nfft floats; freqdata: nfft/2+1 bins. */
+void kiss_fftr(kiss_fftr_cfg cfg, const float *timedata, kiss_fft_cpx *freqdata);
+
+/* ------------------------------------------------------------------ */
+/* Models (rnn_data.c / rnn_reader.c replacement)                       */
+/* ------------------------------------------------------------------ */
+int fvad_model_synthetic(uint64_t seed, fvad_model **out);
+int fvad_model_load_text(const char *path, fvad_model **out);
+void fvad_model_free(fvad_model *m);
+/* all int8 arrays in text-file order; returns the count (blob may be NULL) */
+size_t fvad_model_blob(const fvad_model *m, int8_t *blob);
+
+/* ------------------------------------------------------------------ */
+/* 2. Batched engine — the hot path                                     */
+/*    One engine = one GPU = a partition of streams.  A tick is 480      */
+/*    samples of every channel of every stream (VAD.zig:214-251 frame    */
+/*    loop, Denoiser per channel on one shared state VAD.zig:274-296,    */
+/*    480 -> fft_size re-blocking VAD.zig:298-348, FFT B + band sum      */
+/*    PipelineFFT.zig:88-112).                                            */
+/* ------------------------------------------------------------------ */
+typedef struct fvad_engine fvad_engine;
+
+#define FVAD_MAX_CHANNELS 8
+#define FVAD_MAX_BANDS 4
+
+typedef struct {
+  int n_streams;        /* streams in this engine's partition */
+  int n_channels;       /* channels per stream (2 = onboard stereo) */
+  int device;           /* HIP device ordinal */
+  int sample_rate;      /* must be 48000 */
+  int fft_size;         /* VAD.Config.fft_size: 2048 (or 512) */
+  int max_ticks;        /* largest n_ticks per push */
+  int n_bands;          /* band sums to report per window, 1..4 */
+  int band_lo[FVAD_MAX_BANDS]; /* inclusive FFT-B bin ranges (FFT.freqToBin) */
+  int band_hi[FVAD_MAX_BANDS];
+  int want_denoised;    /* keep denoised PCM (VAD.zig temp_denoiser_segment) */
+} fvad_engine_config;
+
+void fvad_engine_config_default(fvad_engine_config *cfg, int n_streams, int n_channels);
+
+int fvad_engine_create(const fvad_engine_config *cfg, const fvad_model *model, fvad_engine **out);
+void fvad_engine_destroy(fvad_engine *e);
+/* reset every stream to a freshly created rnnoise / VAD state */
+int fvad_engine_reset(fvad_engine *e);
+
+/* Per-tick outputs, host arrays owned by the caller, indexed [tick][stream]...
+ * Any pointer may be NULL to skip that output. */
+typedef struct {
+  float *vad;          /* [ticks][streams]  min over channels of rnnoise vad (VAD.zig:284-293) */
+  float *ratio;        /* [ticks][streams]  preAnalyzeSegment volume ratio (VAD.zig:253-272) */
+  int32_t *win_flag;   /* [ticks][streams]  1 if an FFT-B window completed in this tick */
+  float *win_ratio;    /* [ticks][streams]  share-weighted window volume ratio (VAD.zig:319-325) */
+  float *win_vad;      /* [ticks][streams]  window vad = last frame's vad (VAD.zig:330) */
+  float *band;         /* [ticks][streams][channels][n_bands] band sums (PipelineFFT.zig:99-112) */
+  float *denoised;     /* [ticks][streams][channels][480] normalised denoised PCM (want_denoised) */
+} fvad_outputs;
+
+/* pcm: host [ticks][streams][channels][480] normalised f32.  ticks_valid
+ * (nullable): stream s only consumes its first ticks_valid[s] ticks (ragged
+ * end of file; the rest of its slots are ignored).  Synchronous. */
+int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
+                     fvad_outputs *out);
+
+/* Device-resident variants for benchmarking / zero-copy producers. */
+/* allocate a device input of n_ticks and fill it with the synthetic generator */
+int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t stream_id_base);
+/* run one push over the resident device input, async on the engine stream */
+int fvad_engine_run_resident(fvad_engine *e, int n_ticks);
+int fvad_engine_sync(fvad_engine *e);
+/* average per-launch kernel durations (ms) of the last n resident runs,
+ * measured with HIP events on the engine's stream: [0] prep, [1] frame, [2] total */
+int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_runs);
+int fvad_engine_clear_times(fvad_engine *e);
+/* copy outputs of the last resident run to host */
+int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out);
+
+/* ------------------------------------------------------------------ */
+/* 3. Host mirror of the reference API (C++ above this ABI)             */
+/* ------------------------------------------------------------------ */
+/* VADMachine.Config (VADMachine.zig:18-39) */
+typedef struct {
+  float speech_min_freq, speech_max_freq;
+  float long_term_speech_avg_sec;
+  int has_initial_long_term_avg;
+  double initial_long_term_avg;
+  float short_term_speech_avg_sec;
+  float speech_threshold_factor;
+  float channel_vol_ratio_avg_sec;
+  float channel_vol_ratio_threshold;
+  float min_consecutive_sec_to_open;
+  float max_speech_gap_sec;
+  float min_vad_duration_sec;
+} fvad_vadm_config;
+void fvad_vadm_config_default(fvad_vadm_config *c);
+
+/* VAD.VADSpeechSegment (VAD.zig:25-30) */
+typedef struct {
+  uint64_t sample_from, sample_to;
+  float debug_rnn_vad, debug_avg_speech_vol_ratio;
+} fvad_segment;
+
+/* AudioPipeline (AudioPipeline.zig:20-26,39-120) for one stream, backed by a
+ * 1-stream engine.  n_alt alternative VADMachine configs (VAD.zig:20-23). */
+typedef struct fvad_pipeline fvad_pipeline;
+int fvad_pipeline_create(int sample_rate, int n_channels, const fvad_model *model, int device,
+                         const fvad_vadm_config *main_cfg, const fvad_vadm_config *alt_cfgs, int n_alt,
+                         fvad_pipeline **out);
+void fvad_pipeline_destroy(fvad_pipeline *p);
+/* pushSamples: planar channel pointers, n samples each; *first_index receives
+ * the absolute index of the first pushed sample (AudioPipeline.zig:86-120) */
+int fvad_pipeline_push(fvad_pipeline *p, const float *const *channel_pcm, size_t n, uint64_t *first_index);
+/* vad_segments of the main (alt < 0) or an alternative machine */
+size_t fvad_pipeline_segments(const fvad_pipeline *p, int alt, fvad_segment *out, size_t cap);
+
+/* Multi-stream simulator core: n streams processed in lockstep on the given
+ * devices (one engine per device, streams partitioned contiguously).
+ * pcm[s] points to planar [channels][len[s]] audio of stream s. */
+typedef struct fvad_multi fvad_multi;
+int fvad_multi_create(int n_streams, int n_channels, const fvad_model *model, const int *devices,
+                      int n_devices, const fvad_vadm_config *cfg, int ticks_per_push, fvad_multi **out);
+void fvad_multi_destroy(fvad_multi *m);
+int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size_t *len);
+size_t fvad_multi_segments(const fvad_multi *m, int stream, fvad_segment *out, size_t cap);
+
+/* Evaluator / statistics (Evaluator.zig:90-156, statistics.zig:85-284) */
+typedef struct {
+  float ignore_shorter_than_sec, extrude_start, extrude_end, fill_gaps;
+} fvad_stat_config;
+typedef struct {
+  float total_positives_sec, true_positives_sec, false_positives_sec, false_negatives_sec;
+  float true_positive_rate, false_negative_rate, false_discovery_rate, precision;
+  float fm_index, f_score, f_score_beta;
+} fvad_single_stats;
+typedef struct { float overall, min, max, avg; } fvad_agg_stat;
+typedef struct {
+  float total_positives_sec, true_positives_sec, false_positives_sec, false_negatives_sec;
+  fvad_agg_stat true_positive_rate, false_negative_rate, false_discovery_rate, precision;
+  float fm_index, f_score, f_score_beta;
+} fvad_aggregate_stats;
+/* segments as (from_sec, to_sec) pairs */
+int fvad_eval_stats(const float *vad_from_to, size_t n_vad, const float *ref_from_to, size_t n_ref,
+                    const fvad_stat_config *cfg, fvad_single_stats *out);
+void fvad_eval_aggregate(const fvad_single_stats *stats, size_t n, fvad_aggregate_stats *out);
+/* formats.parseAudacitySegments (formats.zig:7-36): returns count or <0 */
+long fvad_parse_audacity(const char *txt, size_t len, float *from_to, size_t cap);
+
+/* Synthetic 48 kHz onboard audio; returns label count */
+long fvad_synth_stream(uint32_t stream_id, size_t n, int n_channels, float *out, float *labels,
+                       size_t label_cap);
+
+/* simulator -i plan.json (simulator.zig:74-139) — returns process exit code */
+int fvad_simulator_main(int argc, char **argv);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

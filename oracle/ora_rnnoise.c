@@ -12,6 +12,7 @@
  * MAC16_16 = c + a*b, HALF32 = .5f*x, QCONST16(x,b) = x, celt_sqrt = (float)sqrt).
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include "oracle.h"
@@ -327,10 +328,11 @@ static void init_tansig(void) {
   int i;
   if (tansig_init) return;
   for (i = 0; i < 201; i++) {
-    /* %f formatting of tanh(.04 i) then parsed as a float literal */
-    double v = tanh(0.04 * i);
-    double r = floor(v * 1e6 + 0.5) / 1e6;
-    tansig_table[i] = (float)r;
+    /* the upstream table holds tanh(.04 i) printed "%f"; a float literal parses
+       to the nearest float of that decimal string */
+    char buf[64];
+    snprintf(buf, sizeof buf, "%f", tanh(0.04 * i));
+    tansig_table[i] = strtof(buf, NULL);
   }
   tansig_init = 1;
 }
