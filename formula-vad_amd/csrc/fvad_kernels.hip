@@ -82,38 +82,40 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
 // LDS layout (floats).  Work area doubles as the 960/1024-point complex FFT
 // buffer, the pitch-analysis scratch and the pitch spectrum P.
 namespace lds {
-constexpr int kPb = 0;                       // pitch_buf[1728]
-constexpr int kSyn = kPb + kPitchBuf;        // synthesis_mem[480]
-constexpr int kWork = kSyn + kFrame;         // 2048 floats (1024 complex)
-constexpr int kX = kWork + 2048;             // X[481] complex
-constexpr int kEx = kX + 2 * kFreq + 2;      // Ex[22]
+constexpr int kPb = 0;                                   // pitch_buf[1728]
+constexpr int kSyn = kPb + fvad::kPitchBuf;              // synthesis_mem[480]
+constexpr int kWork = kSyn + fvad::kFrame;               // 2048 floats (1024 complex)
+constexpr int kX = kWork + 2048;                         // X[481] complex
+constexpr int kEx = kX + 2 * fvad::kFreq + 2;            // Ex[22]
 constexpr int kEp = kEx + 24;
 constexpr int kExp = kEp + 24;
 constexpr int kLy = kExp + 24;
-constexpr int kFeat = kLy + 24;              // features[42]
-constexpr int kG = kFeat + 44;               // gains[22]
-constexpr int kR = kG + 24;                  // pitch-filter r[22]
+constexpr int kFeat = kLy + 24;                          // features[42]
+constexpr int kG = kFeat + 44;                           // gains[22]
+constexpr int kR = kG + 24;                              // pitch-filter r[22]
 constexpr int kNorm = kR + 24;
 constexpr int kNewE = kNorm + 24;
 constexpr int kLastG = kNewE + 24;
-constexpr int kCeps = kLastG + 24;           // cepstral_mem[8][22]
-constexpr int kGv = kCeps + kCeps * kBands;    // vad_gru_state[128]
+constexpr int kCepsMem = kLastG + 24;                    // cepstral_mem[8][22]
+constexpr int kGv = kCepsMem + fvad::kCeps * fvad::kBands;  // vad_gru_state[128]
 constexpr int kGn = kGv + 128;
 constexpr int kGd = kGn + 128;
-constexpr int kDout = kGd + 128;             // dense_out[128]
-constexpr int kRin = kDout + 128;            // concatenated GRU input[384]
-constexpr int kZr = kRin + 384;              // z,r gates[256]
-constexpr int kH = kZr + 256;                // h[128]
-constexpr int kMisc = kH + 128;              // float scratch[64]
-constexpr int kIMisc = kMisc + 64;           // int scratch[32]
-constexpr int kRd = kIMisc + 32;             // remove_doubling partials [64]
-constexpr int kMag = kRd + 64;               // FFT-B magnitudes of reported bins [256]
+constexpr int kDout = kGd + 128;                         // dense_out[128]
+constexpr int kRin = kDout + 128;                        // concatenated GRU input[384]
+constexpr int kZr = kRin + 384;                          // z,r gates[256]
+constexpr int kH = kZr + 256;                            // h[128]
+constexpr int kMisc = kH + 128;                          // float scratch[64]
+constexpr int kIMisc = kMisc + 64;                       // int scratch[32]
+constexpr int kRd = kIMisc + 32;                         // remove_doubling partials [64]
+constexpr int kMag = kRd + 64;                           // FFT-B magnitudes of reported bins [256]
 constexpr int kTotal = kMag + 256;
 // work-area sub-buffers during pitch analysis
-constexpr int kXlp = kWork;                  // raw x_lp[864]
-constexpr int kXf = kWork + kXlp;            // FIR-filtered x_lp[864]
-constexpr int kXc = kWork + 2 * kXlp;        // xcorr[294]
-constexpr int kYy = kWork;                   // yy_lookup[385] (reuses raw x_lp)
+constexpr int kXlpBuf = kWork;                           // raw x_lp[864]
+constexpr int kXf = kWork + fvad::kXlp;                  // FIR-filtered x_lp[864]
+constexpr int kXc = kWork + 2 * fvad::kXlp;              // xcorr[294]
+constexpr int kYy = kWork;                               // yy_lookup[385] (reuses raw x_lp)
+static_assert(kXc + 294 <= kWork + 2048, "pitch scratch exceeds the work area");
+static_assert(kTotal * 4 <= 32768, "LDS budget");
 }  // namespace lds
 
 // misc slots
@@ -392,14 +394,14 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
   float2 *X = reinterpret_cast<float2 *>(L + lds::kX);
   float *Ex = L + lds::kEx, *Ep = L + lds::kEp, *Exp = L + lds::kExp, *Ly = L + lds::kLy;
   float *feat = L + lds::kFeat, *g = L + lds::kG, *rr = L + lds::kR, *nrm = L + lds::kNorm;
-  float *newE = L + lds::kNewE, *lastg = L + lds::kLastG, *ceps = L + lds::kCeps;
+  float *newE = L + lds::kNewE, *lastg = L + lds::kLastG, *ceps = L + lds::kCepsMem;
   float *gv = L + lds::kGv, *gn = L + lds::kGn, *gd = L + lds::kGd;
   float *dout = L + lds::kDout, *rin = L + lds::kRin, *zr = L + lds::kZr, *hb = L + lds::kH;
   float *misc = L + lds::kMisc;
   int *im = reinterpret_cast<int *>(L + lds::kIMisc);
   float *rd = L + lds::kRd;
   float *mag = L + lds::kMag;
-  float *xlp = L + lds::kXlp, *xf = L + lds::kXf, *xc = L + lds::kXc, *yyl = L + lds::kYy;
+  float *xlp = L + lds::kXlpBuf, *xf = L + lds::kXf, *xc = L + lds::kXc, *yyl = L + lds::kYy;
 
   // ---- load persistent state into LDS
   for (int i = tid; i < kPitchBuf; i += NT) pb[i] = stp[st::kPitch + i];
@@ -1066,6 +1068,7 @@ size_t frame_lds_bytes() { return sizeof(float) * lds::kTotal; }
 
 hipError_t launch_prep(const PrepArgs &a, hipStream_t stream) {
   const int blocks = (a.n_streams + 63) / 64;
+  (void)hipGetLastError();
   hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(64), 0, stream, a);
   return hipGetLastError();
 }
@@ -1079,12 +1082,7 @@ hipError_t launch_kiss_fftr(int ncfft, int stages, const float *twb, const float
 }
 
 hipError_t launch_frame(const FrameArgs &a, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_frame<kFrameThreads>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)frame_lds_bytes());
-    attr_set = true;
-  }
+  (void)hipGetLastError();  // clear stale errors from earlier calls
   hipLaunchKernelGGL(k_frame<kFrameThreads>, dim3(a.n_streams), dim3(kFrameThreads), frame_lds_bytes(), stream, a);
   return hipGetLastError();
 }
