@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Bench: Formula-VAD per-frame hot path on MI355X.
+
+Metric (BASELINE.json): 48 kHz 480-sample VAD frames/sec whole node; max
+concurrent real-time streams.  A VAD frame = one 480-sample channel-frame
+through rnnoise (+ its share of the 2048-point band-energy FFT).
+
+Workload: configs[4]'s per-GPU partition — 2048 synthetic 48 kHz stereo
+streams per GPU (16384 at 8 GPUs), weak scaling, f32 exact numerics (fp32
+weights; the fp16 variant of configs[4] is not used).  A step = one push of
+TICKS ticks (480 samples per channel) for every stream of the partition:
+k_prep + k_frame on the engine's HIP stream, input resident in HBM.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each with its own
+stream partition; the only collectives are the barrier and the max-reduce of
+the timing (no data-path collective).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "formula-vad_amd"))
+
+METRIC = "48 kHz 480-sample VAD frames/sec whole node; max concurrent real-time streams"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector == FP32 MFMA peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--streams-per-gpu", type=int, default=2048)
+    ap.add_argument("--channels", type=int, default=2)
+    ap.add_argument("--ticks", type=int, default=50)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on this host (rank 0)")
+    ap.add_argument("--cpu-streams", type=int, default=256)
+    ap.add_argument("--cpu-ticks", type=int, default=200)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return rank, world, local, dist, torch
+    return rank, world, local, None, None
+
+
+def barrier(dist, torch):
+    if dist is not None:
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(x, dist, torch):
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(args):
+    """Oracle (C restatement, the CPU 'port') on this host's cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle
+    import fvad
+    oracle.build()
+    threads = min(16, os.cpu_count() or 1)
+    S, T, Ch = args.cpu_streams, args.cpu_ticks, args.channels
+    pcm = np.zeros((T, S, Ch, 480), np.float32)
+    for s in range(S):
+        x, _ = fvad.synth_stream(s, T * 480, Ch)
+        pcm[:, s] = (x * np.float32(32767)).reshape(Ch, T, 480).transpose(1, 0, 2)
+    om = oracle.Model(seed=1)
+    secs, _ = oracle.bench_denoise(om, pcm, n_threads=threads)
+    frames = S * T * Ch
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": frames / secs, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "%d synthetic stereo streams x %d ticks (%d channel-frames) through the oracle's rnnoise "
+                      "restatement, %d pthreads, %.1f s wall on %s (nproc %s)" % (
+                          S, T, frames, threads, secs, cpu_model, os.cpu_count())}
+
+
+def main():
+    args = parse()
+    rank, world, local, dist, torch = dist_setup(args.gpus)
+    import fvad
+    from fvad import cost
+
+    B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
+    model = fvad.Model(seed=1)
+    eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T)
+    eng.load_synthetic(T, base=rank * B)
+
+    for _ in range(args.warmup):
+        eng.run_resident(T)
+    eng.sync()
+    eng.clear_times()
+    barrier(dist, torch)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run_resident(T)
+    eng.sync()
+    barrier(dist, torch)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(elapsed, dist, torch)
+    kt = eng.kernel_times()
+
+    frames_per_step = B * Ch * T * world
+    value = frames_per_step * args.steps / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    # roofline of the dominant kernel (k_frame), per launch, measured with HIP events on the engine stream
+    flops_cf = cost.flops_per_channel_frame(Ch)
+    prep_share = cost.phases(Ch)["prep: s16 scale + HP biquad + rms"]
+    frame_flops = (flops_cf - prep_share) * B * Ch * T
+    frame_s = kt["frame_ms"] / 1000.0
+    achieved_tf = frame_flops / frame_s / 1e12
+    alg_bytes = cost.frame_kernel_bytes(B, Ch, T)
+    traffic = None
+    pmc_src = None
+    if os.path.exists(args.pmc_json):
+        try:
+            with open(args.pmc_json) as f:
+                pm = json.load(f)
+            if pm.get("streams") == B and pm.get("ticks") == T and pm.get("channels") == Ch:
+                traffic = pm.get("frame_bytes_per_launch")
+                pmc_src = os.path.relpath(args.pmc_json, ROOT)
+        except Exception:
+            traffic = None
+    roofline = {
+        "bound": "mfma",
+        "roof": "fp32 compute: v_mfma_f32 peak == fp32 VALU peak (157.3 TFLOP/s); the path runs on VALU",
+        "kernel": "k_frame",
+        "achieved": round(achieved_tf, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 5),
+        "traffic": traffic, "traffic_source": pmc_src,
+        "alg_flops_per_launch": frame_flops, "alg_bytes_per_launch": alg_bytes,
+        "kernel_ms_avg": round(kt["frame_ms"], 4), "prep_ms_avg": round(kt["prep_ms"], 4),
+        "hbm_achieved_gbs": round(alg_bytes / frame_s / 1e9, 2),
+        "hbm_frac": round(alg_bytes / frame_s / 1e9 / HBM_PEAK_GBS, 5),
+        "timed_launches": kt["runs"],
+    }
+    cpu = None
+    if args.cpu_baseline and world == 1:
+        try:
+            cpu = cpu_baseline(args)
+        except Exception as ex:  # never let the baseline leg kill the GPU measurement
+            cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port", "sample": "failed: %s" % ex}
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "configs[4] per-GPU partition: %d synthetic 48 kHz streams x %d ch per GPU "
+                               "(%d at %d GPU), %d ticks (480 samples/ch) per step, fp32 weights, bit-exact path"
+                               % (B, Ch, B * world, world, T),
+                   "streams_per_gpu": B, "channels": Ch, "ticks_per_step": T, "fft_size": 2048,
+                   "parallelism": "stream-partition x%d (no collectives)" % world},
+        "realtime_streams": round(value / (100.0 * Ch), 1),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

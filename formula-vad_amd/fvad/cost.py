@@ -1,0 +1,94 @@
+"""Algorithmic cost of one channel-frame (480 samples of one channel through
+rnnoise, plus its share of FFT B) — the unit of the bench metric.
+
+Counts follow the loop trip counts of the restated algorithm (SURVEY.md
+Appendix A / oracle/ora_rnnoise.c): every f32/f64 add, sub, mul, div and sqrt
+is one flop; table lookups, copies, compares and max/min are free.  Pitch
+candidate work uses its upper bound (10 fine-search lags, 14 remove_doubling
+candidates).  The per-phase breakdown is reproduced in DESIGN.md §Roofline.
+"""
+
+FRAME = 480
+
+
+def _fft960():
+    r4_degenerate = 240 * 16          # 16 adds per m=1 butterfly
+    r4_general = 2 * 240 * (3 * 6 + 16)  # 3 complex muls + 16 adds, two stages
+    r3 = 320 * 28
+    r5 = 192 * 72
+    return r4_degenerate + r4_general + r3 + r5  # 42944
+
+
+def _band_sum():
+    # per bin: |.|^2 or re/im product (3), weighted into two bands (2 mul, 2 add, 1 sub)
+    return 400 * 8
+
+
+def _fftb_per_window(nfft=2048, n_bins=61):
+    nc = nfft // 2
+    stages = 0
+    n = nc
+    while n > 1:
+        n //= 4
+        stages += 1
+    fft = stages * (nc // 4) * (3 * 6 + 16)
+    window = nfft
+    post = n_bins * (2 + 2 + 6 + 2 + 2)  # fpnk/f1k/f2k, super-twiddle cmul, halves
+    mag = n_bins * 4                     # r^2 + i^2, sqrt, norm
+    band = n_bins
+    return fft + window + post + mag + band
+
+
+def gru_flops(nin, nout):
+    macs = 3 * nout * (nin + nout)
+    extra = nout * nout            # (w*state)*r in the candidate gate
+    act = 3 * nout * 10 + nout * 4  # activations + state update
+    return 2 * macs + extra + act
+
+
+def phases(n_channels=2, fft_size=2048):
+    p = {}
+    p["prep: s16 scale + HP biquad + rms"] = FRAME * (1 + 1 + 3 + 4 + 2) + 2
+    p["analysis window + FFT A + scale"] = 960 + 1920 + _fft960()
+    p["band energy Ex"] = _band_sum()
+    p["pitch downsample + autocorr + LPC + FIR5"] = 864 * 4 + 5 * 864 * 2 + 60 + 864 * 10
+    p["coarse xcorr 147x240 + find_best_pitch"] = 147 * 240 * 2 + 240 * 2 + 147 * 8
+    p["fine xcorr <=10x480 + find_best_pitch"] = 10 * 480 * 2 + 480 * 2 + 294 * 8
+    p["remove_doubling"] = 480 * 4 + 480 * 2 + 384 * 4 + 14 * 480 * 4 + 3 * 480 * 2 + 14 * 12
+    p["pitch window + FFT + Ep + Exp"] = 960 + 1920 + _fft960() + 2 * _band_sum() + 22 * 5
+    p["features (log10, DCTs, cepstra, spectral variability)"] = 22 * 3 + 28 * 44 + 18 * 3 + 8 * 8 * 22 * 3 + 16
+    p["GRU stack"] = (2 * 42 * 24 + 24 * 10) + gru_flops(24, 24) + 2 * 24 + gru_flops(90, 48) + \
+        gru_flops(114, 96) + (2 * 96 * 22 + 22 * 12)
+    p["pitch filter + gains"] = 22 * 20 + 481 * 7 + _band_sum() + 22 * 6 + 481 * (2 * 3 + 4)
+    p["synthesis (scale, FFT A, window, OLA, 1/32767)"] = 1920 + _fft960() + 960 + 960 + 480 + 480
+    p["re-block + FFT B share"] = _fftb_per_window(fft_size) * FRAME / fft_size + 4
+    return p
+
+
+def flops_per_channel_frame(n_channels=2, fft_size=2048):
+    return sum(phases(n_channels, fft_size).values())
+
+
+def frame_kernel_bytes(n_streams, n_channels, n_ticks, n_bands=1, state_words=2816, live_state_words=2788,
+                       fft_size=2048):
+    """Algorithmic HBM bytes of one k_frame launch (T ticks of B streams)."""
+    B, C, T = n_streams, n_channels, n_ticks
+    frames = T * B * C
+    xbuf = frames * FRAME * 4
+    ratio = T * B * 4
+    state = 2 * B * live_state_words * 4
+    ring_w = frames * FRAME * 4
+    ring_r = frames * FRAME * 4  # every denoised sample is read once by FFT B
+    outs = T * B * (4 * 4 + C * n_bands * 4)
+    return xbuf + ratio + state + ring_w + ring_r + outs
+
+
+def prep_kernel_bytes(n_streams, n_channels, n_ticks):
+    frames = n_streams * n_channels * n_ticks
+    return frames * FRAME * 4 * 2 + n_streams * n_ticks * 4 + n_streams * 16
+
+
+if __name__ == "__main__":
+    for k, v in phases().items():
+        print("%-58s %9d" % (k, v))
+    print("%-58s %9d" % ("TOTAL flops / channel-frame", flops_per_channel_frame()))
