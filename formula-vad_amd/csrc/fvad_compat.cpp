@@ -122,7 +122,7 @@ extern "C" kiss_fftr_cfg kiss_fftr_alloc(int nfft, int inverse_fft, void *mem, s
     n /= 4;
     stages++;
   }
-  if (n != 1 || stages < 1 || ncfft > fvad::kMaxFftB / 2) {
+  if (n != 1 || stages < 1 || ncfft > 4096) {  // LDS holds ncfft complex (<= 32 KiB)
     if (lenmem) *lenmem = 0;
     return nullptr;  // device path: nfft/2 must be a power of 4
   }

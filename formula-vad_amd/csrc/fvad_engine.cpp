@@ -50,6 +50,7 @@ struct fvad_engine {
   fvad::Plan *d_plan = nullptr;
   float *d_weights = nullptr;
   fvad::DevModel dmodel{};
+  fvad::DevModel *d_model = nullptr;
   float *d_state = nullptr, *d_ring = nullptr;
   float *d_pcm = nullptr, *d_xbuf = nullptr, *d_ratio = nullptr;
   float *d_vad = nullptr, *d_wratio = nullptr, *d_wvad = nullptr, *d_band = nullptr, *d_den = nullptr;
@@ -60,7 +61,21 @@ struct fvad_engine {
   int n_timed = 0;
   bool timing_pending = false;
   int raw_s16 = 0;  // rnnoise compat mode (s16-scaled I/O)
+  unsigned long long *d_stamps = nullptr;  // diagnostic stamp buffer (FVAD_STAMPS builds)
 };
+
+// Diagnostic builds: per-phase cycle totals of k_frame (thread 0 of every workgroup).
+extern "C" int fvad_engine_stamps(fvad_engine *e, unsigned long long *out, int n) {
+  if (!e) return FVAD_EINVAL;
+  if (!e->d_stamps) {
+    HIP_TRY(hipMalloc(&e->d_stamps, 64 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(e->d_stamps, 0, 64 * sizeof(unsigned long long)));
+    return FVAD_OK;
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (out) HIP_TRY(hipMemcpy(out, e->d_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return FVAD_OK;
+}
 
 void fvad_engine_set_raw_s16(fvad_engine *e, int raw) { e->raw_s16 = raw; }
 
@@ -122,12 +137,15 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
   e->dmodel.den = gru(3);
   e->dmodel.den_out = dense(4);
   e->dmodel.vad_out = dense(5);
+  rc = dalloc(&e->d_model, 1);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(e->d_model, &e->dmodel, sizeof(fvad::DevModel), hipMemcpyHostToDevice));
   return FVAD_OK;
 }
 
 void free_all(fvad_engine *e) {
   void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm, e->d_xbuf, e->d_ratio, e->d_vad,
-                  e->d_wratio, e->d_wvad, e->d_band, e->d_den, e->d_wflag, e->d_ticks};
+                  e->d_wratio, e->d_wvad, e->d_band, e->d_den, e->d_wflag, e->d_ticks, e->d_model, e->d_stamps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &ev : e->ev)
@@ -236,7 +254,7 @@ int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   fa.ring = e->d_ring;
   fa.ring_len = e->ring_len;
   fa.plan = e->d_plan;
-  fa.model = e->dmodel;
+  fa.model = e->d_model;
   fa.n_bands = c.n_bands;
   int lo = 1 << 30, hi = -1;
   for (int b = 0; b < fvad::kMaxBandCfg; b++) {
@@ -256,6 +274,7 @@ int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   fa.out_den = e->d_den;
   fa.out_win_flag = e->d_wflag;
   fa.raw_s16 = e->raw_s16;
+  fa.stamps = e->d_stamps;
   if (timed) HIP_TRY(hipEventRecord(e->ev[0], e->stream));
   HIP_TRY(fvad::launch_prep(pa, e->stream));
   if (timed) HIP_TRY(hipEventRecord(e->ev[1], e->stream));

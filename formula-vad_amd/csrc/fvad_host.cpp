@@ -209,6 +209,44 @@ extern "C" void fvad_vadm_config_default(fvad_vadm_config *c) {
 }
 
 // ---------------------------------------------------------------------------
+// Standalone VADMachine (host decision logic; testable without a GPU)
+// ---------------------------------------------------------------------------
+struct fvad_vadm {
+  VADMachine m;
+  int n_channels;
+  fvad_vadm(const fvad_vadm_config &c, int sr, int fft, int ch) : m(c, sr, fft), n_channels(ch) {}
+};
+
+extern "C" int fvad_vadm_create(const fvad_vadm_config *cfg, int sample_rate, int fft_size, int n_channels,
+                                fvad_vadm **out) {
+  if (!out || n_channels < 1 || fft_size <= 0 || sample_rate <= 0) return FVAD_EINVAL;
+  fvad_vadm_config def;
+  fvad_vadm_config_default(&def);
+  *out = new fvad_vadm(cfg ? *cfg : def, sample_rate, fft_size, n_channels);
+  return FVAD_OK;
+}
+
+extern "C" void fvad_vadm_destroy(fvad_vadm *v) { delete v; }
+
+extern "C" void fvad_vadm_bins(const fvad_vadm *v, int *lo, int *hi) {
+  if (lo) *lo = (int)v->m.min_bin;
+  if (hi) *hi = (int)v->m.max_bin;
+}
+
+extern "C" int fvad_vadm_run(fvad_vadm *v, uint64_t index, const float *band_per_channel, float vad,
+                             float vol_ratio) {
+  if (!v || !band_per_channel) return FVAD_EINVAL;
+  v->m.run(index, band_per_channel, v->n_channels, 1, vad, vol_ratio);
+  return FVAD_OK;
+}
+
+extern "C" size_t fvad_vadm_segments(const fvad_vadm *v, fvad_segment *out, size_t cap) {
+  const auto &segs = v->m.segments;
+  for (size_t i = 0; i < segs.size() && i < cap; i++) out[i] = segs[i];
+  return segs.size();
+}
+
+// ---------------------------------------------------------------------------
 // Tick driver shared by the single-stream pipeline and the multi-stream core:
 // consumes engine outputs of n_ticks and feeds each stream's machines.
 // ---------------------------------------------------------------------------

@@ -25,13 +25,14 @@ struct FrameArgs {
   float *ring;  // [s][c][ring_len] denoised re-block ring
   int ring_len;
   const Plan *plan;
-  DevModel model;
+  const DevModel *model;  // device-resident layer descriptors
   int n_bands;
   int band_lo[kMaxBandCfg], band_hi[kMaxBandCfg];
   int bin_lo_all, bin_hi_all;
   float *out_vad, *out_win_ratio, *out_win_vad, *out_band, *out_den;
   int *out_win_flag;
   int raw_s16;  // rnnoise compat: emit s16-scaled output (no 1/32767)
+  unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS)
 };
 
 size_t frame_lds_bytes();

@@ -114,6 +114,8 @@ constexpr int kXlpBuf = kWork;                           // raw x_lp[864]
 constexpr int kXf = kWork + fvad::kXlp;                  // FIR-filtered x_lp[864]
 constexpr int kXc = kWork + 2 * fvad::kXlp;              // xcorr[294]
 constexpr int kYy = kWork;                               // yy_lookup[385] (reuses raw x_lp)
+constexpr int kSyyC = kWork;                             // coarse Syy sequence[147] (raw x_lp is dead)
+constexpr int kSyyF = kWork + 160;                       // fine Syy sequence[294]
 static_assert(kXc + 294 <= kWork + 2048, "pitch scratch exceeds the work area");
 static_assert(kTotal * 4 <= 32768, "LDS budget");
 }  // namespace lds
@@ -128,12 +130,32 @@ constexpr int kPg = 18;     // last_gain; [19] holds the tentative gain
 constexpr int kMind = 24;   // mindist[8]
 constexpr int kXc3 = 32;    // remove_doubling final xcorr[3]
 constexpr int kVadCh = 40;  // per-channel vad[8]
+constexpr int kFine = 48;   // fine-search xcorr of the 10 candidate lags
 }  // namespace ms
 namespace is {
-constexpr int kBest0 = 0, kBest1 = 1, kPitch = 2, kT0 = 3, kT = 4, kSilence = 5, kMemId = 6, kLastPeriod = 7;
+constexpr int kBest0 = 0, kBest1 = 1, kPitch = 2, kT0 = 3, kT = 4, kSilence = 5, kMemId = 6, kLastPeriod = 7,
+              kFineBase = 8;  // [8..17] candidate-lane valid flags
 }
 
 constexpr float kWs = 1.f / 256;  // WEIGHTS_SCALE
+
+// Diagnostic build only (-DFVAD_STAMPS): per-phase s_memtime accounting on
+// thread 0, written to a debug buffer that no other code reads.
+#ifdef FVAD_STAMPS
+#define STAMP(id)                                          \
+  do {                                                     \
+    if (tid == 0) {                                        \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+      stamp_acc[id] += t_ - stamp_last;                    \
+      stamp_last = t_;                                     \
+    }                                                      \
+  } while (0)
+#else
+#define STAMP(id) \
+  do {            \
+  } while (0)
+#endif
+constexpr int kStamps = 24;
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   float2 m;
@@ -269,6 +291,7 @@ __device__ void fft960_stages(float2 *W, const float2 *__restrict__ tw, int tid)
 __device__ __forceinline__ float band_sum(const float2 *A, const float2 *B, const Plan *__restrict__ P, int b) {
   float acc = 0;
   if (b >= 1) {
+#pragma unroll 4
     for (int k = P->eband4[b - 1]; k < P->eband4[b]; k++) {
       float tmp = A[k].x * B[k].x;
       tmp += A[k].y * B[k].y;
@@ -276,6 +299,7 @@ __device__ __forceinline__ float band_sum(const float2 *A, const float2 *B, cons
     }
   }
   if (b <= kBands - 2) {
+#pragma unroll 4
     for (int k = P->eband4[b]; k < P->eband4[b + 1]; k++) {
       float tmp = A[k].x * B[k].x;
       tmp += A[k].y * B[k].y;
@@ -294,39 +318,45 @@ __device__ __forceinline__ float interp_gain(const float *bandE, const Plan *__r
   return (1 - frac) * bandE[b] + frac * bandE[b + 1];
 }
 
-// find_best_pitch (pitch.c), one lane.  y indexed with stride ys.
-__device__ void find_best_pitch(const float *xcorr, const float *y, int ys, int len, int max_pitch, int *best) {
+// find_best_pitch (pitch.c) split in two: the Syy energy recurrence depends
+// only on y, so syy_sequence() produces the value Syy holds at every lag i
+// (before its update), and best_pitch_visit() replays the selection for one
+// lag.  Visiting the lags in increasing order reproduces find_best_pitch
+// exactly; lags with xcorr <= 0 only advance Syy and may be skipped.
+__device__ void syy_sequence(const float *y, int ys, int len, int max_pitch, float *syy) {
   float Syy = 1;
-  float best_num0 = -1, best_num1 = -1, best_den0 = 0, best_den1 = 0;
-  int b0 = 0, b1 = 1;
+#pragma unroll 8
   for (int j = 0; j < len; j++) Syy = Syy + y[j * ys] * y[j * ys];
+#pragma unroll 4
   for (int i = 0; i < max_pitch; i++) {
-    const float xc = xcorr[i];
-    if (xc > 0) {
-      float xcorr16 = xc;
-      xcorr16 *= 1e-12f;
-      const float num = xcorr16 * xcorr16;
-      if (num * best_den1 > best_num1 * Syy) {
-        if (num * best_den0 > best_num0 * Syy) {
-          best_num1 = best_num0;
-          best_den1 = best_den0;
-          b1 = b0;
-          best_num0 = num;
-          best_den0 = Syy;
-          b0 = i;
-        } else {
-          best_num1 = num;
-          best_den1 = Syy;
-          b1 = i;
-        }
-      }
-    }
+    syy[i] = Syy;
     const float ya = y[(i + len) * ys], yb = y[i * ys];
     Syy += ya * ya - yb * yb;
     Syy = (1 > Syy) ? 1 : Syy;
   }
-  best[0] = b0;
-  best[1] = b1;
+}
+
+__device__ __forceinline__ void best_pitch_visit(float xc, float Syy, int i, float &bn0, float &bn1, float &bd0,
+                                                 float &bd1, int *best) {
+  if (xc > 0) {
+    float xcorr16 = xc;
+    xcorr16 *= 1e-12f;
+    const float num = xcorr16 * xcorr16;
+    if (num * bd1 > bn1 * Syy) {
+      if (num * bd0 > bn0 * Syy) {
+        bn1 = bn0;
+        bd1 = bd0;
+        best[1] = best[0];
+        bn0 = num;
+        bd0 = Syy;
+        best[0] = i;
+      } else {
+        bn1 = num;
+        bd1 = Syy;
+        best[1] = i;
+      }
+    }
+  }
 }
 
 __device__ __forceinline__ float pitch_gain(float xy, float xx, float yy) { return xy / sqrtf(1 + xx * yy); }
@@ -337,6 +367,7 @@ template <int NT>
 __device__ void dense_layer(const DevDense &d, const float *in, float *out, const float *tansig_tab, int tid) {
   for (int i = tid; i < d.nout; i += NT) {
     float sum = d.b[i];
+#pragma unroll 8
     for (int j = 0; j < d.nin; j++) sum += d.w[j * d.nout + i] * in[j];
     out[i] = activate(tansig_tab, d.act, kWs * sum);
   }
@@ -351,7 +382,9 @@ __device__ void gru_gates(const DevGru &g, const float *in, const float *state, 
   for (int t = tid; t < 2 * N; t += NT) {
     const int col = t;  // z: col = i, r: col = N + i
     float sum = g.b[col];
+#pragma unroll 8
     for (int j = 0; j < M; j++) sum += g.win[j * S3 + col] * in[j];
+#pragma unroll 8
     for (int j = 0; j < N; j++) sum += g.wrec[j * S3 + col] * state[j];
     zr[t] = sigmoid(tab, kWs * sum);
   }
@@ -362,7 +395,9 @@ __device__ void gru_out(const DevGru &g, const float *in, const float *state, co
   const int N = g.nout, M = g.nin, S3 = 3 * N;
   for (int i = tid; i < N; i += NT) {
     float sum = g.b[2 * N + i];
+#pragma unroll 8
     for (int j = 0; j < M; j++) sum += g.win[j * S3 + 2 * N + i] * in[j];
+#pragma unroll 8
     for (int j = 0; j < N; j++) sum += g.wrec[j * S3 + 2 * N + i] * state[j] * zr[N + j];
     sum = activate(tab, g.act, kWs * sum);
     h[i] = zr[i] * state[i] + (1 - zr[i]) * sum;
@@ -380,11 +415,16 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
   if (s >= a.n_streams) return;
   const int nt = a.ticks_valid ? a.ticks_valid[s] : a.n_ticks;
   if (nt <= 0) return;
+#ifdef FVAD_STAMPS
+  unsigned long long stamp_acc[kStamps];
+  for (int i = 0; i < kStamps; i++) stamp_acc[i] = 0;
+  unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
+#endif
   const Plan *__restrict__ P = a.plan;
   const float2 *__restrict__ tw = reinterpret_cast<const float2 *>(P->tw960);
   const float *__restrict__ hw = P->half_window;
   const float *__restrict__ tt = P->tansig;
-  const DevModel &M = a.model;
+  const DevModel &M = *a.model;
   const int C = a.n_channels;
   float *stp = a.state + (size_t)s * st::kWords;
   int *istp = reinterpret_cast<int *>(stp);
@@ -423,6 +463,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
   const float scale = 1.f / 960;
   const int FB = P->nfft_b, ring_len = a.ring_len;
   __syncthreads();
+      STAMP(0);
 
   for (int t = 0; t < nt; t++) {
     for (int c = 0; c < C; c++) {
@@ -444,6 +485,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         for (int i = tid; i < kFrame; i += NT) pb[kPitchBuf - kFrame + i] = xin[i];
       }
       __syncthreads();
+      STAMP(1);
       // ---- frame_analysis: [analysis_mem | x] = pb[768..1728), window, FFT, Ex
       for (int i = tid; i < kWin; i += NT) {
         float v = pb[kPitchBuf - kWin + i];
@@ -452,25 +494,30 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         W[d] = make_float2(scale * v, scale * 0.0f);
       }
       __syncthreads();
+      STAMP(1);
       fft960_stages<NT>(W, tw, tid);
       for (int k = tid; k < kFreq; k += NT) X[k] = W[k];
       __syncthreads();
+      STAMP(2);
       if (tid < kBands) Ex[tid] = band_sum(X, X, P, tid);
       // ---- pitch_downsample: x_lp, autocorr, LPC, FIR5
       for (int i = tid; i < kXlp; i += NT) {
         xlp[i] = (i == 0) ? .5f * (.5f * (pb[1]) + pb[0]) : .5f * (.5f * (pb[2 * i - 1] + pb[2 * i + 1]) + pb[2 * i]);
       }
       __syncthreads();
+      STAMP(3);
       if (tid < 5) {
         const int k = tid;
         const int fastN = kXlp - 4;
         float acc = 0;
+#pragma unroll 8
         for (int i = 0; i < fastN; i++) acc = acc + xlp[i] * xlp[i + k];
         float d = 0;
         for (int i = k + fastN; i < kXlp; i++) d = d + xlp[i] * xlp[i - k];
         misc[ms::kAc + k] = acc + d;
       }
       __syncthreads();
+      STAMP(4);
       if (tid == 0) {
         float ac[5];
         for (int i = 0; i < 5; i++) ac[i] = misc[ms::kAc + i];
@@ -507,6 +554,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         misc[ms::kLpc2 + 4] = c1 * lpc[3];
       }
       __syncthreads();
+      STAMP(5);
       {
         const float n0 = misc[ms::kLpc2 + 0], n1 = misc[ms::kLpc2 + 1], n2 = misc[ms::kLpc2 + 2],
                     n3 = misc[ms::kLpc2 + 3], n4 = misc[ms::kLpc2 + 4];
@@ -524,32 +572,79 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         }
       }
       __syncthreads();
-      // ---- pitch_search: coarse xcorr (4x decimation) on 147 lanes
+      STAMP(6);
+      // ---- pitch_search: coarse xcorr (4x decimation) on 147 lanes.  The
+      //      find_best_pitch energy recurrences (Syy) depend only on y, so
+      //      two more lanes produce the per-lag Syy sequences meanwhile.
       const float *xl = xf + (kPitchMax >> 1);  // x_lp = pitch_buf_lp + 384
-      for (int k = tid; k < 147; k += NT) {
+      float *syy_c = L + lds::kSyyC, *syy_f = L + lds::kSyyF;
+      if (tid < 147) {
+        const int k = tid;
         float acc = 0;
+#pragma unroll 8
         for (int j = 0; j < 240; j++) acc = acc + xl[2 * j] * xf[2 * (j + k)];
         xc[k] = acc;
+      } else if (tid == 160) {
+        syy_sequence(xf, 2, 240, 147, syy_c);
+      } else if (tid == 192) {
+        syy_sequence(xf, 1, 480, 294, syy_f);
       }
       __syncthreads();
-      if (tid == 0) find_best_pitch(xc, xf, 2, 240, 147, &im[is::kBest0]);
+      STAMP(7);
+      if (tid == 0) {
+        int best[2] = {0, 1};
+        float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
+#pragma unroll 4
+        for (int i = 0; i < 147; i++) best_pitch_visit(xc[i], syy_c[i], i, bn0, bn1, bd0, bd1, best);
+        im[is::kBest0] = best[0];
+        im[is::kBest1] = best[1];
+      }
       __syncthreads();
+      STAMP(8);
       {
+        // fine search: only lags within +-2 of 2*best[0] or 2*best[1] are non-zero
         const int bp0 = im[is::kBest0], bp1 = im[is::kBest1];
-        for (int i = tid; i < 294; i += NT) {
-          float v = 0;
-          if (!(abs(i - 2 * bp0) > 2 && abs(i - 2 * bp1) > 2)) {
+        for (int i = tid; i < 294; i += NT) xc[i] = 0;
+        const int lane = tid;
+        if (lane < 10) {
+          const int i = (lane < 5 ? 2 * bp0 : 2 * bp1) - 2 + (lane % 5);
+          const bool dup = lane >= 5 && abs(i - 2 * bp0) <= 2;  // also in the first window
+          if (i >= 0 && i < 294 && !dup) {
             float sum = 0;
+#pragma unroll 8
             for (int j = 0; j < 480; j++) sum = sum + xl[j] * xf[i + j];
-            v = (-1 > sum) ? -1 : sum;
+            im[is::kFineBase + lane] = 1;
+            misc[ms::kFine + lane] = (-1 > sum) ? -1 : sum;
+          } else {
+            im[is::kFineBase + lane] = 0;
           }
-          xc[i] = v;
         }
       }
       __syncthreads();
+      STAMP(9);
+      if (tid < 10 && im[is::kFineBase + tid]) {
+        const int bp0 = im[is::kBest0], bp1 = im[is::kBest1];
+        const int i = (tid < 5 ? 2 * bp0 : 2 * bp1) - 2 + (tid % 5);
+        xc[i] = misc[ms::kFine + tid];
+      }
+      __syncthreads();
       if (tid == 0) {
-        int best[2];
-        find_best_pitch(xc, xf, 1, 480, 294, best);
+        const int bp0 = im[is::kBest0], bp1 = im[is::kBest1];
+        int best[2] = {0, 1};
+        float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
+        // visit the union of the two candidate windows in increasing lag order
+        int w0lo = 2 * bp0 - 2, w0hi = 2 * bp0 + 2, w1lo = 2 * bp1 - 2, w1hi = 2 * bp1 + 2;
+        if (w1lo < w0lo) {
+          int t0 = w0lo, t1 = w0hi;
+          w0lo = w1lo;
+          w0hi = w1hi;
+          w1lo = t0;
+          w1hi = t1;
+        }
+        for (int i = max(0, w0lo); i <= min(293, w0hi); i++)
+          best_pitch_visit(xc[i], syy_f[i], i, bn0, bn1, bd0, bd1, best);
+        for (int i = max(max(0, w1lo), w0hi + 1); i <= min(293, w1hi); i++)
+          best_pitch_visit(xc[i], syy_f[i], i, bn0, bn1, bd0, bd1, best);
         int offset;
         if (best[0] > 0 && best[0] < 294 - 1) {
           const float aa = xc[best[0] - 1], bb = xc[best[0]], cc = xc[best[0] + 1];
@@ -568,6 +663,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         im[is::kT0] = T0;
       }
       __syncthreads();
+      STAMP(10);
       // ---- remove_doubling: independent inner products in parallel
       //   lane 0: xx, xy(T0); lane 1: xx then yy_lookup chain; lanes 2..15: k candidates
       {
@@ -575,6 +671,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         const int T0 = im[is::kT0];
         if (tid == 0) {
           float xx = 0, xy = 0;
+#pragma unroll 8
           for (int i = 0; i < 480; i++) {
             xx = xx + x[i] * x[i];
             xy = xy + x[i] * x[i - T0];
@@ -583,9 +680,11 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
           misc[ms::kXy] = xy;
         } else if (tid == 1) {
           float xx = 0;
+#pragma unroll 8
           for (int i = 0; i < 480; i++) xx = xx + x[i] * x[i];
           float yy = xx;
           yyl[0] = xx;
+#pragma unroll 8
           for (int i = 1; i <= 384; i++) {
             yy = yy + x[-i] * x[-i] - x[480 - i] * x[480 - i];
             yyl[i] = (0 > yy) ? 0 : yy;
@@ -600,6 +699,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
             else
               T1b = (int)((unsigned)(2 * c_second_check[k] * T0 + k) / (unsigned)(2 * k));
             float s1 = 0, s2 = 0;
+#pragma unroll 8
             for (int i = 0; i < 480; i++) {
               s1 = s1 + x[i] * x[i - T1];
               s2 = s2 + x[i] * x[i - T1b];
@@ -610,6 +710,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         }
       }
       __syncthreads();
+      STAMP(11);
       if (tid == 0) {
         const int T0 = im[is::kT0];
         const int prev_period = im[is::kLastPeriod] / 2;
@@ -669,10 +770,12 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         misc[ms::kPg + 1] = pg;  // tentative gain (final after offset)
       }
       __syncthreads();
+      STAMP(12);
       if (tid < 3) {
         const float *x = xl;
         const int T = im[is::kT];
         float acc = 0;
+#pragma unroll 8
         for (int i = 0; i < 480; i++) acc = acc + x[i] * x[i - (T + tid - 1)];
         misc[ms::kXc3 + tid] = acc;
       }
@@ -693,6 +796,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         misc[ms::kPg] = misc[ms::kPg + 1];  // last_gain
       }
       __syncthreads();
+      STAMP(13);
       // ---- pitch spectrum P (in W), Ep, Exp
       {
         const int pitch = im[is::kPitch];
@@ -709,6 +813,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
       else if (tid >= 32 && tid < 32 + kBands)
         Exp[tid - 32] = band_sum(X, W, P, tid - 32);
       __syncthreads();
+      STAMP(14);
       if (tid < kBands) {
         Exp[tid] = (float)((double)Exp[tid] / sqrt(.001 + (double)(Ex[tid] * Ep[tid])));
         Ly[tid] = (float)log10(1e-2 + (double)Ex[tid]);
@@ -716,6 +821,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
       __syncthreads();
       if (tid < 6) {  // dct(tmp, Exp) -> features[34..39]
         float sum = 0;
+#pragma unroll
         for (int j = 0; j < kBands; j++) sum += Exp[j] * P->dct[j * kBands + tid];
         float v = (float)(sum * sqrt(2. / 22));
         if (tid == 0) v = (float)(v - 1.3);
@@ -737,12 +843,14 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         im[is::kSilence] = ((double)E < 0.04) ? 1 : 0;
       }
       __syncthreads();
+      STAMP(15);
       const bool silence = im[is::kSilence] != 0;
       if (!silence) {
         // ---- features: DCT(Ly), cepstral memory, deltas, spectral variability
         const int memid = im[is::kMemId];
         if (tid < kBands) {
           float sum = 0;
+#pragma unroll
           for (int j = 0; j < kBands; j++) sum += Ly[j] * P->dct[j * kBands + tid];
           float v = (float)(sum * sqrt(2. / 22));
           if (tid == 0) v -= 12;
@@ -766,6 +874,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
           float mindist = 1e15f;
           for (int j = 0; j < kCeps; j++) {
             float dist = 0;
+#pragma unroll
             for (int k = 0; k < kBands; k++) {
               const float tmp = ceps[i * kBands + k] - ceps[j * kBands + k];
               dist += tmp * tmp;
@@ -784,6 +893,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
           im[is::kMemId] = mid;
         }
         __syncthreads();
+      STAMP(16);
         // ---- compute_rnn
         dense_layer<NT>(M.in_dense, feat, dout, tt, tid);
         __syncthreads();
@@ -791,6 +901,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         __syncthreads();
         gru_out<NT>(M.vad, dout, gv, zr, hb, tt, tid);
         __syncthreads();
+      STAMP(17);
         {
           const int nd = M.in_dense.nout, nv = M.vad.nout;
           for (int i = tid; i < nv; i += NT) gv[i] = hb[i];
@@ -810,6 +921,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         __syncthreads();
         gru_out<NT>(M.noise, rin, gn, zr, hb, tt, tid);
         __syncthreads();
+      STAMP(18);
         {
           const int nv = M.vad.nout, nn = M.noise.nout;
           for (int i = tid; i < nn; i += NT) gn[i] = hb[i];
@@ -826,6 +938,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         __syncthreads();
         dense_layer<NT>(M.den_out, gd, g, tt, tid);
         __syncthreads();
+      STAMP(19);
         // ---- pitch_filter
         if (tid < kBands) {
           const int i = tid;
@@ -870,6 +983,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
           X[k] = v;
         }
         __syncthreads();
+      STAMP(20);
       } else {
         if (tid == 0) misc[ms::kVadCh + c] = 0;
       }
@@ -902,6 +1016,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         }
       }
       __syncthreads();
+      STAMP(21);
     }  // channels
     // ---- per tick: vad_low, re-blocking, window completion (VAD.zig:284-348)
     {
@@ -993,6 +1108,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
       }
       frames_done++;
     }
+      STAMP(22);
   }  // ticks
 
   // ---- store persistent state
@@ -1013,6 +1129,11 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
     istp[st::kFramesDone] = frames_done;
     stp[st::kVolAcc] = vol_acc;
   }
+#ifdef FVAD_STAMPS
+  STAMP(23);
+  if (tid == 0 && a.stamps)
+    for (int i = 0; i < kStamps; i++) atomicAdd(&a.stamps[i], stamp_acc[i]);
+#endif
 }
 
 // ---------------------------------------------------------------------------

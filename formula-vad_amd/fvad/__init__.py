@@ -18,7 +18,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfvad.so")
+LIB_PATH = os.environ.get("FVAD_LIB", os.path.join(PKG_ROOT, "lib", "libfvad.so"))
 
 FVAD_OK = 0
 F32P = C.POINTER(C.c_float)
@@ -119,6 +119,11 @@ SYMBOLS = [
     ("fvad_engine_clear_times", C.c_int, [C.c_void_p]),
     ("fvad_engine_fetch", C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     ("fvad_vadm_config_default", None, [C.c_void_p]),
+    ("fvad_vadm_create", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    ("fvad_vadm_destroy", None, [C.c_void_p]),
+    ("fvad_vadm_bins", None, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("fvad_vadm_run", C.c_int, [C.c_void_p, C.c_uint64, F32P, C.c_float, C.c_float]),
+    ("fvad_vadm_segments", C.c_size_t, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("fvad_pipeline_create", C.c_int, [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                        C.POINTER(C.c_void_p)]),
     ("fvad_pipeline_destroy", None, [C.c_void_p]),
@@ -329,6 +334,39 @@ def kiss_fftr(x):
     out = np.zeros(2 * (n // 2 + 1), np.float32)
     lib().kiss_fftr(cfg, fptr(x), out.ctypes.data_as(C.c_void_p))
     return out[0::2] + 1j * out[1::2]
+
+
+class VADMachine:
+    """src/AudioPipeline/VADMachine.zig (host decision logic)."""
+
+    def __init__(self, cfg=None, n_channels=2, sample_rate=48000, fft_size=2048):
+        c = cfg if cfg is not None else VadmConfig.default()
+        self._cfg = c
+        self.n_channels = n_channels
+        h = C.c_void_p()
+        _check(lib().fvad_vadm_create(C.byref(c), sample_rate, fft_size, n_channels, C.byref(h)), "fvad_vadm_create")
+        self.h = h
+
+    def bins(self):
+        lo, hi = C.c_int(), C.c_int()
+        lib().fvad_vadm_bins(self.h, C.byref(lo), C.byref(hi))
+        return lo.value, hi.value
+
+    def run(self, index, band_per_channel, vad, vol_ratio):
+        b = np.ascontiguousarray(band_per_channel, np.float32)
+        _check(lib().fvad_vadm_run(self.h, index, fptr(b), vad, vol_ratio), "fvad_vadm_run")
+
+    def segments(self):
+        n = lib().fvad_vadm_segments(self.h, None, 0)
+        buf = (Segment * max(1, n))()
+        lib().fvad_vadm_segments(self.h, buf, n)
+        return [(s.sample_from, s.sample_to, s.debug_rnn_vad, s.debug_avg_speech_vol_ratio) for s in buf[:n]]
+
+    def __del__(self):
+        try:
+            lib().fvad_vadm_destroy(self.h)
+        except Exception:
+            pass
 
 
 class AudioPipeline:

@@ -174,6 +174,17 @@ typedef struct {
   float debug_rnn_vad, debug_avg_speech_vol_ratio;
 } fvad_segment;
 
+/* VADMachine (VADMachine.zig:65-310) on its own: feed it one FFT-B window at a
+ * time (absolute sample index of the window start, the per-channel band sums
+ * of its speech band, the window's vad and volume ratio). */
+typedef struct fvad_vadm fvad_vadm;
+int fvad_vadm_create(const fvad_vadm_config *cfg, int sample_rate, int fft_size, int n_channels, fvad_vadm **out);
+void fvad_vadm_destroy(fvad_vadm *v);
+/* speech band as FFT-B bins (FFT.freqToBin of speech_min/max_freq) */
+void fvad_vadm_bins(const fvad_vadm *v, int *lo, int *hi);
+int fvad_vadm_run(fvad_vadm *v, uint64_t index, const float *band_per_channel, float vad, float vol_ratio);
+size_t fvad_vadm_segments(const fvad_vadm *v, fvad_segment *out, size_t cap);
+
 /* AudioPipeline (AudioPipeline.zig:20-26,39-120) for one stream, backed by a
  * 1-stream engine.  n_alt alternative VADMachine configs (VAD.zig:20-23). */
 typedef struct fvad_pipeline fvad_pipeline;

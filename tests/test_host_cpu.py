@@ -1,0 +1,124 @@
+"""Product host-side logic vs the oracle, and the C-ABI surface — CPU only
+(no compute call needs a GPU here)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_abi_exports_every_declared_symbol(fvad_mod):
+    """libfvad.so loads and exports every function include/fvad.h declares."""
+    hdr = open(os.path.join(ROOT, "include", "fvad.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    hdr = "\n".join(l for l in hdr.split("\n") if not l.lstrip().startswith("#"))
+    names = set(re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", hdr))
+    names -= {"sizeof"}
+    assert len(names) >= 40
+    L = fvad_mod.lib()
+    missing = [n for n in sorted(names) if not hasattr(L, n)]
+    assert not missing, missing
+    bound = {s[0] for s in fvad_mod.SYMBOLS}
+    assert names <= bound, sorted(names - bound)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 1234, 2 ** 40 + 7])
+def test_synthetic_model_identical_to_oracle(fvad_mod, oracle_mod, seed):
+    assert np.array_equal(fvad_mod.Model(seed=seed).blob(), oracle_mod.Model(seed=seed).blob())
+
+
+def test_text_model_loader(fvad_mod, oracle_mod, tmp_path):
+    from test_oracle_kats import write_text_model
+    blob = oracle_mod.Model(seed=5).blob()
+    p = tmp_path / "m.txt"
+    write_text_model(blob, p)
+    assert np.array_equal(fvad_mod.Model(path=str(p)).blob(), blob)
+    bad = tmp_path / "bad.txt"
+    bad.write_text("rnnoise-nu model file version 2\n")
+    with pytest.raises(fvad_mod.FvadError):
+        fvad_mod.Model(path=str(bad))
+
+
+def test_synth_deterministic(fvad_mod):
+    a, la = fvad_mod.synth_stream(7, 48000 * 3, 2)
+    b, lb = fvad_mod.synth_stream(7, 48000 * 3, 2)
+    c, _ = fvad_mod.synth_stream(8, 48000 * 3, 2)
+    assert np.array_equal(a, b) and np.array_equal(la, lb)
+    assert not np.array_equal(a, c)
+    assert np.abs(a).max() <= 1.0
+    s, _ = fvad_mod.synth_stream(19, 48000 * 7, 2)  # every 20th stream: 1 s of digital silence at 5 s
+    assert not np.any(s[:, 5 * 48000:6 * 48000])
+
+
+def random_segments(rng, n, t_max=120.0):
+    starts = np.sort(rng.uniform(0, t_max, n))
+    return [(float(s), float(s + rng.uniform(0.2, 8))) for s in starts]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_evaluator_matches_oracle(fvad_mod, oracle_mod, seed):
+    rng = np.random.default_rng(seed)
+    vad = random_segments(rng, rng.integers(0, 25))
+    ref = random_segments(rng, rng.integers(1, 25))
+    for cfg in [dict(ignore_shorter_than_sec=0.7), dict(ignore_shorter_than_sec=0.7, extrude_start=5, extrude_end=10,
+                                                         fill_gaps=5)]:
+        a = fvad_mod.evaluate(vad, ref, **cfg)
+        b = oracle_mod.evaluate(vad, ref, **cfg)
+        for k in a:
+            assert (np.isnan(a[k]) and np.isnan(b[k])) or a[k] == b[k], (k, a[k], b[k])
+
+
+def test_aggregate_matches_oracle(fvad_mod, oracle_mod):
+    rng = np.random.default_rng(11)
+    stats = [oracle_mod.evaluate(random_segments(rng, 10), random_segments(rng, 10), 0.7, 5, 10, 5)
+             for _ in range(5)]
+    a = fvad_mod.aggregate(stats)
+    b = oracle_mod.aggregate(stats)
+    for name in ("total_positives_sec", "true_positives_sec", "false_positives_sec", "false_negatives_sec",
+                 "fm_index", "f_score"):
+        assert getattr(a, name) == getattr(b, name)
+    for name in ("true_positive_rate", "false_negative_rate", "false_discovery_rate", "precision"):
+        for f in ("overall", "min", "max", "avg"):
+            assert getattr(getattr(a, name), f) == getattr(getattr(b, name), f)
+
+
+def test_parse_audacity_matches_oracle(fvad_mod, oracle_mod):
+    txt = "0.5\t1.75\tspeech\r\n2\t3\t\n\n4.125\t9.0\tx"
+    assert np.array_equal(fvad_mod.parse_audacity(txt), oracle_mod.parse_audacity(txt))
+    with pytest.raises(ValueError):
+        fvad_mod.parse_audacity("1\t2\r\n")  # CR kept in the 'to' field (formats.zig:11-14)
+
+
+def test_vadmachine_matches_oracle(fvad_mod, oracle_mod):
+    """Product VADMachine fed the oracle's per-window band sums / ratio / vad
+    reproduces the oracle's segment list exactly."""
+    O = oracle_mod
+    om = O.Model(seed=1)
+    x, _ = fvad_mod.synth_stream(1, 48000 * 40, 2)
+    p = O.Pipeline(2, om, trace_frames=5000, trace_windows=1000)
+    p.push([x[0], x[1]])
+    _, wins = p.trace()
+    vm = fvad_mod.VADMachine(n_channels=2)
+    assert vm.bins() == (4, 64)
+    for w in wins:
+        vm.run(int(w["index"]), w["band"][:2], float(w["vad"]), float(w["ratio"]))
+    ref = p.segments()
+    got = vm.segments()
+    assert len(ref) > 0
+    assert got == ref
+
+
+def test_vadmachine_alt_config_bins(fvad_mod):
+    c = fvad_mod.VadmConfig.default()
+    c.speech_min_freq, c.speech_max_freq = 300.0, 3000.0
+    assert fvad_mod.VADMachine(c).bins() == (13, 128)
+
+
+def test_engine_fails_loudly_without_gpu(fvad_mod):
+    from conftest import gpu_available
+    if gpu_available():
+        pytest.skip("GPU present")
+    with pytest.raises(fvad_mod.FvadError):
+        fvad_mod.Engine(fvad_mod.Model(seed=1), 2)

@@ -1,0 +1,36 @@
+"""Diagnostic: per-phase cycle shares of k_frame from the FVAD_STAMPS build.
+Usage: FVAD_LIB=formula-vad_amd/lib/libfvad_stamps.so python tools/stamps.py [streams] [ticks]
+Shares only — the stamp build's fences distort absolute time."""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "formula-vad_amd"))
+import fvad
+
+NAMES = ["load state", "pitch shift", "analysis window+scatter", "FFT A (X) + copy", "Ex + downsample",
+         "autocorr", "LPC", "FIR5", "coarse xcorr + Syy seqs", "coarse scan", "fine xcorr", "fine scan",
+         "remove_doubling products", "rd selection", "rd final xcorr", "P window+FFT+Ep/Exp",
+         "Exp norm/log10/DCT/Ly", "features", "dense + vad GRU", "noise GRU", "denoise GRU + out",
+         "pitch filter + gains", "synthesis", "tick end + FFT B"]
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+L = fvad.lib()
+L.fvad_engine_stamps.restype = C.c_int
+L.fvad_engine_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
+m = fvad.Model(seed=1)
+e = fvad.Engine(m, B, 2, max_ticks=T)
+e.load_synthetic(T)
+e.run_resident(T)
+e.sync()
+assert L.fvad_engine_stamps(e.h, None, 0) == 0  # allocate + zero
+e.run_resident(T)
+e.sync()
+buf = (C.c_ulonglong * 24)()
+assert L.fvad_engine_stamps(e.h, buf, 24) == 0
+tot = sum(buf)
+frames = B * 2 * T
+print("total stamped cycles per channel-frame per WG: %.0f" % (tot / frames))
+for i, n in enumerate(NAMES):
+    print("%2d %-28s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[i] / tot, buf[i] / frames))
+print("   %-28s %6.2f%%" % ("store state", 100.0 * buf[23] / tot if len(buf) > 23 else 0))
