@@ -1,0 +1,84 @@
+"""`fvad-simulator -i plan.json` end to end (simulator.zig:74-139): WAV +
+Audacity labels in, report / Audacity txt out; segments and TP/FP/FN equal
+the oracle's on the same inputs."""
+import json
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SIM = os.path.join(ROOT, "formula-vad_amd", "lib", "fvad-simulator")
+
+
+def write_wav(path, planar, pcm16=False):
+    ch, n = planar.shape
+    inter = planar.T.reshape(-1)
+    if pcm16:
+        data = np.clip(np.round(inter * 32767), -32768, 32767).astype("<i2").tobytes()
+        fmt, bits = 1, 16
+    else:
+        data = inter.astype("<f4").tobytes()
+        fmt, bits = 3, 32
+    bps = bits // 8
+    hdr = b"RIFF" + struct.pack("<I", 36 + len(data)) + b"WAVE"
+    hdr += b"fmt " + struct.pack("<IHHIIHH", 16, fmt, ch, 48000, 48000 * ch * bps, ch * bps, bits)
+    hdr += b"data" + struct.pack("<I", len(data))
+    with open(path, "wb") as f:
+        f.write(hdr + data)
+
+
+def read_back(planar, pcm16):
+    if not pcm16:
+        return planar
+    q = np.clip(np.round(planar * 32767), -32768, 32767).astype(np.int16)
+    return (q.astype(np.float32) / np.float32(32768.0)).astype(np.float32)
+
+
+def test_simulator_plan(fvad_mod, oracle_mod, tmp_path):
+    ids, secs = [0, 4, 19], [40.0, 33.3, 25.0]
+    plan = {"instances": [], "config": {"vad_config": {}, "output_dir": "sim-out", "preload_audio": False,
+                                          "audio_read_frame_count": 48000, "unknown_field": 1}}
+    truth = {}
+    for k, (i, s) in enumerate(zip(ids, secs)):
+        x, lab = fvad_mod.synth_stream(i, int(48000 * s), 2)
+        pcm16 = k == 1
+        write_wav(tmp_path / ("s%d.wav" % i), x, pcm16=pcm16)
+        (tmp_path / ("s%d.txt" % i)).write_text("".join("%f\t%f\tspeech\n" % (a, b) for a, b in lab))
+        plan["instances"].append({"name": "drv%d" % i, "audio_path": "s%d.wav" % i, "ref_path": "s%d.txt" % i})
+        truth["drv%d" % i] = (read_back(x, pcm16), oracle_mod.parse_audacity(
+            (tmp_path / ("s%d.txt" % i)).read_text()))
+    (tmp_path / "plan.json").write_text(json.dumps(plan))
+    js = tmp_path / "summary.json"
+    env = dict(os.environ, FVAD_SIM_JSON=str(js))
+    r = subprocess.run([SIM, "-i", str(tmp_path / "plan.json")], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "=> Performance Report" in r.stdout and "Fowlkes-Mallows" in r.stdout
+    out = json.loads(js.read_text())
+    om = oracle_mod.Model(seed=1)
+    for inst in out["instances"]:
+        x, refs = truth[inst["name"]]
+        p = oracle_mod.Pipeline(2, om)
+        p.push([x[0], x[1]])
+        ref_segs = [(a, b) for a, b, _, _ in p.segments()]
+        assert [tuple(s) for s in inst["segments"]] == ref_segs, inst["name"]
+        st = oracle_mod.evaluate([(a / 48000.0, b / 48000.0) for a, b in ref_segs], refs, 0.7, 5, 10, 5)
+        assert np.float32(inst["tp"]) == np.float32(st["true_positives_sec"])
+        assert np.float32(inst["fp"]) == np.float32(st["false_positives_sec"])
+        assert np.float32(inst["fn"]) == np.float32(st["false_negatives_sec"])
+    outdirs = list((tmp_path / "sim-out").iterdir())
+    assert len(outdirs) == 1
+    files = sorted(f.name for f in outdirs[0].iterdir())
+    assert "report.txt" in files and "plan.json" in files and "drv0-audacity.txt" in files
+
+
+def test_simulator_bad_plan(tmp_path):
+    (tmp_path / "plan.json").write_text('{"instances": [{"name": "a", "audio_path": "missing.wav", '
+                                        '"ref_path": "missing.txt"}]}')
+    r = subprocess.run([SIM, "-i", str(tmp_path / "plan.json")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "Failed to initialize simulation" in r.stdout
