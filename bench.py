@@ -8,8 +8,9 @@ through rnnoise (+ its share of the 2048-point band-energy FFT).
 Workload: configs[4]'s per-GPU partition — 2048 synthetic 48 kHz stereo
 streams per GPU (16384 at 8 GPUs), weak scaling, f32 exact numerics (fp32
 weights; the fp16 variant of configs[4] is not used).  A step = one push of
-TICKS ticks (480 samples per channel) for every stream of the partition:
-k_prep + k_frame on the engine's HIP stream, input resident in HBM.
+TICKS ticks (480 samples per channel) for every stream of the partition —
+the staged pipeline's 10 kernels (fvad_staged.hip; --mode fused: k_prep +
+k_frame) on the engine's HIP stream, input resident in HBM.
 
 Multi-GPU: one process per GPU (torch.distributed.run), each with its own
 stream partition; the only collectives are the barrier and the max-reduce of
@@ -40,6 +41,7 @@ def parse():
     ap.add_argument("--streams-per-gpu", type=int, default=2048)
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--ticks", type=int, default=50)
+    ap.add_argument("--mode", choices=("staged", "fused"), default="staged")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on this host (rank 0)")
     ap.add_argument("--cpu-streams", type=int, default=256)
     ap.add_argument("--cpu-ticks", type=int, default=200)
@@ -114,7 +116,7 @@ def main():
 
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     model = fvad.Model(seed=1)
-    eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T)
+    eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=args.mode)
     eng.load_synthetic(T, base=rank * B)
 
     for _ in range(args.warmup):
@@ -140,36 +142,56 @@ def main():
             dist.destroy_process_group()
         return
 
-    # roofline of the dominant kernel (k_frame), per launch, measured with HIP events on the engine stream
-    flops_cf = cost.flops_per_channel_frame(Ch)
-    prep_share = cost.phases(Ch)["prep: s16 scale + HP biquad + rms"]
-    frame_flops = (flops_cf - prep_share) * B * Ch * T
-    frame_s = kt["frame_ms"] / 1000.0
-    achieved_tf = frame_flops / frame_s / 1e12
-    alg_bytes = cost.frame_kernel_bytes(B, Ch, T)
+    # roofline of the dominant kernel, per launch, from HIP events recorded
+    # around each kernel on the engine stream (fvad_engine_kernel_times)
+    frames_launch = B * Ch * T
+    if args.mode == "fused":
+        prep_share = cost.phases(Ch)["prep: s16 scale + HP biquad + rms"]
+        per_k = {"k_prep": {"flops": prep_share, "bytes": cost.prep_kernel_bytes(B, Ch, T) / frames_launch},
+                 "k_frame": {"flops": cost.flops_per_channel_frame(Ch) - prep_share,
+                             "bytes": cost.frame_kernel_bytes(B, Ch, T) / frames_launch}}
+    else:
+        per_k = cost.staged_kernels(Ch)
+    ridge = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    kernels = {}
+    for name, ms in kt["kernels"].items():
+        c = per_k[name]
+        sec = ms / 1000.0
+        kernels[name] = {"ms": round(ms, 4), "tflops": round(c["flops"] * frames_launch / sec / 1e12, 3),
+                         "gbs": round(c["bytes"] * frames_launch / sec / 1e9, 1),
+                         "intensity": round(c["flops"] / c["bytes"], 2) if c["bytes"] else None}
+    dom = max(kt["kernels"], key=lambda n: kt["kernels"][n])
+    c = per_k[dom]
+    dom_s = kt["kernels"][dom] / 1000.0
+    alg_flops = c["flops"] * frames_launch
+    alg_bytes = c["bytes"] * frames_launch
+    compute_bound = c["flops"] / c["bytes"] >= ridge
     traffic = None
     pmc_src = None
     if os.path.exists(args.pmc_json):
         try:
             with open(args.pmc_json) as f:
                 pm = json.load(f)
-            if pm.get("streams") == B and pm.get("ticks") == T and pm.get("channels") == Ch:
-                traffic = pm.get("frame_bytes_per_launch")
+            if (pm.get("streams"), pm.get("ticks"), pm.get("channels"), pm.get("mode")) == (B, T, Ch, args.mode):
+                traffic = pm.get("bytes_per_launch", {}).get(dom)
                 pmc_src = os.path.relpath(args.pmc_json, ROOT)
         except Exception:
             traffic = None
+    if compute_bound:
+        achieved, peak, unit = alg_flops / dom_s / 1e12, FP32_PEAK_TFLOPS, "TFLOP/s"
+    else:
+        achieved, peak, unit = alg_bytes / dom_s / 1e9, HBM_PEAK_GBS, "GB/s"
     roofline = {
-        "bound": "mfma",
-        "roof": "fp32 compute: v_mfma_f32 peak == fp32 VALU peak (157.3 TFLOP/s); the path runs on VALU",
-        "kernel": "k_frame",
-        "achieved": round(achieved_tf, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 5),
+        "bound": "mfma" if compute_bound else "hbm",
+        "roof": ("fp32 compute: v_mfma_f32 peak == fp32 VALU peak (157.3 TFLOP/s); the path runs on VALU"
+                 if compute_bound else "HBM3E 8 TB/s"),
+        "kernel": dom,
+        "achieved": round(achieved, 4), "peak": peak, "unit": unit, "frac": round(achieved / peak, 5),
         "traffic": traffic, "traffic_source": pmc_src,
-        "alg_flops_per_launch": frame_flops, "alg_bytes_per_launch": alg_bytes,
-        "kernel_ms_avg": round(kt["frame_ms"], 4), "prep_ms_avg": round(kt["prep_ms"], 4),
-        "hbm_achieved_gbs": round(alg_bytes / frame_s / 1e9, 2),
-        "hbm_frac": round(alg_bytes / frame_s / 1e9 / HBM_PEAK_GBS, 5),
+        "alg_flops_per_launch": alg_flops, "alg_bytes_per_launch": alg_bytes,
+        "kernel_ms_avg": round(kt["kernels"][dom], 4), "push_ms_avg": round(kt["total_ms"], 4),
         "timed_launches": kt["runs"],
+        "kernels": kernels,
     }
     cpu = None
     if args.cpu_baseline and world == 1:
@@ -185,7 +207,7 @@ def main():
                                "(%d at %d GPU), %d ticks (480 samples/ch) per step, fp32 weights, bit-exact path"
                                % (B, Ch, B * world, world, T),
                    "streams_per_gpu": B, "channels": Ch, "ticks_per_step": T, "fft_size": 2048,
-                   "parallelism": "stream-partition x%d (no collectives)" % world},
+                   "parallelism": "stream-partition x%d (no collectives)" % world, "mode": args.mode},
         "realtime_streams": round(value / (100.0 * Ch), 1),
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -49,6 +49,7 @@ extern "C" DenoiseState *rnnoise_create(RNNModel *model) {
   fvad_engine_config_default(&cfg, 1, 1);
   cfg.max_ticks = 1;
   cfg.want_denoised = 1;
+  cfg.mode = FVAD_MODE_FUSED;  // one frame per call: nothing to parallelise over time
   fvad_engine *e = nullptr;
   if (fvad_engine_create(&cfg, m, &e) != FVAD_OK) return nullptr;
   fvad_engine_set_raw_s16(e, 1);

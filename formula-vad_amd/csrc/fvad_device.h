@@ -1,0 +1,265 @@
+// Device-side building blocks shared by the fused (k_frame) and the staged
+// kernels.  Every function reproduces the C evaluation order of the restated
+// rnnoise / kissfft sources (see fvad_kernels.hip header on numerics).
+#pragma once
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "fvad_internal.h"
+
+namespace fvad {
+
+constexpr float kWs = 1.f / 256;  // WEIGHTS_SCALE (rnn.c)
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  float2 m;
+  m.x = a.x * b.x - a.y * b.y;
+  m.y = a.x * b.y + a.y * b.x;
+  return m;
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+
+// tansig_approx / sigmoid_approx / relu (rnn.c, [upstream, recalled])
+__device__ __forceinline__ float tansig(const float *__restrict__ table, float x) {
+  if (!(x < 8)) return 1;
+  if (!(x > -8)) return -1;
+  if (x != x) return 0;
+  float sign = 1;
+  if (x < 0) {
+    x = -x;
+    sign = -1;
+  }
+  const int i = (int)floorf(.5f + 25 * x);
+  x -= .04f * i;
+  float y = table[i];
+  const float dy = 1 - y * y;
+  y = y + x * dy * (1 - y * x);
+  return sign * y;
+}
+__device__ __forceinline__ float sigmoid(const float *__restrict__ table, float x) {
+  return (float)(.5 + .5 * (double)tansig(table, (float)(.5 * (double)x)));
+}
+__device__ __forceinline__ float activate(const float *__restrict__ table, int act, float x) {
+  if (act == kActSigmoid) return sigmoid(table, x);
+  if (act == kActTanh) return tansig(table, x);
+  return x < 0 ? 0 : x;
+}
+
+// --- celt kiss_fft (960 = 5*3*4*4*4), forward, in place on W after the
+//     digit-reversed scaled copy.  Stage order and butterfly expressions
+//     follow opus_fft_impl / kf_bfly{4,3,5} (Opus 1.2-era float forms).
+__device__ __forceinline__ void bfly4(float2 *F, int m, float2 tw1, float2 tw2, float2 tw3) {
+  float2 a0 = F[0];
+  const float2 s0 = cmul(F[m], tw1), s1 = cmul(F[2 * m], tw2), s2 = cmul(F[3 * m], tw3);
+  const float2 s5 = csub(a0, s1);
+  a0 = cadd(a0, s1);
+  const float2 s3 = cadd(s0, s2), s4 = csub(s0, s2);
+  F[2 * m] = csub(a0, s3);
+  a0 = cadd(a0, s3);
+  F[0] = a0;
+  F[m] = make_float2(s5.x + s4.y, s5.y - s4.x);
+  F[3 * m] = make_float2(s5.x - s4.y, s5.y + s4.x);
+}
+
+__device__ __forceinline__ void bfly3(float2 *F, int m, float2 tw1, float2 tw2, float2 epi3) {
+  float2 a0 = F[0];
+  const float2 s1 = cmul(F[m], tw1), s2 = cmul(F[2 * m], tw2);
+  const float2 s3 = cadd(s1, s2);
+  float2 s0 = csub(s1, s2);
+  const float2 b1 = make_float2(a0.x - s3.x * .5f, a0.y - s3.y * .5f);
+  s0.x *= epi3.y;
+  s0.y *= epi3.y;
+  a0 = cadd(a0, s3);
+  F[0] = a0;
+  F[2 * m] = make_float2(b1.x + s0.y, b1.y - s0.x);
+  F[m] = make_float2(b1.x - s0.y, b1.y + s0.x);
+}
+
+__device__ __forceinline__ void bfly5(float2 *F, int m, float2 t1, float2 t2, float2 t3, float2 t4, float2 ya,
+                                      float2 yb) {
+  const float2 s0 = F[0];
+  const float2 s1 = cmul(F[m], t1), s2 = cmul(F[2 * m], t2), s3 = cmul(F[3 * m], t3), s4 = cmul(F[4 * m], t4);
+  const float2 s7 = cadd(s1, s4), s10 = csub(s1, s4), s8 = cadd(s2, s3), s9 = csub(s2, s3);
+  float2 f0;
+  f0.x = s0.x + (s7.x + s8.x);
+  f0.y = s0.y + (s7.y + s8.y);
+  float2 s5, s6, s11, s12;
+  s5.x = s0.x + s7.x * ya.x + s8.x * yb.x;
+  s5.y = s0.y + s7.y * ya.x + s8.y * yb.x;
+  s6.x = s10.y * ya.y + s9.y * yb.y;
+  s6.y = -(s10.x * ya.y) - s9.x * yb.y;
+  s11.x = s0.x + s7.x * yb.x + s8.x * ya.x;
+  s11.y = s0.y + s7.y * yb.x + s8.y * ya.x;
+  s12.x = -(s10.y * yb.y) + s9.y * ya.y;
+  s12.y = s10.x * yb.y - s9.x * ya.y;
+  F[0] = f0;
+  F[m] = csub(s5, s6);
+  F[4 * m] = cadd(s5, s6);
+  F[2 * m] = cadd(s11, s12);
+  F[3 * m] = csub(s11, s12);
+}
+
+template <int NT>
+__device__ void fft960_stages(float2 *W, const float2 *__restrict__ tw, int tid) {
+  for (int b = tid; b < 240; b += NT) {  // radix 4, m = 1 (degenerate: no twiddles)
+    float2 *F = W + 4 * b;
+    float2 f0 = F[0];
+    const float2 f1 = F[1], f2 = F[2], f3 = F[3];
+    const float2 s0 = csub(f0, f2);
+    f0 = cadd(f0, f2);
+    float2 s1 = cadd(f1, f3);
+    F[2] = csub(f0, s1);
+    F[0] = cadd(f0, s1);
+    s1 = csub(f1, f3);
+    F[1] = make_float2(s0.x + s1.y, s0.y - s1.x);
+    F[3] = make_float2(s0.x - s1.y, s0.y + s1.x);
+  }
+  __syncthreads();
+  for (int q = tid; q < 240; q += NT) {  // radix 4, m = 4, fstride 60
+    const int i = q >> 2, j = q & 3;
+    bfly4(W + i * 16 + j, 4, tw[j * 60], tw[j * 120], tw[j * 180]);
+  }
+  __syncthreads();
+  for (int q = tid; q < 240; q += NT) {  // radix 4, m = 16, fstride 15
+    const int i = q >> 4, j = q & 15;
+    bfly4(W + i * 64 + j, 16, tw[j * 15], tw[j * 30], tw[j * 45]);
+  }
+  __syncthreads();
+  {
+    const float2 epi3 = tw[320];
+    for (int q = tid; q < 320; q += NT) {  // radix 3, m = 64, fstride 5
+      const int i = q >> 6, k = q & 63;
+      bfly3(W + i * 192 + k, 64, tw[k * 5], tw[k * 10], epi3);
+    }
+  }
+  __syncthreads();
+  {
+    const float2 ya = tw[192], yb = tw[384];
+    for (int u = tid; u < 192; u += NT) bfly5(W + u, 192, tw[u], tw[2 * u], tw[3 * u], tw[4 * u], ya, yb);
+  }
+  __syncthreads();
+}
+
+// compute_band_energy / compute_band_corr: one lane per band, C summation order.
+__device__ __forceinline__ float band_sum(const float2 *A, const float2 *B, const Plan *__restrict__ P, int b) {
+  float acc = 0;
+  if (b >= 1) {
+#pragma unroll 4
+    for (int k = P->eband4[b - 1]; k < P->eband4[b]; k++) {
+      float tmp = A[k].x * B[k].x;
+      tmp += A[k].y * B[k].y;
+      acc += P->band_frac[k] * tmp;
+    }
+  }
+  if (b <= kBands - 2) {
+#pragma unroll 4
+    for (int k = P->eband4[b]; k < P->eband4[b + 1]; k++) {
+      float tmp = A[k].x * B[k].x;
+      tmp += A[k].y * B[k].y;
+      acc += (1 - P->band_frac[k]) * tmp;
+    }
+  }
+  if (b == 0 || b == kBands - 1) acc *= 2;
+  return acc;
+}
+
+// interp_band_gain value at bin k (bins >= 400 keep their zero initialiser)
+__device__ __forceinline__ float interp_gain(const float *bandE, const Plan *__restrict__ P, int k) {
+  if (k >= 400) return 0.0f;
+  const int b = P->band_of[k];
+  const float frac = P->band_frac[k];
+  return (1 - frac) * bandE[b] + frac * bandE[b + 1];
+}
+
+// find_best_pitch (pitch.c) split in two: the Syy energy recurrence depends
+// only on y, so syy_sequence() produces the value Syy holds at every lag i
+// (before its update), and best_pitch_visit() replays the selection for one
+// lag.  Visiting the lags in increasing order reproduces find_best_pitch
+// exactly; lags with xcorr <= 0 only advance Syy and may be skipped.
+__device__ void syy_sequence(const float *y, int ys, int len, int max_pitch, float *syy) {
+  float Syy = 1;
+#pragma unroll 8
+  for (int j = 0; j < len; j++) Syy = Syy + y[j * ys] * y[j * ys];
+#pragma unroll 4
+  for (int i = 0; i < max_pitch; i++) {
+    syy[i] = Syy;
+    const float ya = y[(i + len) * ys], yb = y[i * ys];
+    Syy += ya * ya - yb * yb;
+    Syy = (1 > Syy) ? 1 : Syy;
+  }
+}
+
+__device__ __forceinline__ void best_pitch_visit(float xc, float Syy, int i, float &bn0, float &bn1, float &bd0,
+                                                 float &bd1, int *best) {
+  if (xc > 0) {
+    float xcorr16 = xc;
+    xcorr16 *= 1e-12f;
+    const float num = xcorr16 * xcorr16;
+    if (num * bd1 > bn1 * Syy) {
+      if (num * bd0 > bn0 * Syy) {
+        bn1 = bn0;
+        bd1 = bd0;
+        best[1] = best[0];
+        bn0 = num;
+        bd0 = Syy;
+        best[0] = i;
+      } else {
+        bn1 = num;
+        bd1 = Syy;
+        best[1] = i;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float pitch_gain(float xy, float xx, float yy) { return xy / sqrtf(1 + xx * yy); }
+
+// pitch.c second_check[16] = {0,0,3,2,3,2,5,2,3,2,3,2,5,2,3,2}, packed 3 bits per entry
+__device__ __forceinline__ int second_check(int k) { return (int)((0x4d54d35534c0ull >> (3 * k)) & 7); }
+
+template <int NT>
+__device__ void dense_layer(const DevDense &d, const float *in, float *out, const float *tansig_tab, int tid) {
+  for (int i = tid; i < d.nout; i += NT) {
+    float sum = d.b[i];
+#pragma unroll 8
+    for (int j = 0; j < d.nin; j++) sum += d.w[j * d.nout + i] * in[j];
+    out[i] = activate(tansig_tab, d.act, kWs * sum);
+  }
+}
+
+// compute_gru (rnn.c): z/r gates on 2N lanes, then h on N lanes.  Each
+// neuron's sum runs in C order on its own lane.
+template <int NT>
+__device__ void gru_gates(const DevGru &g, const float *in, const float *state, float *zr, const float *tab,
+                          int tid) {
+  const int N = g.nout, M = g.nin, S3 = 3 * N;
+  for (int t = tid; t < 2 * N; t += NT) {
+    const int col = t;  // z: col = i, r: col = N + i
+    float sum = g.b[col];
+#pragma unroll 8
+    for (int j = 0; j < M; j++) sum += g.win[j * S3 + col] * in[j];
+#pragma unroll 8
+    for (int j = 0; j < N; j++) sum += g.wrec[j * S3 + col] * state[j];
+    zr[t] = sigmoid(tab, kWs * sum);
+  }
+}
+template <int NT>
+__device__ void gru_out(const DevGru &g, const float *in, const float *state, const float *zr, float *h,
+                        const float *tab, int tid) {
+  const int N = g.nout, M = g.nin, S3 = 3 * N;
+  for (int i = tid; i < N; i += NT) {
+    float sum = g.b[2 * N + i];
+#pragma unroll 8
+    for (int j = 0; j < M; j++) sum += g.win[j * S3 + 2 * N + i] * in[j];
+#pragma unroll 8
+    for (int j = 0; j < N; j++) sum += g.wrec[j * S3 + 2 * N + i] * state[j] * zr[N + j];
+    sum = activate(tab, g.act, kWs * sum);
+    h[i] = zr[i] * state[i] + (1 - zr[i]) * sum;
+  }
+}
+
+
+}  // namespace fvad

@@ -8,8 +8,14 @@
 //   pcm     [max_ticks][streams][ch][480] input staging (or resident synthetic)
 //   xbuf    [max_ticks][streams][ch][480] high-passed s16-scale frames (k_prep)
 //   ratio / outputs [max_ticks][streams] (+ channels, bands)
-// A push = k_prep (lane per stream) then k_frame (workgroup per stream) on
-// the engine's HIP stream.
+// staged mode (default, fvad_staged.hip) adds per-frame intermediates,
+// frame f = s * V + tick * C + c with V = max_ticks * C:
+//   xs [streams][1248 + V*480]  high-passed samples with pitch history
+//   X, P [f][481] complex; Ex/Ep/Exp/Lyf [f][22]; f34 [f][8]; rec [f][144];
+//   ys [f][960]; silence / pitch / vad [f]
+// fused mode (fvad_kernels.hip): xbuf [max_ticks][streams][ch][480] and one
+// k_frame workgroup per stream.  Both run on the engine's HIP stream and give
+// identical results.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -23,6 +29,7 @@
 #include "../../include/fvad.h"
 #include "fvad_internal.h"
 #include "fvad_kernels.h"
+#include "fvad_staged.h"
 
 const fvad::HostModel *fvad_model_host(const fvad_model *m);
 
@@ -55,9 +62,16 @@ struct fvad_engine {
   float *d_pcm = nullptr, *d_xbuf = nullptr, *d_ratio = nullptr;
   float *d_vad = nullptr, *d_wratio = nullptr, *d_wvad = nullptr, *d_band = nullptr, *d_den = nullptr;
   int *d_wflag = nullptr, *d_ticks = nullptr;
+  // staged-mode intermediates
+  float *d_xs = nullptr, *d_X = nullptr, *d_P = nullptr, *d_Ex = nullptr, *d_Ep = nullptr, *d_Exp = nullptr,
+        *d_Lyf = nullptr, *d_f34 = nullptr, *d_rec = nullptr, *d_vadf = nullptr, *d_ys = nullptr;
+  int *d_sil = nullptr, *d_pitch = nullptr, *d_wtick = nullptr;
+  long long *d_wstart = nullptr;
+  int V = 0, L = 0, wmax = 0, grid_frames = 0;
   int resident_ticks = 0;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  double ms_sum[3] = {0, 0, 0};
+  int n_kernels = 0;
+  hipEvent_t ev[FVAD_MAX_TIMES] = {};
+  double ms_sum[FVAD_MAX_TIMES] = {};
   int n_timed = 0;
   bool timing_pending = false;
   int raw_s16 = 0;  // rnnoise compat mode (s16-scaled I/O)
@@ -144,8 +158,11 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
 }
 
 void free_all(fvad_engine *e) {
-  void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm, e->d_xbuf, e->d_ratio, e->d_vad,
-                  e->d_wratio, e->d_wvad, e->d_band, e->d_den, e->d_wflag, e->d_ticks, e->d_model, e->d_stamps};
+  void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm,   e->d_xbuf, e->d_ratio,
+                  e->d_vad,  e->d_wratio,  e->d_wvad,  e->d_band, e->d_den,   e->d_wflag, e->d_ticks,
+                  e->d_model, e->d_stamps, e->d_xs,    e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
+                  e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_vadf,  e->d_ys,    e->d_sil,
+                  e->d_pitch, e->d_wtick,  e->d_wstart};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &ev : e->ev)
@@ -183,13 +200,17 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     hi = std::max(hi, c.band_hi[b]);
   }
   if (hi - lo + 1 > 256) return fail(FVAD_EINVAL, "reported bins must span <= 256");
+  if (c.mode != FVAD_MODE_STAGED && c.mode != FVAD_MODE_FUSED) return fail(FVAD_EINVAL, "unknown engine mode");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FVAD_EDEVICE, "no HIP device available");
   if (c.device < 0 || c.device >= ndev) return fail(FVAD_EDEVICE, "device ordinal out of range");
 
   fvad_engine *e = new fvad_engine();
   e->cfg = c;
-  e->ring_len = c.fft_size + fvad::kFrame;
+  // the staged path writes every tick of a push before FFT B reads its
+  // windows, so the ring holds one window plus a whole push
+  e->ring_len = c.fft_size + c.max_ticks * fvad::kFrame;
+  e->n_kernels = c.mode == FVAD_MODE_STAGED ? fvad::kStagedKernels : 2;
   auto bail = [&](int rc) {
     free_all(e);
     delete e;
@@ -198,8 +219,8 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   if (hipSetDevice(c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipSetDevice failed"));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
-  for (auto &ev : e->ev)
-    if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipEventCreate failed"));
+  for (int i = 0; i <= e->n_kernels; i++)
+    if (hipEventCreate(&e->ev[i]) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipEventCreate failed"));
   fvad::Plan *plan = new fvad::Plan();
   fvad::build_plan(plan, c.fft_size);
   int rc = dalloc(&e->d_plan, 1);
@@ -211,11 +232,30 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t frames = T * B * C * fvad::kFrame;
   if ((rc = dalloc(&e->d_state, B * fvad::st::kWords)) || (rc = dalloc(&e->d_ring, B * C * e->ring_len)) ||
-      (rc = dalloc(&e->d_pcm, frames)) || (rc = dalloc(&e->d_xbuf, frames)) || (rc = dalloc(&e->d_ratio, T * B)) ||
+      (rc = dalloc(&e->d_pcm, frames)) || (rc = dalloc(&e->d_ratio, T * B)) ||
       (rc = dalloc(&e->d_vad, T * B)) || (rc = dalloc(&e->d_wratio, T * B)) || (rc = dalloc(&e->d_wvad, T * B)) ||
       (rc = dalloc(&e->d_wflag, T * B)) || (rc = dalloc(&e->d_band, T * B * C * c.n_bands)) ||
       (rc = dalloc(&e->d_ticks, B)) || (c.want_denoised && (rc = dalloc(&e->d_den, frames))))
     return bail(rc);
+  if (c.mode == FVAD_MODE_FUSED) {
+    if ((rc = dalloc(&e->d_xbuf, frames))) return bail(rc);
+  } else {
+    e->V = (int)(T * C);
+    e->L = (fvad::kPitchBuf - fvad::kFrame) + e->V * fvad::kFrame;
+    e->wmax = (int)(T * fvad::kFrame / c.fft_size) + 2;
+    const size_t F = B * e->V;
+    if ((rc = dalloc(&e->d_xs, B * e->L)) || (rc = dalloc(&e->d_X, F * fvad::kFreq * 2)) ||
+        (rc = dalloc(&e->d_P, F * fvad::kFreq * 2)) || (rc = dalloc(&e->d_Ex, F * fvad::kBands)) ||
+        (rc = dalloc(&e->d_Ep, F * fvad::kBands)) || (rc = dalloc(&e->d_Exp, F * fvad::kBands)) ||
+        (rc = dalloc(&e->d_Lyf, F * fvad::kBands)) || (rc = dalloc(&e->d_f34, F * 8)) ||
+        (rc = dalloc(&e->d_rec, F * fvad::kPitchRecord)) || (rc = dalloc(&e->d_vadf, F)) ||
+        (rc = dalloc(&e->d_ys, F * fvad::kWin)) || (rc = dalloc(&e->d_sil, F)) || (rc = dalloc(&e->d_pitch, F)) ||
+        (rc = dalloc(&e->d_wtick, B * e->wmax)) || (rc = dalloc(&e->d_wstart, B * e->wmax)))
+      return bail(rc);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "device query failed"));
+    e->grid_frames = prop.multiProcessorCount * 8;
+  }
   if ((rc = fvad_engine_reset(e))) return bail(rc);
   *out = e;
   return FVAD_OK;
@@ -231,7 +271,21 @@ extern "C" void fvad_engine_destroy(fvad_engine *e) {
 
 namespace {
 
-int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
+void fill_bands(const fvad_engine_config &c, int *band_lo, int *band_hi, int *lo_all, int *hi_all) {
+  int lo = 1 << 30, hi = -1;
+  for (int b = 0; b < fvad::kMaxBandCfg; b++) {
+    band_lo[b] = b < c.n_bands ? c.band_lo[b] : 0;
+    band_hi[b] = b < c.n_bands ? c.band_hi[b] : -1;
+    if (b < c.n_bands) {
+      lo = std::min(lo, c.band_lo[b]);
+      hi = std::max(hi, c.band_hi[b]);
+    }
+  }
+  *lo_all = lo;
+  *hi_all = hi;
+}
+
+int launch_fused(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   const fvad_engine_config &c = e->cfg;
   fvad::PrepArgs pa;
   pa.n_streams = c.n_streams;
@@ -256,17 +310,7 @@ int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   fa.plan = e->d_plan;
   fa.model = e->d_model;
   fa.n_bands = c.n_bands;
-  int lo = 1 << 30, hi = -1;
-  for (int b = 0; b < fvad::kMaxBandCfg; b++) {
-    fa.band_lo[b] = b < c.n_bands ? c.band_lo[b] : 0;
-    fa.band_hi[b] = b < c.n_bands ? c.band_hi[b] : -1;
-    if (b < c.n_bands) {
-      lo = std::min(lo, c.band_lo[b]);
-      hi = std::max(hi, c.band_hi[b]);
-    }
-  }
-  fa.bin_lo_all = lo;
-  fa.bin_hi_all = hi;
+  fill_bands(c, fa.band_lo, fa.band_hi, &fa.bin_lo_all, &fa.bin_hi_all);
   fa.out_vad = e->d_vad;
   fa.out_win_ratio = e->d_wratio;
   fa.out_win_vad = e->d_wvad;
@@ -279,22 +323,73 @@ int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   HIP_TRY(fvad::launch_prep(pa, e->stream));
   if (timed) HIP_TRY(hipEventRecord(e->ev[1], e->stream));
   HIP_TRY(fvad::launch_frame(fa, e->stream));
-  if (timed) {
-    HIP_TRY(hipEventRecord(e->ev[2], e->stream));
-    e->timing_pending = true;
-  }
+  if (timed) HIP_TRY(hipEventRecord(e->ev[2], e->stream));
   return FVAD_OK;
+}
+
+int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
+  const fvad_engine_config &c = e->cfg;
+  fvad::StagedArgs a;
+  a.n_streams = c.n_streams;
+  a.n_channels = c.n_channels;
+  a.n_ticks = n_ticks;
+  a.V = e->V;
+  a.L = e->L;
+  a.ticks_valid = use_ticks ? e->d_ticks : nullptr;
+  a.pcm = e->d_pcm;
+  a.xs = e->d_xs;
+  a.ratio = e->d_ratio;
+  a.state = e->d_state;
+  a.X = reinterpret_cast<float2 *>(e->d_X);
+  a.P = reinterpret_cast<float2 *>(e->d_P);
+  a.Ex = e->d_Ex;
+  a.Ep = e->d_Ep;
+  a.Exp = e->d_Exp;
+  a.Lyf = e->d_Lyf;
+  a.f34 = e->d_f34;
+  a.silence = e->d_sil;
+  a.rec = e->d_rec;
+  a.pitch = e->d_pitch;
+  a.vadf = e->d_vadf;
+  a.ys = e->d_ys;
+  a.ring = e->d_ring;
+  a.ring_len = e->ring_len;
+  a.win_tick = e->d_wtick;
+  a.win_start = e->d_wstart;
+  a.wmax = e->wmax;
+  a.plan = e->d_plan;
+  a.model = e->d_model;
+  a.n_bands = c.n_bands;
+  fill_bands(c, a.band_lo, a.band_hi, &a.bin_lo_all, &a.bin_hi_all);
+  a.out_vad = e->d_vad;
+  a.out_win_ratio = e->d_wratio;
+  a.out_win_vad = e->d_wvad;
+  a.out_band = e->d_band;
+  a.out_den = e->d_den;
+  a.out_win_flag = e->d_wflag;
+  a.raw_s16 = e->raw_s16;
+  HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr));
+  return FVAD_OK;
+}
+
+int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
+  const int rc = e->cfg.mode == FVAD_MODE_FUSED ? launch_fused(e, n_ticks, use_ticks, timed)
+                                                 : launch_staged(e, n_ticks, use_ticks, timed);
+  if (!rc && timed) e->timing_pending = true;
+  return rc;
 }
 
 int collect_timing(fvad_engine *e) {
   if (!e->timing_pending) return FVAD_OK;
-  HIP_TRY(hipEventSynchronize(e->ev[2]));
-  float a = 0, b = 0;
-  HIP_TRY(hipEventElapsedTime(&a, e->ev[0], e->ev[1]));
-  HIP_TRY(hipEventElapsedTime(&b, e->ev[1], e->ev[2]));
-  e->ms_sum[0] += a;
-  e->ms_sum[1] += b;
-  e->ms_sum[2] += a + b;
+  HIP_TRY(hipEventSynchronize(e->ev[e->n_kernels]));
+  float total = 0;
+  for (int i = 0; i < e->n_kernels; i++) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
+    e->ms_sum[1 + i] += ms;
+    total += ms;
+  }
+  e->ms_sum[0] += total;
   e->n_timed++;
   e->timing_pending = false;
   return FVAD_OK;
@@ -394,7 +489,8 @@ extern "C" int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_r
   if (!e) return fail(FVAD_EINVAL, "null engine");
   int rc = fvad_engine_sync(e);
   if (rc) return rc;
-  for (int i = 0; i < 3; i++) ms_avg[i] = e->n_timed ? e->ms_sum[i] / e->n_timed : 0.0;
+  for (int i = 0; i < FVAD_MAX_TIMES; i++)
+    ms_avg[i] = (e->n_timed && i <= e->n_kernels) ? e->ms_sum[i] / e->n_timed : 0.0;
   if (n_runs) *n_runs = e->n_timed;
   return FVAD_OK;
 }
@@ -403,7 +499,7 @@ extern "C" int fvad_engine_clear_times(fvad_engine *e) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   int rc = fvad_engine_sync(e);
   if (rc) return rc;
-  e->ms_sum[0] = e->ms_sum[1] = e->ms_sum[2] = 0;
+  for (double &v : e->ms_sum) v = 0;
   e->n_timed = 0;
   return FVAD_OK;
 }
@@ -413,4 +509,10 @@ extern "C" int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out)
   if (n_ticks < 1 || n_ticks > e->cfg.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range");
   HIP_TRY(hipSetDevice(e->cfg.device));
   return fetch(e, n_ticks, out);
+}
+
+extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
+  if (!e || i < 0 || i >= e->n_kernels) return nullptr;
+  if (e->cfg.mode == FVAD_MODE_FUSED) return i == 0 ? "k_prep" : "k_frame";
+  return fvad::staged_kernel_name(i);
 }

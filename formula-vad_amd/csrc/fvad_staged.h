@@ -1,0 +1,54 @@
+// Argument block and launcher of the staged (time-parallel) pipeline
+// (fvad_staged.hip).  Frame f = s * V + v, v = tick * C + channel: the
+// channels of a stream are one interleaved virtual rnnoise stream
+// (VAD.zig:274-296), so frame order within a stream is tick-major.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "fvad_internal.h"
+
+namespace fvad {
+
+constexpr int kStagedKernels = 10;
+constexpr int kPitchRecord = 144;  // floats per frame of k_pitch output
+
+struct StagedArgs {
+  int n_streams, n_channels, n_ticks;
+  int V;                   // frame-row stride per stream (= max_ticks * C)
+  int L;                   // xs row length (= 1248 + V * 480)
+  const int *ticks_valid;  // nullable
+  const float *pcm;        // [t][s][c][480] normalised input
+  float *xs;               // [s][L] high-passed s16-scale samples, 1248 history first
+  float *ratio;            // [t][s] per-tick volume ratio
+  float *state;            // [s][st::kWords]
+  float2 *X;               // [f][481] analysis spectrum, then filtered/gained spectrum
+  float2 *P;               // [f][481] pitch spectrum
+  float *Ex, *Ep, *Exp;    // [f][22]
+  float *Lyf;              // [f][22] DCT(Ly) features 0..21 (before deltas)
+  float *f34;              // [f][8] features 34..40
+  int *silence;            // [f]
+  float *rec;              // [f][kPitchRecord]
+  int *pitch;              // [f] selected pitch index
+  float *vadf;             // [f] per-frame vad probability
+  float *ys;               // [f][960] windowed synthesis output
+  float *ring;             // [s][c][ring_len]
+  int ring_len;
+  int *win_tick;           // [s][wmax] tick at which window j completes (-1: none)
+  long long *win_start;    // [s][wmax] absolute sample index of window j
+  int wmax;
+  const Plan *plan;
+  const DevModel *model;
+  int n_bands;
+  int band_lo[kMaxBandCfg], band_hi[kMaxBandCfg];
+  int bin_lo_all, bin_hi_all;
+  float *out_vad, *out_win_ratio, *out_win_vad, *out_band, *out_den;
+  int *out_win_flag;
+  int raw_s16;
+};
+
+// Launch the 10 kernels on `stream`; when ev != nullptr, ev[0..10] are
+// recorded around them (per-kernel timing).
+hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t stream, hipEvent_t *ev);
+const char *staged_kernel_name(int i);
+
+}  // namespace fvad

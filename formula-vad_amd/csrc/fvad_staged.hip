@@ -1,0 +1,1020 @@
+// Staged (time-parallel) MI355X pipeline for the Formula-VAD hot path.
+//
+// rnnoise_process_frame splits into work that depends only on the input
+// samples of the (virtual, channel-interleaved) stream and a thin recurrence:
+//
+//   k_prep2   lane/stream   HP biquad (serial IIR), s16 scaling, RMS volume
+//                           ratio; x written stream-contiguous with 1248 samples
+//                           of pitch history in front of the launch's frames
+//   k_fftA    wg/frame      analysis window + FFT A, band energies Ex, the
+//                           log/floor chain (Ly, E, silence gate), DCT(Ly)
+//   k_pitch   wg/frame      pitch_downsample (autocorr, LPC, FIR5), coarse and
+//                           fine xcorr + find_best_pitch, every remove_doubling
+//                           inner product for every candidate period (the
+//                           final 3-lag xcorr speculatively for all 15)
+//   k_select  lane/stream   remove_doubling's sequential candidate selection
+//                           (needs last_period / last_gain) -> pitch index
+//   k_pspec   wg/frame      pitch window + FFT A -> P, Ep, Exp, DCT(Exp)
+//   k_rnn     wg/stream     the true recurrence: cepstral memory, spectral
+//                           variability, GRU stack, pitch filter, gain smoothing
+//   k_synth   wg/frame      Hermitian extension + FFT A + synthesis window
+//   k_ola     per sample    overlap-add, 1/32767, re-block ring, per-tick vad
+//   k_winmeta lane/stream   window completion, share-weighted ratio, state
+//   k_fftb    wg/window     FFT B (kissfft radix-4), magnitudes, band sums
+//
+// Each wg/frame kernel is persistent (grid-stride over frames) so per-thread
+// table values stay in registers across frames.  All arithmetic reproduces the
+// oracle's operation order (see fvad_kernels.hip), so results are
+// bit-identical to the fused kernel and the CPU oracle.
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "fvad_device.h"
+#include "fvad_internal.h"
+#include "fvad_staged.h"
+
+namespace fvad {
+
+namespace {
+constexpr int kHist = kPitchBuf - kFrame;  // 1248
+constexpr float kScale960 = 1.f / 960;
+
+__device__ __forceinline__ int ticks_of(const StagedArgs &a, int s) {
+  return a.ticks_valid ? a.ticks_valid[s] : a.n_ticks;
+}
+
+// analysis / synthesis window value for index i of the 960-sample window
+__device__ __forceinline__ float win960(const float *__restrict__ hw, int i) {
+  return (i < kFrame) ? hw[i] : hw[kWin - 1 - i];
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_prep2(StagedArgs a) {
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= a.n_streams) return;
+  const int nt = ticks_of(a, s);
+  if (nt <= 0) return;
+  const int C = a.n_channels;
+  float *row = a.xs + (size_t)s * a.L;
+  float *stp = a.state + (size_t)s * st::kWords;
+  for (int i = 0; i < kHist; i++) row[i] = stp[st::kPitch + kFrame + i];
+  float mem0 = stp[st::kHp], mem1 = stp[st::kHp + 1];
+  const float b0 = -2.0f, b1 = 1.0f, a0 = -1.99599f, a1 = 0.99600f;
+  const float scalar = (float)32767;
+  for (int t = 0; t < nt; t++) {
+    float vmin = 1, vmax = 0;
+    for (int c = 0; c < C; c++) {
+      const float4 *in4 = reinterpret_cast<const float4 *>(a.pcm + (((size_t)t * a.n_streams + s) * C + c) * kFrame);
+      float4 *out4 = reinterpret_cast<float4 *>(row + kHist + (size_t)(t * C + c) * kFrame);
+      float sum = 0;
+      for (int i4 = 0; i4 < kFrame / 4; i4++) {
+        const float4 v = in4[i4];
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        float yy[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float v0 = vv[k];
+          sum += v0 * v0;
+          const float xi = a.raw_s16 ? v0 : v0 * scalar;
+          const float yi = xi + mem0;
+          mem0 = (float)(mem1 + (b0 * (double)xi - a0 * (double)yi));
+          mem1 = (float)(b1 * (double)xi - a1 * (double)yi);
+          yy[k] = yi;
+        }
+        out4[i4] = make_float4(yy[0], yy[1], yy[2], yy[3]);
+      }
+      const float vol = sqrtf(sum / (float)kFrame);
+      if (vol < vmin) vmin = vol;
+      if (vol > vmax) vmax = vol;
+    }
+    a.ratio[(size_t)t * a.n_streams + s] = (vmax == 0) ? 0 : vmin / vmax;
+  }
+  // pitch_buf after the last frame = the last 1728 samples of the row
+  const float *last = row + (size_t)(nt * C - 1) * kFrame;
+  for (int i = 0; i < kPitchBuf; i++) stp[st::kPitch + i] = last[i];
+  stp[st::kHp] = mem0;
+  stp[st::kHp + 1] = mem1;
+}
+
+// ---------------------------------------------------------------------------
+// k_fftA: X, Ex, Ly chain, silence, DCT(Ly)
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(NT) k_fftA(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 W[kWin];
+  __shared__ float Ly[kBands + 2];
+  __shared__ int sil;
+  const int tid = threadIdx.x;
+  const Plan *__restrict__ P = a.plan;
+  const float2 *__restrict__ tw = reinterpret_cast<const float2 *>(P->tw960);
+  const float *__restrict__ hw = P->half_window;
+  const int V = a.V, total = a.n_streams * V;
+  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    const int s = f / V, v = f - s * V;
+    if (v >= ticks_of(a, s) * a.n_channels) continue;
+    const float *pb = a.xs + (size_t)s * a.L + (size_t)v * kFrame;
+    for (int i = tid; i < kWin; i += NT) {
+      float val = pb[kPitchBuf - kWin + i];
+      val *= win960(hw, i);
+      W[P->bitrev960[i]] = make_float2(kScale960 * val, kScale960 * 0.0f);
+    }
+    __syncthreads();
+    fft960_stages<NT>(W, tw, tid);
+    float2 *Xg = a.X + (size_t)f * kFreq;
+    for (int k = tid; k < kFreq; k += NT) Xg[k] = W[k];
+    if (tid < kBands) {
+      const float ex = band_sum(W, W, P, tid);
+      a.Ex[(size_t)f * kBands + tid] = ex;
+      Ly[tid] = (float)log10(1e-2 + (double)ex);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float logMax = -2, follow = -2, E = 0;
+      const float *ex = a.Ex + (size_t)f * kBands;
+      for (int i = 0; i < kBands; i++) {
+        const float ly0 = Ly[i];
+        const double bb = (follow - 1.5 > (double)ly0) ? follow - 1.5 : (double)ly0;
+        const double aa = ((double)(logMax - 7) > bb) ? (double)(logMax - 7) : bb;
+        const float ly = (float)aa;
+        Ly[i] = ly;
+        logMax = (logMax > ly) ? logMax : ly;
+        follow = (float)((follow - 1.5 > (double)ly) ? follow - 1.5 : (double)ly);
+        E += ex[i];
+      }
+      sil = ((double)E < 0.04) ? 1 : 0;
+      a.silence[f] = sil;
+    }
+    __syncthreads();
+    if (!sil && tid < kBands) {
+      float sum = 0;
+#pragma unroll
+      for (int j = 0; j < kBands; j++) sum += Ly[j] * P->dct[j * kBands + tid];
+      float val = (float)(sum * sqrt(2. / 22));
+      if (tid == 0) val -= 12;
+      if (tid == 1) val -= 4;
+      a.Lyf[(size_t)f * kBands + tid] = val;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_pitch: everything of pitch_search / remove_doubling that does not depend
+// on the previous frame.  Sequential sums keep C order, one sum per lane; the
+// phase structure assigns independent sums of one phase to lanes of one SIMT
+// loop so they run concurrently.
+// ---------------------------------------------------------------------------
+namespace rec {
+constexpr int kT0 = 0, kXx = 1, kXy = 2, kYyT0 = 3, kNValid = 4;
+constexpr int kK = 8;       // per k=2..15: T1, T1b, s1, s2, yyT1, yyT1b (6 each)
+constexpr int kSpec = 96;   // candidate c (0 = T0, k-1 = T1_k): xcorr at T-1, T, T+1
+constexpr int kSize = 144;
+}  // namespace rec
+
+template <int NT>
+__global__ void __launch_bounds__(NT) k_pitch(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float xlp[kXlp];
+  __shared__ __attribute__((aligned(16))) float xf[kXlp];
+  __shared__ float xc[296];
+  __shared__ float syy_c[148], syy_f[296];
+  __shared__ float yyl[388];
+  __shared__ float ac[8], lpc2[8], sc[8];
+  __shared__ int best[2], T0s, nvalid;
+  __shared__ float recl[rec::kSize];
+  const int tid = threadIdx.x;
+  const int V = a.V, total = a.n_streams * V;
+  const float *xl = xf + (kPitchMax >> 1);
+  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    const int s = f / V, v = f - s * V;
+    if (v >= ticks_of(a, s) * a.n_channels) continue;
+    const float *pb = a.xs + (size_t)s * a.L + (size_t)v * kFrame;  // pitch_buf[0..1728)
+    for (int i = tid; i < kXlp; i += NT)
+      xlp[i] = (i == 0) ? .5f * (.5f * (pb[1]) + pb[0]) : .5f * (.5f * (pb[2 * i - 1] + pb[2 * i + 1]) + pb[2 * i]);
+    __syncthreads();
+    if (tid < 5) {  // _celt_autocorr, lag = tid
+      const int k = tid, fastN = kXlp - 4;
+      float acc = 0;
+#pragma unroll 8
+      for (int i = 0; i < fastN; i++) acc = acc + xlp[i] * xlp[i + k];
+      float d = 0;
+      for (int i = k + fastN; i < kXlp; i++) d = d + xlp[i] * xlp[i - k];
+      ac[k] = acc + d;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float acv[5];
+      for (int i = 0; i < 5; i++) acv[i] = ac[i];
+      acv[0] *= 1.0001f;
+      for (int i = 1; i <= 4; i++) acv[i] -= acv[i] * (.008f * i) * (.008f * i);
+      float lpc[4] = {0, 0, 0, 0};
+      float error = acv[0];
+      if (acv[0] != 0) {
+        for (int i = 0; i < 4; i++) {
+          float r_acc = 0;
+          for (int j = 0; j < i; j++) r_acc += lpc[j] * acv[i - j];
+          r_acc += acv[i + 1];
+          const float r = -r_acc / error;
+          lpc[i] = r;
+          for (int j = 0; j < (i + 1) >> 1; j++) {
+            const float tmp1 = lpc[j], tmp2 = lpc[i - 1 - j];
+            lpc[j] = tmp1 + r * tmp2;
+            lpc[i - 1 - j] = tmp2 + r * tmp1;
+          }
+          error = error - (r * r) * error;
+          if (error < .001f * acv[0]) break;
+        }
+      }
+      float tmp = 1.0f;
+      for (int i = 0; i < 4; i++) {
+        tmp = .9f * tmp;
+        lpc[i] = lpc[i] * tmp;
+      }
+      const float c1 = .8f;
+      lpc2[0] = lpc[0] + .8f;
+      lpc2[1] = lpc[1] + c1 * lpc[0];
+      lpc2[2] = lpc[2] + c1 * lpc[1];
+      lpc2[3] = lpc[3] + c1 * lpc[2];
+      lpc2[4] = c1 * lpc[3];
+    }
+    __syncthreads();
+    {
+      const float n0 = lpc2[0], n1 = lpc2[1], n2 = lpc2[2], n3 = lpc2[3], n4 = lpc2[4];
+      for (int i = tid; i < kXlp; i += NT) {
+        const float m0 = i >= 1 ? xlp[i - 1] : 0.0f, m1 = i >= 2 ? xlp[i - 2] : 0.0f, m2 = i >= 3 ? xlp[i - 3] : 0.0f,
+                    m3 = i >= 4 ? xlp[i - 4] : 0.0f, m4 = i >= 5 ? xlp[i - 5] : 0.0f;
+        float sum = xlp[i];
+        sum = sum + n0 * m0;
+        sum = sum + n1 * m1;
+        sum = sum + n2 * m2;
+        sum = sum + n3 * m3;
+        sum = sum + n4 * m4;
+        xf[i] = sum;
+      }
+    }
+    __syncthreads();
+    // phase G1: coarse xcorr (147 lanes), Syy initial sums, xx — all sequential dot products
+    {
+      const float *pa = nullptr, *pbp = nullptr;
+      int sa = 1, sb = 1, len = 0;
+      float init = 0;
+      if (tid < 147) {
+        pa = xl;
+        sa = 2;
+        pbp = xf + 2 * tid;
+        sb = 2;
+        len = 240;
+      } else if (tid == 147) {
+        pa = xf;
+        pbp = xf;
+        sa = sb = 2;
+        len = 240;
+        init = 1;
+      } else if (tid == 148) {
+        pa = xf;
+        pbp = xf;
+        len = 480;
+        init = 1;
+      } else if (tid == 149) {
+        pa = xl;
+        pbp = xl;
+        len = 480;
+      }
+      float acc = init;
+      if (len) {
+#pragma unroll 4
+        for (int i = 0; i < len; i++) acc = acc + pa[i * sa] * pbp[i * sb];
+      }
+      if (tid < 147)
+        xc[tid] = acc;
+      else if (tid < 150)
+        sc[tid - 147] = acc;  // [0] Syy coarse init, [1] Syy fine init, [2] xx
+    }
+    __syncthreads();
+    // phase G2: energy recurrences (find_best_pitch Syy sequences, remove_doubling yy_lookup)
+    if (tid < 2) {
+      const int ys = tid == 0 ? 2 : 1, len = tid == 0 ? 240 : 480, n = tid == 0 ? 147 : 294;
+      float *out = tid == 0 ? syy_c : syy_f;
+      float Syy = sc[tid];
+#pragma unroll 4
+      for (int i = 0; i < n; i++) {
+        out[i] = Syy;
+        const float ya = xf[(i + len) * ys], yb = xf[i * ys];
+        Syy += ya * ya - yb * yb;
+        Syy = (1 > Syy) ? 1 : Syy;
+      }
+    } else if (tid == 64) {
+      const float xx = sc[2];
+      float yy = xx;
+      yyl[0] = xx;
+#pragma unroll 4
+      for (int i = 1; i <= 384; i++) {
+        yy = yy + xl[-i] * xl[-i] - xl[480 - i] * xl[480 - i];
+        yyl[i] = (0 > yy) ? 0 : yy;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int bst[2] = {0, 1};
+      float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
+      for (int i = 0; i < 147; i++) best_pitch_visit(xc[i], syy_c[i], i, bn0, bn1, bd0, bd1, bst);
+      best[0] = bst[0];
+      best[1] = bst[1];
+    }
+    __syncthreads();
+    {
+      const int bp0 = best[0], bp1 = best[1];
+      for (int i = tid; i < 294; i += NT) xc[i] = 0;
+      __syncthreads();
+      if (tid < 10) {
+        const int i = (tid < 5 ? 2 * bp0 : 2 * bp1) - 2 + (tid % 5);
+        const bool dup = tid >= 5 && abs(i - 2 * bp0) <= 2;
+        if (i >= 0 && i < 294 && !dup) {
+          float sum = 0;
+#pragma unroll 8
+          for (int j = 0; j < 480; j++) sum = sum + xl[j] * xf[i + j];
+          xc[i] = (-1 > sum) ? -1 : sum;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const int bp0 = best[0], bp1 = best[1];
+      int bst[2] = {0, 1};
+      float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
+      int w0lo = 2 * bp0 - 2, w0hi = 2 * bp0 + 2, w1lo = 2 * bp1 - 2, w1hi = 2 * bp1 + 2;
+      if (w1lo < w0lo) {
+        const int t0 = w0lo, t1 = w0hi;
+        w0lo = w1lo;
+        w0hi = w1hi;
+        w1lo = t0;
+        w1hi = t1;
+      }
+      for (int i = max(0, w0lo); i <= min(293, w0hi); i++)
+        best_pitch_visit(xc[i], syy_f[i], i, bn0, bn1, bd0, bd1, bst);
+      for (int i = max(max(0, w1lo), w0hi + 1); i <= min(293, w1hi); i++)
+        best_pitch_visit(xc[i], syy_f[i], i, bn0, bn1, bd0, bd1, bst);
+      int offset;
+      if (bst[0] > 0 && bst[0] < 294 - 1) {
+        const float aa = xc[bst[0] - 1], bb = xc[bst[0]], cc = xc[bst[0] + 1];
+        if ((cc - aa) > .7f * (bb - aa))
+          offset = 1;
+        else if ((aa - cc) > .7f * (bb - cc))
+          offset = -1;
+        else
+          offset = 0;
+      } else {
+        offset = 0;
+      }
+      const int pitch = 2 * bst[0] - offset;
+      int T0 = (kPitchMax - pitch) / 2;
+      if (T0 >= 384) T0 = 383;
+      T0s = T0;
+      int nv = 0;
+      for (int k = 2; k <= 15; k++) {
+        if ((int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k)) < 30) break;
+        nv++;
+      }
+      nvalid = nv;
+    }
+    __syncthreads();
+    // phase G3: remove_doubling inner products for every candidate, plus the
+    // final 3-lag xcorr speculatively for each candidate period
+    {
+      const int T0 = T0s, nv = nvalid;
+      int lag = -100000;
+      if (tid == 0) {
+        lag = T0;
+      } else if (tid < 29) {
+        const int kk = (tid - 1) >> 1, k = kk + 2;
+        if (kk < nv) {
+          const int T1 = (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k));
+          int T1b;
+          if (k == 2)
+            T1b = (T1 + T0 > 384) ? T0 : T0 + T1;
+          else
+            T1b = (int)((unsigned)(2 * second_check(k) * T0 + k) / (unsigned)(2 * k));
+          lag = ((tid - 1) & 1) ? T1b : T1;
+        }
+      } else if (tid < 29 + 45) {
+        const int c = (tid - 29) / 3, m = (tid - 29) % 3;
+        int T = -1;
+        if (c == 0)
+          T = T0;
+        else if (c - 1 < nv)
+          T = (int)((unsigned)(2 * T0 + (c + 1)) / (unsigned)(2 * (c + 1)));
+        if (T >= 0) lag = T + m - 1;
+      }
+      if (lag != -100000) {
+        float acc = 0;
+#pragma unroll 8
+        for (int i = 0; i < 480; i++) acc = acc + xl[i] * xl[i - lag];
+        if (tid == 0)
+          recl[rec::kXy] = acc;
+        else if (tid < 29)
+          recl[rec::kK + ((tid - 1) >> 1) * 6 + 2 + ((tid - 1) & 1)] = acc;
+        else
+          recl[rec::kSpec + (tid - 29)] = acc;
+      }
+      if (tid == 0) {
+        recl[rec::kT0] = __int_as_float(T0);
+        recl[rec::kXx] = sc[2];
+        recl[rec::kYyT0] = yyl[T0];
+        recl[rec::kNValid] = __int_as_float(nv);
+      } else if (tid >= 100 && tid < 114) {
+        const int kk = tid - 100, k = kk + 2;
+        if (kk < nv) {
+          const int T1 = (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k));
+          int T1b;
+          if (k == 2)
+            T1b = (T1 + T0 > 384) ? T0 : T0 + T1;
+          else
+            T1b = (int)((unsigned)(2 * second_check(k) * T0 + k) / (unsigned)(2 * k));
+          recl[rec::kK + kk * 6 + 0] = __int_as_float(T1);
+          recl[rec::kK + kk * 6 + 1] = __int_as_float(T1b);
+          recl[rec::kK + kk * 6 + 4] = yyl[T1];
+          recl[rec::kK + kk * 6 + 5] = yyl[T1b];
+        }
+      }
+    }
+    __syncthreads();
+    float *rg = a.rec + (size_t)f * rec::kSize;
+    for (int i = tid; i < rec::kSize; i += NT) rg[i] = recl[i];
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_select: remove_doubling's sequential selection (one lane per stream).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_select(StagedArgs a) {
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= a.n_streams) return;
+  const int nf = ticks_of(a, s) * a.n_channels;
+  if (nf <= 0) return;
+  float *stp = a.state + (size_t)s * st::kWords;
+  int *istp = reinterpret_cast<int *>(stp);
+  int last_period = istp[st::kLastPeriod];
+  float last_gain = stp[st::kLastGain];
+  for (int v = 0; v < nf; v++) {
+    const size_t f = (size_t)s * a.V + v;
+    const float *r = a.rec + f * rec::kSize;
+    const int T0 = __float_as_int(r[rec::kT0]);
+    const int nv = __float_as_int(r[rec::kNValid]);
+    const int prev_period = last_period / 2;
+    const float prev_gain = last_gain;
+    const float xx = r[rec::kXx];
+    float xy = r[rec::kXy];
+    float yy = r[rec::kYyT0];
+    float best_xy = xy, best_yy = yy;
+    const float g0 = pitch_gain(xy, xx, yy);
+    float gg = g0;
+    int T = T0, cand = 0;
+    for (int k = 2; k <= 15; k++) {
+      const int kk = k - 2;
+      if (kk >= nv) break;
+      const float *q = r + rec::kK + kk * 6;
+      const int T1 = __float_as_int(q[0]);
+      xy = .5f * (q[2] + q[3]);
+      yy = .5f * (q[4] + q[5]);
+      const float g1 = pitch_gain(xy, xx, yy);
+      float cont;
+      if (abs(T1 - prev_period) <= 1)
+        cont = prev_gain;
+      else if (abs(T1 - prev_period) <= 2 && 5 * k * k < T0)
+        cont = .5f * prev_gain;
+      else
+        cont = 0;
+      float thresh;
+      {
+        const float vv = .7f * g0 - cont;
+        thresh = (.3f > vv) ? .3f : vv;
+      }
+      if (T1 < 3 * 30) {
+        const float vv = .85f * g0 - cont;
+        thresh = (.4f > vv) ? .4f : vv;
+      } else if (T1 < 2 * 30) {
+        const float vv = .9f * g0 - cont;
+        thresh = (.5f > vv) ? .5f : vv;
+      }
+      if (g1 > thresh) {
+        best_xy = xy;
+        best_yy = yy;
+        T = T1;
+        gg = g1;
+        cand = k - 1;
+      }
+    }
+    best_xy = (0 > best_xy) ? 0 : best_xy;
+    float pg;
+    if (best_yy <= best_xy)
+      pg = 1.0f;
+    else
+      pg = best_xy / (best_yy + 1);
+    const float x0 = r[rec::kSpec + cand * 3], x1 = r[rec::kSpec + cand * 3 + 1], x2 = r[rec::kSpec + cand * 3 + 2];
+    int offset;
+    if ((x2 - x0) > .7f * (x1 - x0))
+      offset = 1;
+    else if ((x0 - x2) > .7f * (x1 - x2))
+      offset = -1;
+    else
+      offset = 0;
+    if (pg > gg) pg = gg;
+    int pi = 2 * T + offset;
+    if (pi < kPitchMin) pi = kPitchMin;
+    a.pitch[f] = pi;
+    last_period = pi;
+    last_gain = pg;
+  }
+  istp[st::kLastPeriod] = last_period;
+  stp[st::kLastGain] = last_gain;
+}
+
+// ---------------------------------------------------------------------------
+// k_pspec: pitch spectrum P, Ep, normalised Exp, DCT(Exp)[0..5], feature 40
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(NT) k_pspec(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 W[kWin];
+  __shared__ __attribute__((aligned(16))) float2 Xl[kFreq + 1];
+  __shared__ float Ep[kBands + 2], Exp[kBands + 2];
+  const int tid = threadIdx.x;
+  const Plan *__restrict__ P = a.plan;
+  const float2 *__restrict__ tw = reinterpret_cast<const float2 *>(P->tw960);
+  const float *__restrict__ hw = P->half_window;
+  const int V = a.V, total = a.n_streams * V;
+  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    const int s = f / V, v = f - s * V;
+    if (v >= ticks_of(a, s) * a.n_channels) continue;
+    const int pitch = a.pitch[f];
+    const float *pb = a.xs + (size_t)s * a.L + (size_t)v * kFrame;
+    for (int i = tid; i < kWin; i += NT) {
+      float val = pb[kPitchBuf - kWin - pitch + i];
+      val *= win960(hw, i);
+      W[P->bitrev960[i]] = make_float2(kScale960 * val, kScale960 * 0.0f);
+    }
+    const float2 *Xg = a.X + (size_t)f * kFreq;
+    for (int k = tid; k < kFreq; k += NT) Xl[k] = Xg[k];
+    __syncthreads();
+    fft960_stages<NT>(W, tw, tid);
+    float2 *Pg = a.P + (size_t)f * kFreq;
+    for (int k = tid; k < kFreq; k += NT) Pg[k] = W[k];
+    if (tid < kBands)
+      Ep[tid] = band_sum(W, W, P, tid);
+    else if (tid >= 32 && tid < 32 + kBands)
+      Exp[tid - 32] = band_sum(Xl, W, P, tid - 32);
+    __syncthreads();
+    if (tid < kBands) {
+      const float ex = a.Ex[(size_t)f * kBands + tid];
+      const float e = (float)((double)Exp[tid] / sqrt(.001 + (double)(ex * Ep[tid])));
+      Exp[tid] = e;
+      a.Ep[(size_t)f * kBands + tid] = Ep[tid];
+      a.Exp[(size_t)f * kBands + tid] = e;
+    }
+    __syncthreads();
+    if (tid < 6) {
+      float sum = 0;
+#pragma unroll
+      for (int j = 0; j < kBands; j++) sum += Exp[j] * P->dct[j * kBands + tid];
+      float val = (float)(sum * sqrt(2. / 22));
+      if (tid == 0) val = (float)(val - 1.3);
+      if (tid == 1) val = (float)(val - 0.9);
+      a.f34[(size_t)f * 8 + tid] = val;
+    } else if (tid == 32) {
+      a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pitch - 300));
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_rnn: the recurrence (one workgroup per stream, frames in stream order)
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Xl[kFreq + 1];
+  __shared__ float Ex[kBands + 2], Ep[kBands + 2], Exp[kBands + 2];
+  __shared__ float feat[kFeat + 2], g[kBands + 2], rr[kBands + 2], nrm[kBands + 2], newE[kBands + 2],
+      lastg[kBands + 2];
+  __shared__ float ceps[kCeps * kBands];
+  __shared__ float gv[kMaxNeurons], gn[kMaxNeurons], gd[kMaxNeurons];
+  __shared__ float dout[kMaxNeurons], rin[3 * kMaxNeurons], zr[2 * kMaxNeurons], hb[kMaxNeurons];
+  __shared__ float mind[kCeps];
+  __shared__ float vad_s;
+  __shared__ int memid_s;
+  const int tid = threadIdx.x;
+  const int s = blockIdx.x;
+  if (s >= a.n_streams) return;
+  const int nf = ticks_of(a, s) * a.n_channels;
+  if (nf <= 0) return;
+  const Plan *__restrict__ P = a.plan;
+  const float *__restrict__ tt = P->tansig;
+  const DevModel &M = *a.model;
+  float *stp = a.state + (size_t)s * st::kWords;
+  int *istp = reinterpret_cast<int *>(stp);
+  for (int i = tid; i < kCeps * kBands; i += NT) ceps[i] = stp[st::kCepsMem + i];
+  for (int i = tid; i < kBands; i += NT) lastg[i] = stp[st::kLastG + i];
+  for (int i = tid; i < kMaxNeurons; i += NT) {
+    gv[i] = stp[st::kVadGru + i];
+    gn[i] = stp[st::kNoiseGru + i];
+    gd[i] = stp[st::kDenGru + i];
+  }
+  if (tid == 0) memid_s = istp[st::kMemId];
+  __syncthreads();
+  for (int v = 0; v < nf; v++) {
+    const size_t f = (size_t)s * a.V + v;
+    if (a.silence[f]) {
+      if (tid == 0) a.vadf[f] = 0;
+      continue;  // X passes through unmodified, state untouched
+    }
+    const int memid = memid_s;
+    // features: ceps_0 = DCT(Ly) (k_fftA), pitch-correlation features (k_pspec)
+    if (tid < kBands) {
+      const float val = a.Lyf[f * kBands + tid];
+      ceps[memid * kBands + tid] = val;
+      feat[tid] = val;
+    } else if (tid >= 34 && tid < 41) {
+      feat[tid] = a.f34[f * 8 + (tid - 34)];
+    } else if (tid >= 64 && tid < 64 + kBands) {
+      Ex[tid - 64] = a.Ex[f * kBands + tid - 64];
+      Ep[tid - 64] = a.Ep[f * kBands + tid - 64];
+      Exp[tid - 64] = a.Exp[f * kBands + tid - 64];
+    }
+    {
+      const float2 *Xg = a.X + f * kFreq;
+      for (int k = tid; k < kFreq; k += NT) Xl[k] = Xg[k];
+    }
+    __syncthreads();
+    if (tid < 6) {
+      const float *c0 = ceps + memid * kBands;
+      const float *c1 = ceps + ((memid < 1) ? kCeps + memid - 1 : memid - 1) * kBands;
+      const float *c2 = ceps + ((memid < 2) ? kCeps + memid - 2 : memid - 2) * kBands;
+      const int i = tid;
+      feat[i] = c0[i] + c1[i] + c2[i];
+      feat[kBands + i] = c0[i] - c2[i];
+      feat[kBands + 6 + i] = c0[i] - 2 * c1[i] + c2[i];
+    } else if (tid >= 32 && tid < 32 + kCeps) {
+      const int i = tid - 32;
+      float mindist = 1e15f;
+      for (int j = 0; j < kCeps; j++) {
+        float dist = 0;
+#pragma unroll
+        for (int k = 0; k < kBands; k++) {
+          const float tmp = ceps[i * kBands + k] - ceps[j * kBands + k];
+          dist += tmp * tmp;
+        }
+        if (j != i) mindist = (mindist < dist) ? mindist : dist;
+      }
+      mind[i] = mindist;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float sv = 0;
+      for (int i = 0; i < kCeps; i++) sv += mind[i];
+      feat[41] = (float)(sv / kCeps - 2.1);
+      int mid = memid + 1;
+      if (mid == kCeps) mid = 0;
+      memid_s = mid;
+    }
+    __syncthreads();
+    // compute_rnn
+    dense_layer<NT>(M.in_dense, feat, dout, tt, tid);
+    __syncthreads();
+    gru_gates<NT>(M.vad, dout, gv, zr, tt, tid);
+    __syncthreads();
+    gru_out<NT>(M.vad, dout, gv, zr, hb, tt, tid);
+    __syncthreads();
+    {
+      const int nd = M.in_dense.nout, nvd = M.vad.nout;
+      for (int i = tid; i < nvd; i += NT) gv[i] = hb[i];
+      __syncthreads();
+      for (int i = tid; i < nd + nvd + kFeat; i += NT)
+        rin[i] = (i < nd) ? dout[i] : (i < nd + nvd) ? gv[i - nd] : feat[i - nd - nvd];
+      if (tid == NT - 1) {
+        const DevDense &d = M.vad_out;
+        float sum = d.b[0];
+        for (int j = 0; j < d.nin; j++) sum += d.w[j * d.nout] * gv[j];
+        vad_s = activate(tt, d.act, kWs * sum);
+      }
+    }
+    __syncthreads();
+    gru_gates<NT>(M.noise, rin, gn, zr, tt, tid);
+    __syncthreads();
+    gru_out<NT>(M.noise, rin, gn, zr, hb, tt, tid);
+    __syncthreads();
+    {
+      const int nvd = M.vad.nout, nn = M.noise.nout;
+      for (int i = tid; i < nn; i += NT) gn[i] = hb[i];
+      __syncthreads();
+      for (int i = tid; i < nvd + nn + kFeat; i += NT)
+        rin[i] = (i < nvd) ? gv[i] : (i < nvd + nn) ? gn[i - nvd] : feat[i - nvd - nn];
+    }
+    __syncthreads();
+    gru_gates<NT>(M.den, rin, gd, zr, tt, tid);
+    __syncthreads();
+    gru_out<NT>(M.den, rin, gd, zr, hb, tt, tid);
+    __syncthreads();
+    for (int i = tid; i < M.den.nout; i += NT) gd[i] = hb[i];
+    __syncthreads();
+    dense_layer<NT>(M.den_out, gd, g, tt, tid);
+    __syncthreads();
+    // pitch_filter
+    if (tid < kBands) {
+      const int i = tid;
+      float r;
+      if (Exp[i] > g[i])
+        r = 1;
+      else
+        r = (float)((double)((Exp[i] * Exp[i]) * (1 - (g[i] * g[i]))) /
+                    (.001 + (double)((g[i] * g[i]) * (1 - (Exp[i] * Exp[i])))));
+      float cl = (0 > r) ? 0 : r;
+      cl = (1 < cl) ? 1 : cl;
+      r = (float)sqrt((double)cl);
+      r = (float)((double)r * sqrt((double)Ex[i] / (1e-8 + (double)Ep[i])));
+      rr[i] = r;
+    }
+    if (tid == 0) a.vadf[f] = vad_s;
+    __syncthreads();
+    {
+      const float2 *Pg = a.P + f * kFreq;
+      for (int k = tid; k < kFreq; k += NT) {
+        const float rf = interp_gain(rr, P, k);
+        const float2 pk = Pg[k];
+        Xl[k].x += rf * pk.x;
+        Xl[k].y += rf * pk.y;
+      }
+    }
+    __syncthreads();
+    if (tid < kBands) newE[tid] = band_sum(Xl, Xl, P, tid);
+    __syncthreads();
+    if (tid < kBands) {
+      const int i = tid;
+      nrm[i] = (float)sqrt((double)Ex[i] / (1e-8 + (double)newE[i]));
+      const float al = .6f * lastg[i];
+      const float gi = (g[i] > al) ? g[i] : al;
+      g[i] = gi;
+      lastg[i] = gi;
+    }
+    __syncthreads();
+    {
+      float2 *Xg = a.X + f * kFreq;
+      for (int k = tid; k < kFreq; k += NT) {
+        const float nf2 = interp_gain(nrm, P, k);
+        float2 val = Xl[k];
+        val.x *= nf2;
+        val.y *= nf2;
+        const float gf = interp_gain(g, P, k);
+        val.x *= gf;
+        val.y *= gf;
+        Xg[k] = val;
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < kCeps * kBands; i += NT) stp[st::kCepsMem + i] = ceps[i];
+  for (int i = tid; i < kBands; i += NT) stp[st::kLastG + i] = lastg[i];
+  for (int i = tid; i < kMaxNeurons; i += NT) {
+    stp[st::kVadGru + i] = gv[i];
+    stp[st::kNoiseGru + i] = gn[i];
+    stp[st::kDenGru + i] = gd[i];
+  }
+  if (tid == 0) istp[st::kMemId] = memid_s;
+}
+
+// ---------------------------------------------------------------------------
+// k_synth: inverse transform (forward FFT of the Hermitian extension), window
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(NT) k_synth(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 W[kWin];
+  const int tid = threadIdx.x;
+  const Plan *__restrict__ P = a.plan;
+  const float2 *__restrict__ tw = reinterpret_cast<const float2 *>(P->tw960);
+  const float *__restrict__ hw = P->half_window;
+  const int V = a.V, total = a.n_streams * V;
+  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    const int s = f / V, v = f - s * V;
+    if (v >= ticks_of(a, s) * a.n_channels) continue;
+    const float2 *Xg = a.X + (size_t)f * kFreq;
+    for (int i = tid; i < kWin; i += NT) {
+      float2 val;
+      if (i < kFreq) {
+        val = Xg[i];
+      } else {
+        const float2 c = Xg[kWin - i];
+        val = make_float2(c.x, -c.y);
+      }
+      W[P->bitrev960[i]] = make_float2(kScale960 * val.x, kScale960 * val.y);
+    }
+    __syncthreads();
+    fft960_stages<NT>(W, tw, tid);
+    float *y = a.ys + (size_t)f * kWin;
+    for (int i = tid; i < kWin; i += NT) {
+      const float yv = (i == 0) ? kWin * W[0].x : kWin * W[kWin - i].x;
+      y[i] = yv * win960(hw, i);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_ola: out = x[0..479] + synthesis_mem; denoised * 1/32767; re-block ring;
+// per-tick vad_low (min over channels in channel order)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_ola(StagedArgs a) {
+  const int C = a.n_channels, V = a.V;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)a.n_streams * V * kFrame;
+  if (gid >= total) return;
+  const int i = (int)(gid % kFrame);
+  const long long fv = gid / kFrame;
+  const int s = (int)(fv / V), v = (int)(fv - (long long)s * V);
+  const int nt = ticks_of(a, s);
+  if (v >= nt * C) return;
+  const int t = v / C, c = v - t * C;
+  const float *stp = a.state + (size_t)s * st::kWords;
+  const size_t f = (size_t)s * V + v;
+  const float prev = (v == 0) ? stp[st::kSyn + i] : a.ys[(f - 1) * kWin + kFrame + i];
+  const float o = a.ys[f * kWin + i] + prev;
+  const float dn = a.raw_s16 ? o : o * (1.0f / (float)32767);
+  const int frames_done = reinterpret_cast<const int *>(stp)[st::kFramesDone];
+  const long long absi = (long long)(frames_done + t) * kFrame + i;
+  a.ring[((size_t)s * C + c) * a.ring_len + (size_t)(absi % a.ring_len)] = dn;
+  if (a.out_den) a.out_den[(((size_t)t * a.n_streams + s) * C + c) * kFrame + i] = dn;
+  if (i == 0 && c == 0) {
+    float vad_low = 1;
+    for (int cc = 0; cc < C; cc++) {
+      const float vv = a.vadf[(size_t)s * V + t * C + cc];
+      if (vv < vad_low) vad_low = vv;
+    }
+    a.out_vad[(size_t)t * a.n_streams + s] = vad_low;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_winmeta: window completion bookkeeping (VAD.zig:298-348), lane per stream
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= a.n_streams) return;
+  const int nt = ticks_of(a, s);
+  int *wt = a.win_tick + (size_t)s * a.wmax;
+  long long *wsx = a.win_start + (size_t)s * a.wmax;
+  int j = 0;
+  if (nt > 0) {
+    float *stp = a.state + (size_t)s * st::kWords;
+    int *istp = reinterpret_cast<int *>(stp);
+    int fd = istp[st::kFramesDone];
+    float vol = stp[st::kVolAcc];
+    const int FB = a.plan->nfft_b;
+    for (int t = 0; t < nt; t++) {
+      const size_t o = (size_t)t * a.n_streams + s;
+      const float ratio = a.ratio[o];
+      const long long a0 = (long long)fd * kFrame;
+      const long long wdone = a0 / FB;
+      const long long next_end = (wdone + 1) * FB;
+      const bool complete = a0 + kFrame >= next_end;
+      if (complete) {
+        const int r = (int)(next_end - a0);
+        vol += ratio * ((float)r / (float)FB);
+        a.out_win_ratio[o] = vol;
+        a.out_win_vad[o] = a.out_vad[o];
+        vol = 0;
+        if (kFrame - r > 0) vol += ratio * ((float)(kFrame - r) / (float)FB);
+        wt[j] = t;
+        wsx[j] = wdone * FB;
+        j++;
+      } else {
+        vol += ratio * ((float)kFrame / (float)FB);
+        a.out_win_ratio[o] = 0.0f;
+        a.out_win_vad[o] = 0.0f;
+      }
+      a.out_win_flag[o] = complete ? 1 : 0;
+      fd++;
+    }
+    istp[st::kFramesDone] = fd;
+    stp[st::kVolAcc] = vol;
+    // synthesis_mem for the next launch = second half of the last frame's window
+    const float *yl = a.ys + ((size_t)s * a.V + (size_t)nt * a.n_channels - 1) * kWin + kFrame;
+    for (int i = 0; i < kFrame; i++) stp[st::kSyn + i] = yl[i];
+  }
+  for (; j < a.wmax; j++) wt[j] = -1;
+}
+
+// ---------------------------------------------------------------------------
+// k_fftb: one workgroup per (stream, completed window): FFT B per channel
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(NT) k_fftb(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 W[kMaxFftB / 2];
+  __shared__ float mag[256];
+  const int tid = threadIdx.x;
+  const int s = blockIdx.x / a.wmax, j = blockIdx.x - s * a.wmax;
+  if (s >= a.n_streams) return;
+  const int t = a.win_tick[(size_t)s * a.wmax + j];
+  if (t < 0) return;
+  const long long wstart = a.win_start[(size_t)s * a.wmax + j];
+  const Plan *__restrict__ P = a.plan;
+  const int nc = P->ncfft_b, C = a.n_channels;
+  const float2 *__restrict__ twb = reinterpret_cast<const float2 *>(P->twb);
+  const float2 *__restrict__ sup = reinterpret_cast<const float2 *>(P->superb);
+  const size_t o = (size_t)t * a.n_streams + s;
+  for (int c = 0; c < C; c++) {
+    const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
+    for (int k = tid; k < nc; k += NT) {
+      const int n = P->permb[k];
+      const float t0 = ring[(wstart + 2 * n) % a.ring_len] * P->hannb[2 * n];
+      const float t1 = ring[(wstart + 2 * n + 1) % a.ring_len] * P->hannb[2 * n + 1];
+      W[k] = make_float2(t0, t1);
+    }
+    __syncthreads();
+    for (int stg = 0, m = 1; stg < P->stages_b; stg++, m *= 4) {
+      const int fstride = nc / (4 * m);
+      for (int q = tid; q < nc / 4; q += NT) {
+        const int blk = q / m, u = q - blk * m;
+        bfly4(W + blk * 4 * m + u, m, twb[u * fstride], twb[2 * u * fstride], twb[3 * u * fstride]);
+      }
+      __syncthreads();
+    }
+    const int lo = a.bin_lo_all, hi = a.bin_hi_all;
+    for (int k = lo + tid; k <= hi; k += NT) {
+      float re, imv;
+      if (k == 0) {
+        re = W[0].x + W[0].y;
+        imv = 0;
+      } else if (k == nc) {
+        re = W[0].x - W[0].y;
+        imv = 0;
+      } else {
+        const int kk = (k < nc / 2) ? k : nc - k;
+        const float2 fpk = W[kk];
+        const float2 fpnk = make_float2(W[nc - kk].x, -W[nc - kk].y);
+        const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
+        const float2 tw2 = cmul(f2k, sup[kk - 1]);
+        if (k < nc / 2) {
+          re = (f1k.x + tw2.x) * ((float).5);
+          imv = (f1k.y + tw2.y) * ((float).5);
+        } else {
+          re = (f1k.x - tw2.x) * ((float).5);
+          imv = (tw2.y - f1k.y) * ((float).5);
+        }
+      }
+      const float r2 = re * re, i2 = imv * imv;
+      mag[k - lo] = sqrtf(r2 + i2) * P->norm_b;
+    }
+    __syncthreads();
+    if (tid < a.n_bands) {
+      float acc = 0.0f;
+      for (int k = a.band_lo[tid]; k <= a.band_hi[tid]; k++) acc += mag[k - lo];
+      a.out_band[(o * C + c) * a.n_bands + tid] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launcher
+// ---------------------------------------------------------------------------
+const char *staged_kernel_name(int i) {
+  static const char *const names[kStagedKernels] = {"k_prep2", "k_fftA",  "k_pitch", "k_select", "k_pspec",
+                                                     "k_rnn",   "k_synth", "k_ola",   "k_winmeta", "k_fftb"};
+  return (i >= 0 && i < kStagedKernels) ? names[i] : nullptr;
+}
+
+hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t stream, hipEvent_t *ev) {
+  constexpr int NT = 256;
+  const int lane_blocks = (a.n_streams + 63) / 64;
+  const long long frames = (long long)a.n_streams * a.V;
+  const int g = (int)std::min<long long>(frames, grid_frames);
+  (void)hipGetLastError();
+  auto rec = [&](int k) {
+    if (ev) (void)hipEventRecord(ev[k], stream);
+  };
+  rec(0);
+  hipLaunchKernelGGL(k_prep2, dim3(lane_blocks), dim3(64), 0, stream, a);
+  rec(1);
+  hipLaunchKernelGGL(k_fftA<NT>, dim3(g), dim3(NT), 0, stream, a);
+  rec(2);
+  hipLaunchKernelGGL(k_pitch<NT>, dim3(g), dim3(NT), 0, stream, a);
+  rec(3);
+  hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(64), 0, stream, a);
+  rec(4);
+  hipLaunchKernelGGL(k_pspec<NT>, dim3(g), dim3(NT), 0, stream, a);
+  rec(5);
+  hipLaunchKernelGGL(k_rnn<NT>, dim3(a.n_streams), dim3(NT), 0, stream, a);
+  rec(6);
+  hipLaunchKernelGGL(k_synth<NT>, dim3(g), dim3(NT), 0, stream, a);
+  rec(7);
+  const long long ola_threads = frames * kFrame;
+  hipLaunchKernelGGL(k_ola, dim3((unsigned)((ola_threads + 255) / 256)), dim3(256), 0, stream, a);
+  rec(8);
+  hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(64), 0, stream, a);
+  rec(9);
+  hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
+  rec(10);
+  return hipGetLastError();
+}
+
+}  // namespace fvad

@@ -34,7 +34,12 @@ class FvadError(RuntimeError):
 class EngineConfig(C.Structure):
     _fields_ = [("n_streams", C.c_int), ("n_channels", C.c_int), ("device", C.c_int), ("sample_rate", C.c_int),
                 ("fft_size", C.c_int), ("max_ticks", C.c_int), ("n_bands", C.c_int),
-                ("band_lo", C.c_int * MAX_BANDS), ("band_hi", C.c_int * MAX_BANDS), ("want_denoised", C.c_int)]
+                ("band_lo", C.c_int * MAX_BANDS), ("band_hi", C.c_int * MAX_BANDS), ("want_denoised", C.c_int),
+                ("mode", C.c_int)]
+
+
+MODE_STAGED, MODE_FUSED = 0, 1
+MAX_TIMES = 16
 
 
 class Outputs(C.Structure):
@@ -116,6 +121,7 @@ SYMBOLS = [
     ("fvad_engine_run_resident", C.c_int, [C.c_void_p, C.c_int]),
     ("fvad_engine_sync", C.c_int, [C.c_void_p]),
     ("fvad_engine_kernel_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+    ("fvad_engine_kernel_name", C.c_char_p, [C.c_void_p, C.c_int]),
     ("fvad_engine_clear_times", C.c_int, [C.c_void_p]),
     ("fvad_engine_fetch", C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     ("fvad_vadm_config_default", None, [C.c_void_p]),
@@ -206,7 +212,7 @@ class Engine:
     """Batched hot path for a partition of streams on one GPU."""
 
     def __init__(self, model, n_streams, n_channels=2, device=0, max_ticks=100, fft_size=2048, bands=((4, 64),),
-                 want_denoised=False):
+                 want_denoised=False, mode="staged"):
         cfg = EngineConfig()
         lib().fvad_engine_config_default(C.byref(cfg), n_streams, n_channels)
         cfg.device = device
@@ -217,6 +223,7 @@ class Engine:
             cfg.band_lo[i] = lo
             cfg.band_hi[i] = hi
         cfg.want_denoised = int(want_denoised)
+        cfg.mode = {"staged": MODE_STAGED, "fused": MODE_FUSED}[mode]
         self.cfg = cfg
         self.model = model
         h = C.c_void_p()
@@ -261,10 +268,17 @@ class Engine:
         _check(lib().fvad_engine_sync(self.h), "fvad_engine_sync")
 
     def kernel_times(self):
-        ms = (C.c_double * 3)()
+        """{"total_ms": push average, "kernels": {name: ms average}, "runs": n}"""
+        ms = (C.c_double * MAX_TIMES)()
         n = C.c_int()
         _check(lib().fvad_engine_kernel_times(self.h, ms, C.byref(n)), "fvad_engine_kernel_times")
-        return {"prep_ms": ms[0], "frame_ms": ms[1], "total_ms": ms[2], "runs": n.value}
+        names = []
+        while len(names) < MAX_TIMES - 1:
+            nm = lib().fvad_engine_kernel_name(self.h, len(names))
+            if nm is None:
+                break
+            names.append(nm.decode())
+        return {"total_ms": ms[0], "kernels": {nm: ms[1 + i] for i, nm in enumerate(names)}, "runs": n.value}
 
     def clear_times(self):
         _check(lib().fvad_engine_clear_times(self.h), "fvad_engine_clear_times")

@@ -88,6 +88,38 @@ def prep_kernel_bytes(n_streams, n_channels, n_ticks):
     return frames * FRAME * 4 * 2 + n_streams * n_ticks * 4 + n_streams * 16
 
 
+def staged_kernels(n_channels=2, fft_size=2048):
+    """Per channel-frame algorithmic flops and HBM bytes of each staged kernel
+    (fvad_staged.hip).  Flops re-partition phases() (the sum is unchanged);
+    bytes are the kernel's compulsory reads + writes of its inputs/outputs in
+    the staged layout.  k_pitch's speculative work (the
+    final 3-lag xcorr for every candidate instead of the selected one) is
+    counted once, as the reference computes it."""
+    p = phases(n_channels, fft_size)
+    C = n_channels
+    feat = p["features (log10, DCTs, cepstra, spectral variability)"]
+    dct_ly = 22 * 44 + 22 * 2
+    dct_exp = 6 * 44 + 6 * 2
+    spec = 481 * 8  # one complex spectrum
+    k = {
+        "k_prep2": (p["prep: s16 scale + HP biquad + rms"], 480 * 4 * 2 + 4.0 / C),
+        "k_fftA": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly,
+                   960 * 4 + spec + 22 * 4 * 2 + 4),
+        "k_pitch": (p["pitch downsample + autocorr + LPC + FIR5"] + p["coarse xcorr 147x240 + find_best_pitch"] +
+                    p["fine xcorr <=10x480 + find_best_pitch"] + p["remove_doubling"] - 14 * 12,
+                    1728 * 4 + 144 * 4),
+        "k_select": (14 * 12, 144 * 4 + 4),
+        "k_pspec": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
+        "k_rnn": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"] + p["pitch filter + gains"],
+                  22 * 4 * 4 + 8 * 4 + 3 * spec + 4),
+        "k_synth": (p["synthesis (scale, FFT A, window, OLA, 1/32767)"] - 960, spec + 960 * 4),
+        "k_ola": (960, 960 * 4 + 480 * 4 + 4.0 / C),
+        "k_winmeta": (0.0, 4 * 4.0 / C),
+        "k_fftb": (p["re-block + FFT B share"], 480 * 4 + 4),
+    }
+    return {n: {"flops": f, "bytes": b} for n, (f, b) in k.items()}
+
+
 if __name__ == "__main__":
     for k, v in phases().items():
         print("%-58s %9d" % (k, v))

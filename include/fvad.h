@@ -109,7 +109,14 @@ typedef struct {
   int band_lo[FVAD_MAX_BANDS]; /* inclusive FFT-B bin ranges (FFT.freqToBin) */
   int band_hi[FVAD_MAX_BANDS];
   int want_denoised;    /* keep denoised PCM (VAD.zig temp_denoiser_segment) */
+  int mode;             /* FVAD_MODE_STAGED (default) or FVAD_MODE_FUSED; identical results */
 } fvad_engine_config;
+
+/* staged: time-parallel frame kernels + a thin per-stream recurrence kernel;
+ * fused: one workgroup runs every frame of a stream (lower memory). */
+#define FVAD_MODE_STAGED 0
+#define FVAD_MODE_FUSED 1
+#define FVAD_MAX_TIMES 16
 
 void fvad_engine_config_default(fvad_engine_config *cfg, int n_streams, int n_channels);
 
@@ -142,9 +149,12 @@ int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t stream_id_b
 /* run one push over the resident device input, async on the engine stream */
 int fvad_engine_run_resident(fvad_engine *e, int n_ticks);
 int fvad_engine_sync(fvad_engine *e);
-/* average per-launch kernel durations (ms) of the last n resident runs,
- * measured with HIP events on the engine's stream: [0] prep, [1] frame, [2] total */
+/* average per-launch kernel durations (ms) of the timed resident runs,
+ * measured with HIP events on the engine's stream.  ms_avg holds
+ * FVAD_MAX_TIMES doubles: [0] whole push, [1 + i] kernel i (names below). */
 int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_runs);
+/* name of kernel i of this engine's mode, NULL past the last one */
+const char *fvad_engine_kernel_name(const fvad_engine *e, int i);
 int fvad_engine_clear_times(fvad_engine *e);
 /* copy outputs of the last resident run to host */
 int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out);

@@ -36,7 +36,8 @@ def assert_stream_equal(ref, got, ch):
     assert np.array_equal(wi["vad"], got["win_vad"])
 
 
-def test_engine_bit_exact_ragged(fvad_mod, oracle_mod, models):
+@pytest.mark.parametrize("mode", ["staged", "fused"])
+def test_engine_bit_exact_ragged(fvad_mod, oracle_mod, models, mode):
     """Stereo streams of different (non-multiple-of-480) lengths, pushed in
     ragged chunks: every per-frame and per-window output is bit-identical."""
     m, om = models
@@ -44,14 +45,15 @@ def test_engine_bit_exact_ragged(fvad_mod, oracle_mod, models):
     ids = [0, 1, 19, 42]
     streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip(ids, secs)]
     ref = pu.oracle_run(oracle_mod, om, streams)
-    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=37, want_denoised=True)
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=37, want_denoised=True, mode=mode)
     got = pu.engine_run(fvad_mod, eng, streams, 37)
     for r, g in zip(ref, got):
         assert_stream_equal(r, g, 2)
 
 
+@pytest.mark.parametrize("mode", ["staged", "fused"])
 @pytest.mark.parametrize("n_channels,fft_size", [(1, 2048), (2, 512), (3, 2048)])
-def test_engine_channels_and_fft_size(fvad_mod, oracle_mod, models, n_channels, fft_size):
+def test_engine_channels_and_fft_size(fvad_mod, oracle_mod, models, n_channels, fft_size, mode):
     m, om = models
     streams = [fvad_mod.synth_stream(i, 48000 * 6, n_channels)[0] for i in (5, 6)]
     ref = []
@@ -63,10 +65,31 @@ def test_engine_channels_and_fft_size(fvad_mod, oracle_mod, models, n_channels, 
         fr, wi = p.trace()
         ref.append({"frames": fr, "windows": wi, "denoised": p.tden[:, :frames * 480].copy()})
     bins = (1, 16) if fft_size == 512 else (4, 64)
-    eng = fvad_mod.Engine(m, 2, n_channels, max_ticks=50, fft_size=fft_size, bands=(bins,), want_denoised=True)
+    eng = fvad_mod.Engine(m, 2, n_channels, max_ticks=50, fft_size=fft_size, bands=(bins,), want_denoised=True,
+                          mode=mode)
     got = pu.engine_run(fvad_mod, eng, streams, 50)
     for r, g in zip(ref, got):
         assert_stream_equal(r, g, n_channels)
+
+
+def test_staged_equals_fused_resident(fvad_mod, models):
+    """Both engine modes on the same resident synthetic batch (256 stereo
+    streams x 3 pushes of 40 ticks): every output bit-identical."""
+    m, _ = models
+    outs = []
+    for mode in ("staged", "fused"):
+        eng = fvad_mod.Engine(m, 256, 2, max_ticks=40, mode=mode)
+        eng.load_synthetic(40, 7)
+        res = []
+        for _ in range(3):
+            eng.run_resident(40)
+            res.append(eng.fetch(40))
+        outs.append(res)
+    for a, b in zip(*outs):
+        for k in ("vad", "ratio", "win_flag", "win_ratio", "win_vad"):
+            assert np.array_equal(a[k], b[k]), (k, pu.first_mismatch(a[k], b[k]))
+        wf = a["win_flag"].astype(bool)  # band sums are only written for completed windows
+        assert wf.sum() > 0 and np.array_equal(a["band"][wf], b["band"][wf])
 
 
 def test_engine_multiple_bands(fvad_mod, oracle_mod, models):
