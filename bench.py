@@ -49,32 +49,53 @@ def parse():
     return ap.parse_args()
 
 
-def dist_setup(n_gpus):
+def dist_setup(n_gpus, backend="nccl"):
+    """One process per GPU (torch.distributed.run env).  backend "gloo" is
+    used by the CPU tests of this logic (tests/test_dist_cpu.py)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         return rank, world, local, dist, torch
     return rank, world, local, None, None
+
+
+def _on_gpu(dist):
+    return dist.get_backend() == "nccl"
 
 
 def barrier(dist, torch):
     if dist is not None:
         dist.barrier()
-        torch.cuda.synchronize()
+        if _on_gpu(dist):
+            torch.cuda.synchronize()
 
 
 def max_over_ranks(x, dist, torch):
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if _on_gpu(dist) else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def stream_partition(rank, streams_per_gpu):
+    """Weak scaling: rank r owns synthetic stream ids [r*B, (r+1)*B) (configs[3]/[4]);
+    streams are independent, so there is no data-path collective."""
+    return rank * streams_per_gpu, streams_per_gpu
+
+
+def aggregate_rate(frames_per_rank_step, world, steps, elapsed_max):
+    """Whole-job channel-frames/s: every rank's frames over the slowest rank's time."""
+    return frames_per_rank_step * world * steps / elapsed_max
 
 
 def cpu_baseline(args):
@@ -117,7 +138,8 @@ def main():
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     model = fvad.Model(seed=1)
     eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=args.mode)
-    eng.load_synthetic(T, base=rank * B)
+    base, _ = stream_partition(rank, B)
+    eng.load_synthetic(T, base=base)
 
     for _ in range(args.warmup):
         eng.run_resident(T)
@@ -133,8 +155,7 @@ def main():
     elapsed = max_over_ranks(elapsed, dist, torch)
     kt = eng.kernel_times()
 
-    frames_per_step = B * Ch * T * world
-    value = frames_per_step * args.steps / elapsed
+    value = aggregate_rate(B * Ch * T, world, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
     if rank != 0:

@@ -1,0 +1,54 @@
+"""world_size-2 gloo run of bench.py's multi-GPU logic on CPU: rendezvous on
+127.0.0.1, disjoint stream partitions per rank, barrier, max-over-ranks timing
+and the whole-job rate (the N>1 path the driver launches with
+torch.distributed.run, minus the GPU)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.path.insert(0, ROOT)
+    import bench
+    r, w, local, dist, torch = bench.dist_setup(world, backend="gloo")
+    base, n = bench.stream_partition(r, 2048)
+    bench.barrier(dist, torch)
+    elapsed = 1.0 + r  # rank 1 is the slow one
+    mx = bench.max_over_ranks(elapsed, dist, torch)
+    ids = torch.tensor([base, base + n], dtype=torch.int64)
+    gathered = [torch.zeros(2, dtype=torch.int64) for _ in range(w)]
+    dist.all_gather(gathered, ids)
+    q.put((r, w, mx, [g.tolist() for g in gathered], bench.aggregate_rate(2048 * 2 * 50, w, 10, mx)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_partition_and_timing():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r, w, mx, parts, rate in res:
+        assert w == 2 and mx == 2.0
+        assert parts == [[0, 2048], [2048, 4096]]  # disjoint, contiguous stream ids
+        assert rate == pytest.approx(2048 * 2 * 50 * 2 * 10 / 2.0)

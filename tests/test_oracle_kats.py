@@ -7,63 +7,59 @@ import pytest
 
 # ---------------- reference unit tests, ported as expected values ----------------
 
+import json
+import os
+
+REF = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_vectors.json")))
+
+
 def test_segment_writer_reference_vector(oracle_mod):
     """SegmentWriter.zig:124-175 — pack a {1}{2,3,4} split source into 10 samples."""
     import ctypes as C
     O = oracle_mod
-    buf = np.zeros(10, np.float32)
+    v = REF["segment_writer"]
+    buf = np.zeros(v["buffer_len"], np.float32)
 
     class SW(C.Structure):
         _fields_ = [("buf", C.c_void_p), ("len", C.c_size_t), ("write_index", C.c_size_t), ("index", C.c_uint64)]
 
-    w = SW(buf.ctypes.data, 10, 0, 0)
-    first = np.array([1], np.float32)
-    second = np.array([2, 3, 4], np.float32)
-
-    def write(off):
-        return O.lib().ora_segwriter_write(C.byref(w), O.fptr(first), 1, O.fptr(second), 3, off, -1)
-
-    assert write(0) == 4
-    assert write(2) == 2
-    assert write(1) == 3
-    assert w.write_index == 9
-    assert write(2) == 1
-    assert write(3) == 0
-    assert buf.tolist() == [1, 2, 3, 4, 3, 4, 2, 3, 4, 3]
+    w = SW(buf.ctypes.data, v["buffer_len"], 0, 0)
+    first = np.array(v["first"], np.float32)
+    second = np.array(v["second"], np.float32)
+    for k, (off, expect) in enumerate(v["writes"]):
+        got = O.lib().ora_segwriter_write(C.byref(w), O.fptr(first), len(first), O.fptr(second), len(second), off,
+                                          -1)
+        assert got == expect
+        if k == 2:
+            assert w.write_index == v["write_index_after_third"]
+    assert buf.tolist() == v["final_buffer"]
 
 
 def test_multi_ring_buffer_reference_vectors(oracle_mod):
     """MultiRingBuffer.zig:203-249 — eight wrap-around write cases on capacity 5."""
     import ctypes as C
     O = oracle_mod
+    v = REF["multi_ring_buffer"]
 
     class Ring(C.Structure):
         _fields_ = [("buf", C.c_void_p), ("capacity", C.c_size_t), ("total_write_count", C.c_uint64)]
 
-    pcm = np.zeros(5, np.int32)
-    r = Ring(pcm.ctypes.data, 5, 0)
-
-    def write(src, off, n):
-        a = np.array(src, np.int32)
-        O.lib().ora_ring_write(C.byref(r), a.ctypes.data_as(C.POINTER(C.c_int32)), len(a), off, n)
-        return pcm.tolist()
-
-    assert write([0, 1, 2, 9, 9, 9], 0, 2) == [0, 1, 0, 0, 0]
-    assert write([0, 1, 2, 9, 9, 9], 1, 1) == [0, 1, 1, 0, 0]
-    assert write([4, 5, 6, 7, 8, 9], 0, 9999) == [6, 7, 8, 9, 5]
-    assert write([2, 3, 4], 0, 9999) == [3, 4, 8, 9, 2]
-    assert write([0, 0, 0, 0, 0, 50, 60, 70, 80, 90], 0, 9999) == [80, 90, 50, 60, 70]
-    assert write([-1, 0, 2, 0], 0, 9999) == [0, 90, -1, 0, 2]
-    assert write([1, 2, 3, 4, 5, 6, 7, 8, 9, -1, -2], 4, 3) == [0, 5, 6, 7, 2]
-    assert write([1, 2, 3, 4, 5, 6, 7, 8, 9, -1, -2], 8, 3) == [-1, -2, 6, 7, 9]
+    pcm = np.zeros(v["capacity"], np.int32)
+    r = Ring(pcm.ctypes.data, v["capacity"], 0)
+    for st in v["steps"]:
+        a = np.array(st["src"], np.int32)
+        O.lib().ora_ring_write(C.byref(r), a.ctypes.data_as(C.POINTER(C.c_int32)), len(a), st["offset"], st["n"])
+        assert pcm.tolist() == st["expect"]
 
 
-@pytest.mark.parametrize("vad,expected", [((1, 6), 0.0), ((1, 10), 3.0)])
-def test_calc_false_positive_reference_vectors(oracle_mod, vad, expected):
+@pytest.mark.parametrize("case", REF["calc_false_positive"]["cases"])
+def test_calc_false_positive_reference_vectors(oracle_mod, case):
     """statistics.zig:472-546 — refs [2,3],[4,5], extrude 2/2, fill gaps 2."""
-    fp = oracle_mod.calc_false_positive_sec(vad[0], vad[1], [(2, 3), (4, 5)], extrude_start=2, extrude_end=2,
-                                            fill_gaps=2)
-    assert abs(fp - expected) < 0.001
+    v = REF["calc_false_positive"]
+    fp = oracle_mod.calc_false_positive_sec(case["vad"][0], case["vad"][1], [tuple(r) for r in v["refs"]],
+                                            extrude_start=v["extrude_start"], extrude_end=v["extrude_end"],
+                                            fill_gaps=v["fill_gaps"])
+    assert abs(fp - case["expect"]) < v["tolerance"]
 
 
 # ---------------- derived KATs ----------------
