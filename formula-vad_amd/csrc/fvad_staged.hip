@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "fvad_device.h"
 #include "fvad_internal.h"
@@ -39,6 +40,10 @@ namespace fvad {
 
 namespace {
 constexpr int kHist = kPitchBuf - kFrame;  // 1248
+#ifndef FVAD_PITCH_FRAMES
+#define FVAD_PITCH_FRAMES 4
+#endif
+constexpr int kPitchFrames = FVAD_PITCH_FRAMES;  // frames per k_pitch workgroup
 constexpr float kScale960 = 1.f / 960;
 
 __device__ __forceinline__ int ticks_of(const StagedArgs &a, int s) {
@@ -163,50 +168,98 @@ __global__ void __launch_bounds__(NT) k_fftA(StagedArgs a) {
 
 // ---------------------------------------------------------------------------
 // k_pitch: everything of pitch_search / remove_doubling that does not depend
-// on the previous frame.  Sequential sums keep C order, one sum per lane; the
-// phase structure assigns independent sums of one phase to lanes of one SIMT
-// loop so they run concurrently.
+// on the previous frame, for F frames per workgroup.  Every C-order sum stays
+// on one lane; lanes are assigned (frame, task) pairs so the serial chains of
+// F different frames (autocorr lags, Syy / yy recurrences, find_best_pitch
+// scans) share wave instructions instead of running on 1-5 lanes each.
+//   P0 x_lp (pitch_downsample)        all lanes
+//   P1 _celt_autocorr, 5 lags x F     wave 0
+//   P2 LPC + lag window + FIR coeffs  F lanes
+//   P3 5-tap FIR in place             all lanes (via registers)
+//   P4 wave 0: coarse / fine Syy sequences; wave 1: xx + yy_lookup chain;
+//      waves 2-3: coarse xcorr, R consecutive lags per lane
+//   P5 coarse find_best_pitch scan    F lanes
+//   P6 fine xcorr at the <= 10 candidate lags
+//   P7 fine scan -> T0, candidate periods and energies
+//   P8 remove_doubling inner products + speculative final xcorr (T-1, T+1)
 // ---------------------------------------------------------------------------
 namespace rec {
 constexpr int kT0 = 0, kXx = 1, kXy = 2, kYyT0 = 3, kNValid = 4;
-constexpr int kK = 8;       // per k=2..15: T1, T1b, s1, s2, yyT1, yyT1b (6 each)
-constexpr int kSpec = 96;   // candidate c (0 = T0, k-1 = T1_k): xcorr at T-1, T, T+1
-constexpr int kSize = 144;
+constexpr int kK = 8;       // per k=2..15: T1, T1b, s1 = xcorr(T1), s2 = xcorr(T1b), yyT1, yyT1b
+constexpr int kSpec = 96;   // candidate c (0 = T0, k-1 = T1_k): xcorr at T-1 [+0] and T+1 [+2]
+constexpr int kSize = 144;  // (the xcorr at T itself is kXy / s1)
 }  // namespace rec
+static_assert(rec::kSize == kPitchRecord, "pitch record size");
 
-template <int NT>
-__global__ void __launch_bounds__(NT) k_pitch(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float xlp[kXlp];
-  __shared__ __attribute__((aligned(16))) float xf[kXlp];
-  __shared__ float xc[296];
-  __shared__ float syy_c[148], syy_f[296];
-  __shared__ float yyl[388];
-  __shared__ float ac[8], lpc2[8], sc[8];
-  __shared__ int best[2], T0s, nvalid;
-  __shared__ float recl[rec::kSize];
-  const int tid = threadIdx.x;
-  const int V = a.V, total = a.n_streams * V;
-  const float *xl = xf + (kPitchMax >> 1);
-  for (int f = blockIdx.x; f < total; f += gridDim.x) {
-    const int s = f / V, v = f - s * V;
-    if (v >= ticks_of(a, s) * a.n_channels) continue;
-    const float *pb = a.xs + (size_t)s * a.L + (size_t)v * kFrame;  // pitch_buf[0..1728)
-    for (int i = tid; i < kXlp; i += NT)
-      xlp[i] = (i == 0) ? .5f * (.5f * (pb[1]) + pb[0]) : .5f * (.5f * (pb[2 * i - 1] + pb[2 * i + 1]) + pb[2 * i]);
-    __syncthreads();
-    if (tid < 5) {  // _celt_autocorr, lag = tid
-      const int k = tid, fastN = kXlp - 4;
-      float acc = 0;
-#pragma unroll 8
-      for (int i = 0; i < fastN; i++) acc = acc + xlp[i] * xlp[i + k];
-      float d = 0;
-      for (int i = k + fastN; i < kXlp; i++) d = d + xlp[i] * xlp[i - k];
-      ac[k] = acc + d;
+template <int F>
+struct PitchGeom {
+  static constexpr int kXS = 868;                    // padded x row (floats)
+  static constexpr int kR = (F * 147 + 127) / 128;   // coarse lags per lane
+  static constexpr int kTPF = (147 + kR - 1) / kR;   // coarse lanes per frame
+  static constexpr int kG3 = 59;                     // remove_doubling dots per frame
+  static_assert(F * kTPF <= 128, "coarse xcorr lanes exceed waves 2-3");
+  static_assert(5 * F <= 64 && 2 * F <= 64, "serial lanes exceed one wave");
+};
+
+__device__ __forceinline__ int rd_T1(int T0, int k) { return (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k)); }
+__device__ __forceinline__ int rd_T1b(int T0, int T1, int k) {
+  if (k == 2) return (T1 + T0 > 384) ? T0 : T0 + T1;
+  return (int)((unsigned)(2 * second_check(k) * T0 + k) / (unsigned)(2 * k));
+}
+
+template <int F>
+__global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
+  using G = PitchGeom<F>;
+  constexpr int NT = 256, XS = G::kXS, R = G::kR, TPF = G::kTPF;
+  __shared__ __attribute__((aligned(16))) float xf[F][XS];  // FIR output (x_lp filtered)
+  // per-frame scratch: x_lp during P0-P3, then xcorr / Syy / yy sequences
+  __shared__ __attribute__((aligned(16))) float scr[F][980];
+  constexpr int oXc = 0, oSyc = 148, oSyf = 296, oYy = 592;
+  __shared__ float ac[F][5], lpc2[F][5], xxs[F], fine[F][10];
+  __shared__ int best[F][2], T0s[F], nvs[F], fval[F];
+  __shared__ long long pbo[F];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int V = a.V;
+  const long long total = (long long)a.n_streams * V;
+  const long long ngroups = (total + F - 1) / F;
+  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    if (tid < F) {
+      const long long f = g * F + tid;
+      int ok = 0;
+      long long off = 0;
+      if (f < total) {
+        const int s = (int)(f / V), v = (int)(f - (long long)s * V);
+        ok = v < ticks_of(a, s) * a.n_channels;
+        off = (long long)s * a.L + (long long)v * kFrame;
+      }
+      fval[tid] = ok;
+      pbo[tid] = off;
     }
     __syncthreads();
-    if (tid == 0) {
+    // P0: x_lp[i] = .5*(.5*(pb[2i-1] + pb[2i+1]) + pb[2i])
+    for (int idx = tid; idx < F * kXlp; idx += NT) {
+      const int fr = idx / kXlp, i = idx - fr * kXlp;
+      const float *pb = a.xs + pbo[fr];
+      scr[fr][i] = (i == 0) ? .5f * (.5f * (pb[1]) + pb[0]) : .5f * (.5f * (pb[2 * i - 1] + pb[2 * i + 1]) + pb[2 * i]);
+    }
+    __syncthreads();
+    // P1: _celt_autocorr, lag k of frame fr
+    if (tid < 5 * F) {
+      const int fr = tid / 5, k = tid - 5 * fr;
+      const float *x = scr[fr];
+      const int fastN = kXlp - 4;
+      float acc = 0;
+#pragma unroll 8
+      for (int i = 0; i < fastN; i++) acc = acc + x[i] * x[i + k];
+      float d = 0;
+      for (int i = k + fastN; i < kXlp; i++) d = d + x[i] * x[i - k];
+      ac[fr][k] = acc + d;
+    }
+    __syncthreads();
+    // P2: lag window, _celt_lpc (order 4), bandwidth expansion, FIR coefficients
+    if (tid < F) {
       float acv[5];
-      for (int i = 0; i < 5; i++) acv[i] = ac[i];
+      for (int i = 0; i < 5; i++) acv[i] = ac[tid][i];
       acv[0] *= 1.0001f;
       for (int i = 1; i <= 4; i++) acv[i] -= acv[i] * (.008f * i) * (.008f * i);
       float lpc[4] = {0, 0, 0, 0};
@@ -233,132 +286,123 @@ __global__ void __launch_bounds__(NT) k_pitch(StagedArgs a) {
         lpc[i] = lpc[i] * tmp;
       }
       const float c1 = .8f;
-      lpc2[0] = lpc[0] + .8f;
-      lpc2[1] = lpc[1] + c1 * lpc[0];
-      lpc2[2] = lpc[2] + c1 * lpc[1];
-      lpc2[3] = lpc[3] + c1 * lpc[2];
-      lpc2[4] = c1 * lpc[3];
+      lpc2[tid][0] = lpc[0] + .8f;
+      lpc2[tid][1] = lpc[1] + c1 * lpc[0];
+      lpc2[tid][2] = lpc[2] + c1 * lpc[1];
+      lpc2[tid][3] = lpc[3] + c1 * lpc[2];
+      lpc2[tid][4] = c1 * lpc[3];
     }
     __syncthreads();
-    {
-      const float n0 = lpc2[0], n1 = lpc2[1], n2 = lpc2[2], n3 = lpc2[3], n4 = lpc2[4];
-      for (int i = tid; i < kXlp; i += NT) {
-        const float m0 = i >= 1 ? xlp[i - 1] : 0.0f, m1 = i >= 2 ? xlp[i - 2] : 0.0f, m2 = i >= 3 ? xlp[i - 3] : 0.0f,
-                    m3 = i >= 4 ? xlp[i - 4] : 0.0f, m4 = i >= 5 ? xlp[i - 5] : 0.0f;
-        float sum = xlp[i];
-        sum = sum + n0 * m0;
-        sum = sum + n1 * m1;
-        sum = sum + n2 * m2;
-        sum = sum + n3 * m3;
-        sum = sum + n4 * m4;
-        xf[i] = sum;
-      }
+    // P3: celt_fir5, x_lp (scratch) -> xf
+    for (int idx = tid; idx < F * kXlp; idx += NT) {
+      const int fr = idx / kXlp, i = idx - fr * kXlp;
+      const float *x = scr[fr];
+      const float m0 = i >= 1 ? x[i - 1] : 0.0f, m1 = i >= 2 ? x[i - 2] : 0.0f, m2 = i >= 3 ? x[i - 3] : 0.0f,
+                  m3 = i >= 4 ? x[i - 4] : 0.0f, m4 = i >= 5 ? x[i - 5] : 0.0f;
+      float sum = x[i];
+      sum = sum + lpc2[fr][0] * m0;
+      sum = sum + lpc2[fr][1] * m1;
+      sum = sum + lpc2[fr][2] * m2;
+      sum = sum + lpc2[fr][3] * m3;
+      sum = sum + lpc2[fr][4] * m4;
+      xf[fr][i] = sum;
     }
     __syncthreads();
-    // phase G1: coarse xcorr (147 lanes), Syy initial sums, xx — all sequential dot products
-    {
-      const float *pa = nullptr, *pbp = nullptr;
-      int sa = 1, sb = 1, len = 0;
-      float init = 0;
-      if (tid < 147) {
-        pa = xl;
-        sa = 2;
-        pbp = xf + 2 * tid;
-        sb = 2;
-        len = 240;
-      } else if (tid == 147) {
-        pa = xf;
-        pbp = xf;
-        sa = sb = 2;
-        len = 240;
-        init = 1;
-      } else if (tid == 148) {
-        pa = xf;
-        pbp = xf;
-        len = 480;
-        init = 1;
-      } else if (tid == 149) {
-        pa = xl;
-        pbp = xl;
-        len = 480;
+    // P4: energy sequences (waves 0-1) concurrently with the coarse xcorr (waves 2-3)
+    if (wave == 0) {
+      if (lane < 2 * F) {
+        const int fr = lane % F;
+        const bool fs = lane >= F;
+        syy_sequence(xf[fr], fs ? 1 : 2, fs ? 480 : 240, fs ? 294 : 147, scr[fr] + (fs ? oSyf : oSyc));
       }
-      float acc = init;
-      if (len) {
-#pragma unroll 4
-        for (int i = 0; i < len; i++) acc = acc + pa[i * sa] * pbp[i * sb];
-      }
-      if (tid < 147)
-        xc[tid] = acc;
-      else if (tid < 150)
-        sc[tid - 147] = acc;  // [0] Syy coarse init, [1] Syy fine init, [2] xx
-    }
-    __syncthreads();
-    // phase G2: energy recurrences (find_best_pitch Syy sequences, remove_doubling yy_lookup)
-    if (tid < 2) {
-      const int ys = tid == 0 ? 2 : 1, len = tid == 0 ? 240 : 480, n = tid == 0 ? 147 : 294;
-      float *out = tid == 0 ? syy_c : syy_f;
-      float Syy = sc[tid];
-#pragma unroll 4
-      for (int i = 0; i < n; i++) {
-        out[i] = Syy;
-        const float ya = xf[(i + len) * ys], yb = xf[i * ys];
-        Syy += ya * ya - yb * yb;
-        Syy = (1 > Syy) ? 1 : Syy;
-      }
-    } else if (tid == 64) {
-      const float xx = sc[2];
-      float yy = xx;
-      yyl[0] = xx;
-#pragma unroll 4
-      for (int i = 1; i <= 384; i++) {
-        yy = yy + xl[-i] * xl[-i] - xl[480 - i] * xl[480 - i];
-        yyl[i] = (0 > yy) ? 0 : yy;
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int bst[2] = {0, 1};
-      float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
-      for (int i = 0; i < 147; i++) best_pitch_visit(xc[i], syy_c[i], i, bn0, bn1, bd0, bd1, bst);
-      best[0] = bst[0];
-      best[1] = bst[1];
-    }
-    __syncthreads();
-    {
-      const int bp0 = best[0], bp1 = best[1];
-      for (int i = tid; i < 294; i += NT) xc[i] = 0;
-      __syncthreads();
-      if (tid < 10) {
-        const int i = (tid < 5 ? 2 * bp0 : 2 * bp1) - 2 + (tid % 5);
-        const bool dup = tid >= 5 && abs(i - 2 * bp0) <= 2;
-        if (i >= 0 && i < 294 && !dup) {
-          float sum = 0;
+    } else if (wave == 1) {
+      if (lane < F) {
+        const float *x = xf[lane] + (kPitchMax >> 1);
+        float xx = 0;
 #pragma unroll 8
-          for (int j = 0; j < 480; j++) sum = sum + xl[j] * xf[i + j];
-          xc[i] = (-1 > sum) ? -1 : sum;
+        for (int i = 0; i < 480; i++) xx = xx + x[i] * x[i];
+        xxs[lane] = xx;
+        float yy = xx;
+        float *yo = scr[lane] + oYy;
+        yo[0] = xx;
+#pragma unroll 4
+        for (int i = 1; i <= 384; i++) {
+          yy = yy + x[-i] * x[-i] - x[480 - i] * x[480 - i];
+          yo[i] = (0 > yy) ? 0 : yy;
         }
       }
+    } else {
+      const int l = tid - 128;
+      const int fr = l / TPF, blk = l - fr * TPF;
+      if (fr < F) {
+        const int k0 = blk * R;
+        const float *xr = xf[fr] + (kPitchMax >> 1);
+        const float *yr = xf[fr] + 2 * k0;
+        float acc[R];
+#pragma unroll
+        for (int m = 0; m < R; m++) acc[m] = 0;
+        for (int j = 0; j < 240; j++) {
+          const float xv = xr[2 * j];
+#pragma unroll
+          for (int m = 0; m < R; m++) acc[m] = acc[m] + xv * yr[2 * (j + m)];
+        }
+#pragma unroll
+        for (int m = 0; m < R; m++)
+          if (k0 + m < 147) scr[fr][oXc + k0 + m] = acc[m];
+      }
     }
     __syncthreads();
-    if (tid == 0) {
-      const int bp0 = best[0], bp1 = best[1];
+    // P5: coarse find_best_pitch
+    if (tid < F) {
       int bst[2] = {0, 1};
       float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
-      int w0lo = 2 * bp0 - 2, w0hi = 2 * bp0 + 2, w1lo = 2 * bp1 - 2, w1hi = 2 * bp1 + 2;
-      if (w1lo < w0lo) {
-        const int t0 = w0lo, t1 = w0hi;
-        w0lo = w1lo;
-        w0hi = w1hi;
-        w1lo = t0;
-        w1hi = t1;
+#pragma unroll 4
+      for (int i = 0; i < 147; i++) best_pitch_visit(scr[tid][oXc + i], scr[tid][oSyc + i], i, bn0, bn1, bd0, bd1, bst);
+      best[tid][0] = bst[0];
+      best[tid][1] = bst[1];
+    }
+    __syncthreads();
+    // P6: fine xcorr, only the lags within +-2 of 2*best0 / 2*best1 are non-zero
+    if (tid < 10 * F) {
+      const int fr = tid / 10, t = tid - 10 * fr;
+      const int bp0 = best[fr][0], bp1 = best[fr][1];
+      const int i = (t < 5 ? 2 * bp0 : 2 * bp1) - 2 + (t % 5);
+      const bool dup = t >= 5 && abs(i - 2 * bp0) <= 2;
+      if (i >= 0 && i < 294 && !dup) {
+        const float *xl = xf[fr] + (kPitchMax >> 1), *y = xf[fr] + i;
+        float sum = 0;
+#pragma unroll 8
+        for (int j = 0; j < 480; j++) sum = sum + xl[j] * y[j];
+        fine[fr][t] = (-1 > sum) ? -1 : sum;
       }
-      for (int i = max(0, w0lo); i <= min(293, w0hi); i++)
-        best_pitch_visit(xc[i], syy_f[i], i, bn0, bn1, bd0, bd1, bst);
-      for (int i = max(max(0, w1lo), w0hi + 1); i <= min(293, w1hi); i++)
-        best_pitch_visit(xc[i], syy_f[i], i, bn0, bn1, bd0, bd1, bst);
+    }
+    __syncthreads();
+    // P7: fine find_best_pitch + pseudo-interpolation -> T0 (remove_doubling input)
+    if (tid < F) {
+      const int fr = tid;
+      const int bp0 = best[fr][0], bp1 = best[fr][1];
+      const int w0 = 2 * bp0 - 2, w1 = 2 * bp1 - 2;
+      auto xcf = [&](int i) -> float {
+        if (i >= w0 && i <= w0 + 4) return fine[fr][i - w0];
+        if (i >= w1 && i <= w1 + 4) return fine[fr][5 + i - w1];
+        return 0.0f;
+      };
+      int bst[2] = {0, 1};
+      float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
+      int lo0 = w0, hi0 = w0 + 4, lo1 = w1, hi1 = w1 + 4;
+      if (lo1 < lo0) {
+        const int t0 = lo0, t1 = hi0;
+        lo0 = lo1;
+        hi0 = hi1;
+        lo1 = t0;
+        hi1 = t1;
+      }
+      for (int i = max(0, lo0); i <= min(293, hi0); i++) best_pitch_visit(xcf(i), scr[fr][oSyf + i], i, bn0, bn1, bd0, bd1, bst);
+      for (int i = max(max(0, lo1), hi0 + 1); i <= min(293, hi1); i++)
+        best_pitch_visit(xcf(i), scr[fr][oSyf + i], i, bn0, bn1, bd0, bd1, bst);
       int offset;
       if (bst[0] > 0 && bst[0] < 294 - 1) {
-        const float aa = xc[bst[0] - 1], bb = xc[bst[0]], cc = xc[bst[0] + 1];
+        const float aa = xcf(bst[0] - 1), bb = xcf(bst[0]), cc = xcf(bst[0] + 1);
         if ((cc - aa) > .7f * (bb - aa))
           offset = 1;
         else if ((aa - cc) > .7f * (bb - cc))
@@ -371,77 +415,65 @@ __global__ void __launch_bounds__(NT) k_pitch(StagedArgs a) {
       const int pitch = 2 * bst[0] - offset;
       int T0 = (kPitchMax - pitch) / 2;
       if (T0 >= 384) T0 = 383;
-      T0s = T0;
       int nv = 0;
       for (int k = 2; k <= 15; k++) {
-        if ((int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k)) < 30) break;
+        if (rd_T1(T0, k) < 30) break;
         nv++;
       }
-      nvalid = nv;
+      T0s[fr] = T0;
+      nvs[fr] = nv;
+      if (fval[fr]) {
+        float *rg = a.rec + (g * F + fr) * rec::kSize;
+        rg[rec::kT0] = __int_as_float(T0);
+        rg[rec::kXx] = xxs[fr];
+        rg[rec::kYyT0] = scr[fr][oYy + T0];
+        rg[rec::kNValid] = __int_as_float(nv);
+      }
     }
     __syncthreads();
-    // phase G3: remove_doubling inner products for every candidate, plus the
-    // final 3-lag xcorr speculatively for each candidate period
-    {
-      const int T0 = T0s, nv = nvalid;
-      int lag = -100000;
-      if (tid == 0) {
-        lag = T0;
-      } else if (tid < 29) {
-        const int kk = (tid - 1) >> 1, k = kk + 2;
-        if (kk < nv) {
-          const int T1 = (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k));
-          int T1b;
-          if (k == 2)
-            T1b = (T1 + T0 > 384) ? T0 : T0 + T1;
-          else
-            T1b = (int)((unsigned)(2 * second_check(k) * T0 + k) / (unsigned)(2 * k));
-          lag = ((tid - 1) & 1) ? T1b : T1;
-        }
-      } else if (tid < 29 + 45) {
-        const int c = (tid - 29) / 3, m = (tid - 29) % 3;
-        int T = -1;
-        if (c == 0)
-          T = T0;
-        else if (c - 1 < nv)
-          T = (int)((unsigned)(2 * T0 + (c + 1)) / (unsigned)(2 * (c + 1)));
-        if (T >= 0) lag = T + m - 1;
+    // P8: candidate metadata + remove_doubling dots (C order, one per lane)
+    if (tid < 14 * F) {
+      const int fr = tid / 14, kk = tid - 14 * fr, k = kk + 2;
+      if (fval[fr] && kk < nvs[fr]) {
+        const int T0 = T0s[fr], T1 = rd_T1(T0, k), T1b = rd_T1b(T0, T1, k);
+        float *q = a.rec + (g * F + fr) * rec::kSize + rec::kK + kk * 6;
+        q[0] = __int_as_float(T1);
+        q[1] = __int_as_float(T1b);
+        q[4] = scr[fr][oYy + T1];
+        q[5] = scr[fr][oYy + T1b];
       }
-      if (lag != -100000) {
+    }
+    for (int idx = tid; idx < F * G::kG3; idx += NT) {
+      const int fr = idx / G::kG3, q = idx - fr * G::kG3;
+      if (!fval[fr]) continue;
+      const int T0 = T0s[fr], nv = nvs[fr];
+      int lag = -1, slot = 0;
+      if (q == 0) {
+        lag = T0;
+        slot = rec::kXy;
+      } else if (q < 29) {
+        const int kk = (q - 1) >> 1, k = kk + 2;
+        if (kk < nv) {
+          const int T1 = rd_T1(T0, k);
+          lag = ((q - 1) & 1) ? rd_T1b(T0, T1, k) : T1;
+          slot = rec::kK + kk * 6 + 2 + ((q - 1) & 1);
+        }
+      } else {
+        const int c = (q - 29) >> 1, side = (q - 29) & 1;
+        if (c == 0 || c - 1 < nv) {
+          const int T = (c == 0) ? T0 : rd_T1(T0, c + 1);
+          lag = side ? T + 1 : T - 1;
+          slot = rec::kSpec + c * 3 + (side ? 2 : 0);
+        }
+      }
+      if (lag >= 0) {
+        const float *xl = xf[fr] + (kPitchMax >> 1);
         float acc = 0;
 #pragma unroll 8
         for (int i = 0; i < 480; i++) acc = acc + xl[i] * xl[i - lag];
-        if (tid == 0)
-          recl[rec::kXy] = acc;
-        else if (tid < 29)
-          recl[rec::kK + ((tid - 1) >> 1) * 6 + 2 + ((tid - 1) & 1)] = acc;
-        else
-          recl[rec::kSpec + (tid - 29)] = acc;
-      }
-      if (tid == 0) {
-        recl[rec::kT0] = __int_as_float(T0);
-        recl[rec::kXx] = sc[2];
-        recl[rec::kYyT0] = yyl[T0];
-        recl[rec::kNValid] = __int_as_float(nv);
-      } else if (tid >= 100 && tid < 114) {
-        const int kk = tid - 100, k = kk + 2;
-        if (kk < nv) {
-          const int T1 = (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k));
-          int T1b;
-          if (k == 2)
-            T1b = (T1 + T0 > 384) ? T0 : T0 + T1;
-          else
-            T1b = (int)((unsigned)(2 * second_check(k) * T0 + k) / (unsigned)(2 * k));
-          recl[rec::kK + kk * 6 + 0] = __int_as_float(T1);
-          recl[rec::kK + kk * 6 + 1] = __int_as_float(T1b);
-          recl[rec::kK + kk * 6 + 4] = yyl[T1];
-          recl[rec::kK + kk * 6 + 5] = yyl[T1b];
-        }
+        a.rec[(g * F + fr) * rec::kSize + slot] = acc;
       }
     }
-    __syncthreads();
-    float *rg = a.rec + (size_t)f * rec::kSize;
-    for (int i = tid; i < rec::kSize; i += NT) rg[i] = recl[i];
     __syncthreads();
   }
 }
@@ -513,7 +545,8 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
       pg = 1.0f;
     else
       pg = best_xy / (best_yy + 1);
-    const float x0 = r[rec::kSpec + cand * 3], x1 = r[rec::kSpec + cand * 3 + 1], x2 = r[rec::kSpec + cand * 3 + 2];
+    const float x0 = r[rec::kSpec + cand * 3], x2 = r[rec::kSpec + cand * 3 + 2];
+    const float x1 = cand == 0 ? r[rec::kXy] : r[rec::kK + (cand - 1) * 6 + 2];  // xcorr at T itself
     int offset;
     if ((x2 - x0) > .7f * (x1 - x0))
       offset = 1;
@@ -997,7 +1030,19 @@ hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t strea
   rec(1);
   hipLaunchKernelGGL(k_fftA<NT>, dim3(g), dim3(NT), 0, stream, a);
   rec(2);
-  hipLaunchKernelGGL(k_pitch<NT>, dim3(g), dim3(NT), 0, stream, a);
+  {
+    // frames per k_pitch workgroup: 4 (default) or 8 (FVAD_PITCH_FRAMES=8, tuning only)
+    static const int fp = [] {
+      const char *e = getenv("FVAD_PITCH_FRAMES");
+      return (e && atoi(e) == 8) ? 8 : kPitchFrames;
+    }();
+    const long long groups = (frames + fp - 1) / fp;
+    const unsigned gp = (unsigned)std::min<long long>(groups, grid_frames);
+    if (fp == 8)
+      hipLaunchKernelGGL(k_pitch<8>, dim3(gp), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL(k_pitch<kPitchFrames>, dim3(gp), dim3(256), 0, stream, a);
+  }
   rec(3);
   hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(64), 0, stream, a);
   rec(4);
