@@ -66,6 +66,9 @@ struct fvad_engine {
   float *d_xs = nullptr, *d_X = nullptr, *d_P = nullptr, *d_Ex = nullptr, *d_Ep = nullptr, *d_Exp = nullptr,
         *d_Lyf = nullptr, *d_f34 = nullptr, *d_rec = nullptr, *d_vadf = nullptr, *d_ys = nullptr;
   int *d_sil = nullptr, *d_pitch = nullptr, *d_wtick = nullptr;
+  float *d_gr = nullptr, *d_gs = nullptr;
+  int8_t *d_rnn_img = nullptr;
+  int rnn_act[fvad::rnnimg::kMats] = {};
   long long *d_wstart = nullptr;
   int V = 0, L = 0, wmax = 0, grid_frames = 0;
   int resident_ticks = 0;
@@ -118,6 +121,40 @@ int dalloc(T **p, size_t count) {
   return FVAD_OK;
 }
 
+// int8 GRU-stack image for k_rnn (layout: fvad_internal.h rnnimg)
+void build_rnn_image(const fvad::HostModel &hm, std::vector<int8_t> &img, int *act) {
+  namespace R = fvad::rnnimg;
+  img.assign(R::kBytes, 0);
+  const int8_t *b = hm.blob;
+  auto put = [&](int m, int c, int j, int8_t v) { img[R::off_w(m) + c * R::stride(m) + j] = v; };
+  auto dense = [&](int m, int l) {
+    const fvad::HostLayer &L = hm.layers[l];
+    for (int c = 0; c < L.nout; c++) {
+      img[R::off_b(m) + c] = b[L.off_b + c];
+      for (int j = 0; j < L.nin; j++) put(m, c, j, b[L.off_w + (size_t)j * L.nout + c]);
+    }
+    act[m] = L.act;
+  };
+  auto gru = [&](int mg, int mh, int l) {
+    const fvad::HostLayer &L = hm.layers[l];
+    const int N = L.nout, M = L.nin, S3 = 3 * N;
+    for (int col = 0; col < S3; col++) {
+      const int m = col < 2 * N ? mg : mh, c = col < 2 * N ? col : col - 2 * N;
+      img[R::off_b(m) + c] = b[L.off_b + col];
+      for (int j = 0; j < M; j++) put(m, c, j, b[L.off_w + (size_t)j * S3 + col]);
+      for (int j = 0; j < N; j++) put(m, c, M + j, b[L.off_r + (size_t)j * S3 + col]);
+    }
+    act[mg] = fvad::kActSigmoid;
+    act[mh] = L.act;
+  };
+  dense(0, 0);
+  gru(1, 2, 1);
+  gru(3, 4, 2);
+  gru(5, 6, 3);
+  dense(7, 4);
+  dense(8, 5);
+}
+
 int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
   std::vector<float> w(hm.blob_size);
   for (size_t i = 0; i < hm.blob_size; i++) w[i] = (float)hm.blob[i];
@@ -145,6 +182,19 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
     g.b = e->d_weights + L.off_b;
     return g;
   };
+  for (int l = 0; l < 6; l++) {
+    const fvad::HostLayer &L = hm.layers[l];
+    const int m = l == 0 ? 0 : l == 1 ? 1 : l == 2 ? 3 : l == 3 ? 5 : l == 4 ? 7 : 8;
+    if (L.nin != fvad::rnnimg::kKin[m] || (l >= 1 && l <= 3 ? 2 * L.nout : L.nout) != fvad::rnnimg::kCols[m])
+      return fail(FVAD_EFORMAT, "model layer shapes differ from the rnnoise classic model");
+  }
+  {
+    std::vector<int8_t> img;
+    build_rnn_image(hm, img, e->rnn_act);
+    rc = dalloc(&e->d_rnn_img, img.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(e->d_rnn_img, img.data(), img.size(), hipMemcpyHostToDevice));
+  }
   e->dmodel.in_dense = dense(0);
   e->dmodel.vad = gru(1);
   e->dmodel.noise = gru(2);
@@ -162,7 +212,7 @@ void free_all(fvad_engine *e) {
                   e->d_vad,  e->d_wratio,  e->d_wvad,  e->d_band, e->d_den,   e->d_wflag, e->d_ticks,
                   e->d_model, e->d_stamps, e->d_xs,    e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_vadf,  e->d_ys,    e->d_sil,
-                  e->d_pitch, e->d_wtick,  e->d_wstart};
+                  e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &ev : e->ev)
@@ -250,7 +300,8 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
         (rc = dalloc(&e->d_Lyf, F * fvad::kBands)) || (rc = dalloc(&e->d_f34, F * 8)) ||
         (rc = dalloc(&e->d_rec, F * fvad::kPitchRecord)) || (rc = dalloc(&e->d_vadf, F)) ||
         (rc = dalloc(&e->d_ys, F * fvad::kWin)) || (rc = dalloc(&e->d_sil, F)) || (rc = dalloc(&e->d_pitch, F)) ||
-        (rc = dalloc(&e->d_wtick, B * e->wmax)) || (rc = dalloc(&e->d_wstart, B * e->wmax)))
+        (rc = dalloc(&e->d_wtick, B * e->wmax)) || (rc = dalloc(&e->d_wstart, B * e->wmax)) ||
+        (rc = dalloc(&e->d_gr, F * fvad::kBands)) || (rc = dalloc(&e->d_gs, F * fvad::kBands)))
       return bail(rc);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "device query failed"));
@@ -351,6 +402,10 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.rec = e->d_rec;
   a.pitch = e->d_pitch;
   a.vadf = e->d_vadf;
+  a.gr = e->d_gr;
+  a.gs = e->d_gs;
+  a.rnn_img = e->d_rnn_img;
+  for (int m = 0; m < fvad::rnnimg::kMats; m++) a.rnn_act[m] = e->rnn_act[m];
   a.ys = e->d_ys;
   a.ring = e->d_ring;
   a.ring_len = e->ring_len;

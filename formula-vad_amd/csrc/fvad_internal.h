@@ -45,8 +45,34 @@ constexpr int kLastPeriod = kMemId + 1;         // int
 constexpr int kLastGain = kLastPeriod + 1;      // float
 constexpr int kFramesDone = kLastGain + 1;      // int: ticks processed (480-sample frames per channel)
 constexpr int kVolAcc = kFramesDone + 1;        // float: temp_fft_buffer_vol_ratio
-constexpr int kWords = ((kVolAcc + 1 + 63) / 64) * 64;
+constexpr int kCepsDist = kVolAcc + 1;          // staged mode: cepstral distance matrix [8][8]
+constexpr int kWords = ((kCepsDist + kCeps * kCeps + 63) / 64) * 64;
 }  // namespace st
+
+// ---------------------------------------------------------------------------
+// int8 image of the GRU stack for the staged recurrence kernel (k_rnn keeps it
+// in LDS).  Nine column-major matrices; column c of matrix m holds the K
+// weights of one output neuron in summation order (input part, then the
+// recurrent part for GRU gates), so one lane walks one column.
+//   0 input_dense   1 vad z|r   2 vad h   3 noise z|r   4 noise h
+//   5 denoise z|r   6 denoise h 7 denoise_output        8 vad_output
+// Shapes are the classic rnnoise model's (the only ones the loaders accept).
+// ---------------------------------------------------------------------------
+namespace rnnimg {
+constexpr int kMats = 9;
+constexpr int kCols[kMats] = {24, 48, 24, 96, 48, 192, 96, 22, 1};
+constexpr int kKin[kMats] = {42, 24, 24, 90, 90, 114, 114, 96, 24};  // input-vector part of K
+constexpr int kK[kMats] = {42, 48, 48, 138, 138, 210, 210, 96, 24};
+constexpr int pad16(int x) { return (x + 15) & ~15; }
+constexpr int stride(int m) { return (kK[m] + 3) & ~3; }  // bytes per column
+constexpr int off_b(int m) {
+  int o = 0;
+  for (int i = 0; i < m; i++) o += pad16(kCols[i]) + pad16(kCols[i] * stride(i));
+  return o;
+}
+constexpr int off_w(int m) { return off_b(m) + pad16(kCols[m]); }
+constexpr int kBytes = off_b(kMats);
+}  // namespace rnnimg
 
 // ---------------------------------------------------------------------------
 // Read-only plan tables (built on the host by fvad_plan.cpp, uploaded once).

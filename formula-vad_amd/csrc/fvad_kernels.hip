@@ -155,7 +155,9 @@ constexpr int kBest0 = 0, kBest1 = 1, kPitch = 2, kT0 = 3, kT = 4, kSilence = 5,
   do {            \
   } while (0)
 #endif
+#ifdef FVAD_STAMPS
 constexpr int kStamps = 24;
+#endif
 
 // ---------------------------------------------------------------------------
 // k_frame

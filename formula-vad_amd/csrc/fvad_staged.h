@@ -30,6 +30,9 @@ struct StagedArgs {
   float *rec;              // [f][kPitchRecord]
   int *pitch;              // [f] selected pitch index
   float *vadf;             // [f] per-frame vad probability
+  float *gr, *gs;          // [f][22] GRU gains g and smoothed gains max(g, .6*lastg)
+  const int8_t *rnn_img;   // rnnimg image (fvad_internal.h), device
+  int rnn_act[rnnimg::kMats];  // activation of each image matrix
   float *ys;               // [f][960] windowed synthesis output
   float *ring;             // [s][c][ring_len]
   int ring_len;

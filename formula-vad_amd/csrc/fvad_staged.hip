@@ -57,51 +57,123 @@ __device__ __forceinline__ float win960(const float *__restrict__ hw, int i) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_prep2(StagedArgs a) {
-  const int s = blockIdx.x * 64 + threadIdx.x;
-  if (s >= a.n_streams) return;
-  const int nt = ticks_of(a, s);
-  if (nt <= 0) return;
-  const int C = a.n_channels;
-  float *row = a.xs + (size_t)s * a.L;
-  float *stp = a.state + (size_t)s * st::kWords;
-  for (int i = 0; i < kHist; i++) row[i] = stp[st::kPitch + kFrame + i];
-  float mem0 = stp[st::kHp], mem1 = stp[st::kHp + 1];
+// k_prep2: high-pass biquad (a serial IIR with f64 intermediates: no exact
+// parallel form exists, so one lane walks one stream), s16 scaling, RMS
+// volume ratio.  A 256-thread workgroup owns S = 16 / C streams: wave 0 runs
+// the S serial biquad chains out of LDS while waves 2-3 stream the next
+// tick's input in and the previous tick's output out with coalesced 16-byte
+// accesses (the input of S consecutive streams of one tick is contiguous),
+// and wave 1 computes the per-channel RMS sums.
+// ---------------------------------------------------------------------------
+constexpr int kPrepSlots = 16;  // channel-frames per tick per workgroup
+
+__global__ void __launch_bounds__(256) k_prep2(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float inb[2][kPrepSlots * kFrame];
+  __shared__ __attribute__((aligned(16))) float outb[2][kPrepSlots * kFrame];
+  __shared__ float vol[2][kPrepSlots];
+  __shared__ int nts[kPrepSlots];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int C = a.n_channels, S = kPrepSlots / C, sb = blockIdx.x * S;
+  const int ns = min(S, a.n_streams - sb);  // streams in this workgroup
+  if (ns <= 0) return;
+  const int slots = ns * C;
+  if (tid < S) nts[tid] = (tid < ns) ? ticks_of(a, sb + tid) : 0;
+  __syncthreads();
+  int T = 0;
+  for (int s = 0; s < ns; s++) T = max(T, nts[s]);
+  // pitch history of every stream -> xs[s][0..1248)
+  for (int idx = tid; idx < ns * kHist; idx += 256) {
+    const int s = idx / kHist, i = idx - s * kHist;
+    if (nts[s] > 0)
+      a.xs[(size_t)(sb + s) * a.L + i] = a.state[(size_t)(sb + s) * st::kWords + st::kPitch + kFrame + i];
+  }
+  auto load_tick = [&](int t, int buf) {  // waves 2-3
+    const float4 *src = reinterpret_cast<const float4 *>(a.pcm + ((size_t)t * a.n_streams + sb) * C * kFrame);
+    float4 *dst = reinterpret_cast<float4 *>(inb[buf]);
+    for (int i = tid - 128; i < slots * kFrame / 4; i += 128) dst[i] = src[i];
+  };
+  auto store_tick = [&](int t, int buf) {  // waves 2-3
+    for (int i = tid - 128; i < slots * kFrame / 4; i += 128) {
+      const int slot = i / (kFrame / 4), s = slot / C, c = slot - s * C, k = i - slot * (kFrame / 4);
+      if (t < nts[s])
+        reinterpret_cast<float4 *>(a.xs + (size_t)(sb + s) * a.L + kHist + (size_t)(t * C + c) * kFrame)[k] =
+            reinterpret_cast<const float4 *>(outb[buf] + slot * kFrame)[k];
+    }
+  };
+  float mem0 = 0, mem1 = 0;
+  if (wave == 0 && lane < ns) {
+    mem0 = a.state[(size_t)(sb + lane) * st::kWords + st::kHp];
+    mem1 = a.state[(size_t)(sb + lane) * st::kWords + st::kHp + 1];
+  }
+  if (wave >= 2 && T > 0) load_tick(0, 0);
+  __syncthreads();
   const float b0 = -2.0f, b1 = 1.0f, a0 = -1.99599f, a1 = 0.99600f;
   const float scalar = (float)32767;
-  for (int t = 0; t < nt; t++) {
-    float vmin = 1, vmax = 0;
-    for (int c = 0; c < C; c++) {
-      const float4 *in4 = reinterpret_cast<const float4 *>(a.pcm + (((size_t)t * a.n_streams + s) * C + c) * kFrame);
-      float4 *out4 = reinterpret_cast<float4 *>(row + kHist + (size_t)(t * C + c) * kFrame);
-      float sum = 0;
-      for (int i4 = 0; i4 < kFrame / 4; i4++) {
-        const float4 v = in4[i4];
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-        float yy[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const float v0 = vv[k];
-          sum += v0 * v0;
-          const float xi = a.raw_s16 ? v0 : v0 * scalar;
-          const float yi = xi + mem0;
-          mem0 = (float)(mem1 + (b0 * (double)xi - a0 * (double)yi));
-          mem1 = (float)(b1 * (double)xi - a1 * (double)yi);
-          yy[k] = yi;
+  for (int t = 0; t <= T; t++) {
+    const int cur = t & 1;
+    if (t < T) {
+      if (wave == 0) {
+        if (lane < ns && t < nts[lane]) {
+          for (int c = 0; c < C; c++) {
+            const float *x = inb[cur] + (lane * C + c) * kFrame;
+            float *y = outb[cur] + (lane * C + c) * kFrame;
+#pragma unroll 8
+            for (int i = 0; i < kFrame; i++) {
+              const float v0 = x[i];
+              const float xi = a.raw_s16 ? v0 : v0 * scalar;
+              const float yi = xi + mem0;
+              mem0 = (float)(mem1 + (b0 * (double)xi - a0 * (double)yi));
+              mem1 = (float)(b1 * (double)xi - a1 * (double)yi);
+              y[i] = yi;
+            }
+          }
         }
-        out4[i4] = make_float4(yy[0], yy[1], yy[2], yy[3]);
+      } else if (wave == 1) {
+        if (lane < slots) {
+          const float *x = inb[cur] + lane * kFrame;
+          float sum = 0;
+#pragma unroll 8
+          for (int i = 0; i < kFrame; i++) sum += x[i] * x[i];
+          vol[cur][lane] = sqrtf(sum / (float)kFrame);
+        }
+        if (t > 0 && lane < ns && t - 1 < nts[lane]) {
+          float vmin = 1, vmax = 0;
+          for (int c = 0; c < C; c++) {
+            const float vl = vol[cur ^ 1][lane * C + c];
+            if (vl < vmin) vmin = vl;
+            if (vl > vmax) vmax = vl;
+          }
+          a.ratio[(size_t)(t - 1) * a.n_streams + sb + lane] = (vmax == 0) ? 0 : vmin / vmax;
+        }
+      } else {
+        if (t + 1 < T) load_tick(t + 1, cur ^ 1);
+        if (t > 0) store_tick(t - 1, cur ^ 1);
       }
-      const float vol = sqrtf(sum / (float)kFrame);
-      if (vol < vmin) vmin = vol;
-      if (vol > vmax) vmax = vol;
+    } else {
+      if (wave >= 2 && t > 0) store_tick(t - 1, cur ^ 1);
+      if (wave == 1 && t > 0 && lane < ns && t - 1 < nts[lane]) {
+        float vmin = 1, vmax = 0;
+        for (int c = 0; c < C; c++) {
+          const float vl = vol[cur ^ 1][lane * C + c];
+          if (vl < vmin) vmin = vl;
+          if (vl > vmax) vmax = vl;
+        }
+        a.ratio[(size_t)(t - 1) * a.n_streams + sb + lane] = (vmax == 0) ? 0 : vmin / vmax;
+      }
     }
-    a.ratio[(size_t)t * a.n_streams + s] = (vmax == 0) ? 0 : vmin / vmax;
+    __syncthreads();
+  }
+  if (wave == 0 && lane < ns && nts[lane] > 0) {
+    a.state[(size_t)(sb + lane) * st::kWords + st::kHp] = mem0;
+    a.state[(size_t)(sb + lane) * st::kWords + st::kHp + 1] = mem1;
   }
   // pitch_buf after the last frame = the last 1728 samples of the row
-  const float *last = row + (size_t)(nt * C - 1) * kFrame;
-  for (int i = 0; i < kPitchBuf; i++) stp[st::kPitch + i] = last[i];
-  stp[st::kHp] = mem0;
-  stp[st::kHp + 1] = mem1;
+  for (int idx = tid; idx < ns * kPitchBuf; idx += 256) {
+    const int s = idx / kPitchBuf, i = idx - s * kPitchBuf;
+    if (nts[s] > 0)
+      a.state[(size_t)(sb + s) * st::kWords + st::kPitch + i] =
+          a.xs[(size_t)(sb + s) * a.L + (size_t)(nts[s] * C - 1) * kFrame + i];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -482,7 +554,7 @@ __global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
 // k_select: remove_doubling's sequential selection (one lane per stream).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
-  const int s = blockIdx.x * 64 + threadIdx.x;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.n_streams) return;
   const int nf = ticks_of(a, s) * a.n_channels;
   if (nf <= 0) return;
@@ -623,205 +695,306 @@ __global__ void __launch_bounds__(NT) k_pspec(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_rnn: the recurrence (one workgroup per stream, frames in stream order)
+// k_rnn: the recurrence.  One workgroup owns S streams and walks their frames
+// in lockstep (frame v of every stream, then v+1 ...).  The whole GRU stack is
+// resident in LDS as an int8 image (rnnimg, 88 KB; int8 -> f32 is exact), so
+// weights never come from L2 per frame.  A matrix column = one neuron's C-order
+// sum: lane (column, stream group) accumulates SL streams of that column with
+// one weight fetch per term; per-stream vectors are stored [j][S] so the SL
+// inputs of a term are one 16-byte LDS read.  Per frame and stream:
+// cepstral memory + deltas, spectral variability (distance matrix kept in the
+// state, only the new row recomputed), compute_rnn, and the gain recurrence
+// lastg; the pitch filter and gain application move to k_synth (they depend
+// on nothing recurrent once g and the smoothed gains are known).
 // ---------------------------------------------------------------------------
-template <int NT>
-__global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 Xl[kFreq + 1];
-  __shared__ float Ex[kBands + 2], Ep[kBands + 2], Exp[kBands + 2];
-  __shared__ float feat[kFeat + 2], g[kBands + 2], rr[kBands + 2], nrm[kBands + 2], newE[kBands + 2],
-      lastg[kBands + 2];
-  __shared__ float ceps[kCeps * kBands];
-  __shared__ float gv[kMaxNeurons], gn[kMaxNeurons], gd[kMaxNeurons];
-  __shared__ float dout[kMaxNeurons], rin[3 * kMaxNeurons], zr[2 * kMaxNeurons], hb[kMaxNeurons];
-  __shared__ float mind[kCeps];
-  __shared__ float vad_s;
-  __shared__ int memid_s;
-  const int tid = threadIdx.x;
-  const int s = blockIdx.x;
-  if (s >= a.n_streams) return;
-  const int nf = ticks_of(a, s) * a.n_channels;
-  if (nf <= 0) return;
-  const Plan *__restrict__ P = a.plan;
-  const float *__restrict__ tt = P->tansig;
-  const DevModel &M = *a.model;
-  float *stp = a.state + (size_t)s * st::kWords;
-  int *istp = reinterpret_cast<int *>(stp);
-  for (int i = tid; i < kCeps * kBands; i += NT) ceps[i] = stp[st::kCepsMem + i];
-  for (int i = tid; i < kBands; i += NT) lastg[i] = stp[st::kLastG + i];
-  for (int i = tid; i < kMaxNeurons; i += NT) {
-    gv[i] = stp[st::kVadGru + i];
-    gn[i] = stp[st::kNoiseGru + i];
-    gd[i] = stp[st::kDenGru + i];
+constexpr int kRnnS = 8;   // streams per workgroup
+constexpr int kRnnG = 2;   // lanes per column (stream groups)
+constexpr int kRnnNT = 512;
+
+template <int S, int SL>
+__device__ __forceinline__ void mv_terms(const int8_t *__restrict__ wc, int j0, int j1, const float *vT, int jv0,
+                                         int s0, float (&acc)[SL]) {
+  // acc[q] += w[j] * v[j - j0 + jv0][s0 + q], j in [j0, j1), C order
+#pragma unroll 8
+  for (int j = j0; j < j1; j++) {
+    const float w = (float)wc[j];
+    const float *v = vT + (jv0 + j - j0) * S + s0;
+#pragma unroll
+    for (int q = 0; q < SL; q++) acc[q] = acc[q] + w * v[q];
   }
-  if (tid == 0) memid_s = istp[st::kMemId];
+}
+
+// dense / GRU gate matrix m: out[c][s] = act(kWs * (b[c] + sum_j w[c][j] * in[j][s]))
+// (for gates the input is [in ; state] with the state part starting at kKin[m])
+template <int m, int S, int G, int NT>
+__device__ void rnn_mat(const int8_t *W, const float *inT, const float *stT, float *outT, int act,
+                        const float *tt, int tid) {
+  constexpr int SL = S / G, cols = rnnimg::kCols[m], kin = rnnimg::kKin[m], K = rnnimg::kK[m];
+  constexpr int ob = rnnimg::off_b(m), ow = rnnimg::off_w(m), ws = rnnimg::stride(m);
+  for (int t = tid; t < cols * G; t += NT) {
+    const int c = t / G, s0 = (t - c * G) * SL;
+    const int8_t *wc = W + ow + c * ws;
+    const float b = (float)W[ob + c];
+    float acc[SL];
+#pragma unroll
+    for (int q = 0; q < SL; q++) acc[q] = b;
+    mv_terms<S, SL>(wc, 0, kin, inT, 0, s0, acc);
+    if (K > kin) mv_terms<S, SL>(wc, kin, K, stT, 0, s0, acc);
+#pragma unroll
+    for (int q = 0; q < SL; q++) outT[c * S + s0 + q] = activate(tt, act, kWs * acc[q]);
+  }
+}
+
+// GRU candidate matrix m (h part): sum = b + sum_j w*in[j] + sum_j (w*state[j])*r[j];
+// h = z*state + (1-z)*act(kWs*sum)
+template <int m, int S, int G, int NT>
+__device__ void rnn_h(const int8_t *W, const float *inT, const float *stT, const float *zrT, float *hT, int act,
+                      const float *tt, int tid) {
+  constexpr int SL = S / G, cols = rnnimg::kCols[m], kin = rnnimg::kKin[m], K = rnnimg::kK[m];
+  constexpr int ob = rnnimg::off_b(m), ow = rnnimg::off_w(m), ws = rnnimg::stride(m);
+  constexpr int N = cols;
+  for (int t = tid; t < cols * G; t += NT) {
+    const int c = t / G, s0 = (t - c * G) * SL;
+    const int8_t *wc = W + ow + c * ws;
+    const float b = (float)W[ob + c];
+    float acc[SL];
+#pragma unroll
+    for (int q = 0; q < SL; q++) acc[q] = b;
+    mv_terms<S, SL>(wc, 0, kin, inT, 0, s0, acc);
+#pragma unroll 8
+    for (int j = kin; j < K; j++) {
+      const float w = (float)wc[j];
+      const float *sv = stT + (j - kin) * S + s0;
+      const float *rv = zrT + (N + j - kin) * S + s0;
+#pragma unroll
+      for (int q = 0; q < SL; q++) acc[q] = acc[q] + w * sv[q] * rv[q];
+    }
+#pragma unroll
+    for (int q = 0; q < SL; q++) {
+      const float sum = activate(tt, act, kWs * acc[q]);
+      const float z = zrT[c * S + s0 + q];
+      hT[c * S + s0 + q] = z * stT[c * S + s0 + q] + (1 - z) * sum;
+    }
+  }
+}
+
+template <int S, int G, int NT>
+__global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) int8_t W[rnnimg::kBytes];
+  __shared__ float tt[204];
+  __shared__ __attribute__((aligned(16))) float featT[44 * S];
+  __shared__ float ceps[S][kCeps * kBands];
+  __shared__ float dist[S][kCeps * kCeps];
+  __shared__ __attribute__((aligned(16))) float doutT[24 * S], gvT[24 * S], gnT[48 * S], gdT[96 * S];
+  __shared__ __attribute__((aligned(16))) float zrT[192 * S], hT[96 * S], rinT[116 * S];
+  __shared__ float lastg[S][kBands];
+  __shared__ int memid[S], act[S], nfs[S];
+  __shared__ long long fbase[S];
+  __shared__ float vad_s[S];
+  const int tid = threadIdx.x;
+  const int sb = blockIdx.x * S;
+  // GRU image + tansig table -> LDS
+  {
+    const int4 *src = reinterpret_cast<const int4 *>(a.rnn_img);
+    int4 *dst = reinterpret_cast<int4 *>(W);
+    for (int i = tid; i < rnnimg::kBytes / 16; i += NT) dst[i] = src[i];
+    for (int i = tid; i < 201; i += NT) tt[i] = a.plan->tansig[i];
+  }
+  // per-stream state -> LDS
+  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
+    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
+    ceps[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] : 0.0f;
+  }
+  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
+    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
+    dist[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] : 0.0f;
+  }
+  for (int idx = tid; idx < S * kBands; idx += NT) {
+    const int s = idx / kBands, i = idx - s * kBands;
+    lastg[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] : 0.0f;
+  }
+  for (int idx = tid; idx < S * 96; idx += NT) {
+    const int s = idx / 96, i = idx - s * 96;
+    const bool ok = sb + s < a.n_streams;
+    const float *stp = a.state + (size_t)(sb + s) * st::kWords;
+    if (i < 24) gvT[i * S + s] = ok ? stp[st::kVadGru + i] : 0.0f;
+    if (i < 48) gnT[i * S + s] = ok ? stp[st::kNoiseGru + i] : 0.0f;
+    gdT[i * S + s] = ok ? stp[st::kDenGru + i] : 0.0f;
+  }
+  if (tid < S) {
+    const int s = sb + tid;
+    const bool ok = s < a.n_streams;
+    memid[tid] = ok ? reinterpret_cast<const int *>(a.state)[(size_t)s * st::kWords + st::kMemId] : 0;
+    nfs[tid] = ok ? ticks_of(a, s) * a.n_channels : 0;
+    fbase[tid] = (long long)s * a.V;
+  }
   __syncthreads();
-  for (int v = 0; v < nf; v++) {
-    const size_t f = (size_t)s * a.V + v;
-    if (a.silence[f]) {
-      if (tid == 0) a.vadf[f] = 0;
-      continue;  // X passes through unmodified, state untouched
-    }
-    const int memid = memid_s;
-    // features: ceps_0 = DCT(Ly) (k_fftA), pitch-correlation features (k_pspec)
-    if (tid < kBands) {
-      const float val = a.Lyf[f * kBands + tid];
-      ceps[memid * kBands + tid] = val;
-      feat[tid] = val;
-    } else if (tid >= 34 && tid < 41) {
-      feat[tid] = a.f34[f * 8 + (tid - 34)];
-    } else if (tid >= 64 && tid < 64 + kBands) {
-      Ex[tid - 64] = a.Ex[f * kBands + tid - 64];
-      Ep[tid - 64] = a.Ep[f * kBands + tid - 64];
-      Exp[tid - 64] = a.Exp[f * kBands + tid - 64];
-    }
-    {
-      const float2 *Xg = a.X + f * kFreq;
-      for (int k = tid; k < kFreq; k += NT) Xl[k] = Xg[k];
+  int maxnf = 0;
+#pragma unroll
+  for (int s = 0; s < S; s++) maxnf = max(maxnf, nfs[s]);
+  const int *ra = a.rnn_act;
+  for (int v = 0; v < maxnf; v++) {
+    if (tid < S) {
+      int ok = 0;
+      if (v < nfs[tid]) {
+        const long long f = fbase[tid] + v;
+        ok = !a.silence[f];
+        if (!ok) a.vadf[f] = 0;  // silent frame: X passes through, state untouched
+      }
+      act[tid] = ok;
     }
     __syncthreads();
-    if (tid < 6) {
-      const float *c0 = ceps + memid * kBands;
-      const float *c1 = ceps + ((memid < 1) ? kCeps + memid - 1 : memid - 1) * kBands;
-      const float *c2 = ceps + ((memid < 2) ? kCeps + memid - 2 : memid - 2) * kBands;
-      const int i = tid;
-      feat[i] = c0[i] + c1[i] + c2[i];
-      feat[kBands + i] = c0[i] - c2[i];
-      feat[kBands + 6 + i] = c0[i] - 2 * c1[i] + c2[i];
-    } else if (tid >= 32 && tid < 32 + kCeps) {
-      const int i = tid - 32;
-      float mindist = 1e15f;
-      for (int j = 0; j < kCeps; j++) {
-        float dist = 0;
+    // features 0..21 = DCT(Ly) (k_fftA), 34..40 (k_pspec); cepstral memory
+    for (int idx = tid; idx < S * 29; idx += NT) {
+      const int s = idx / 29, i = idx - s * 29;
+      if (!act[s]) continue;
+      const long long f = fbase[s] + v;
+      if (i < kBands) {
+        const float val = a.Lyf[f * kBands + i];
+        ceps[s][memid[s] * kBands + i] = val;
+        featT[i * S + s] = val;
+      } else {
+        featT[(34 + i - kBands) * S + s] = a.f34[f * 8 + (i - kBands)];
+      }
+    }
+    __syncthreads();
+    // deltas (features 0..5, 22..33) and the new row of the distance matrix
+    for (int idx = tid; idx < S * 14; idx += NT) {
+      const int s = idx / 14, i = idx - s * 14;
+      if (!act[s]) continue;
+      const int mi = memid[s];
+      const float *c0 = ceps[s] + mi * kBands;
+      if (i < 6) {
+        const float *c1 = ceps[s] + ((mi < 1) ? kCeps + mi - 1 : mi - 1) * kBands;
+        const float *c2 = ceps[s] + ((mi < 2) ? kCeps + mi - 2 : mi - 2) * kBands;
+        featT[i * S + s] = c0[i] + c1[i] + c2[i];
+        featT[(kBands + i) * S + s] = c0[i] - c2[i];
+        featT[(kBands + 6 + i) * S + s] = c0[i] - 2 * c1[i] + c2[i];
+      } else {
+        const int j = i - 6;
+        const float *cj = ceps[s] + j * kBands;
+        float d = 0;
 #pragma unroll
         for (int k = 0; k < kBands; k++) {
-          const float tmp = ceps[i * kBands + k] - ceps[j * kBands + k];
-          dist += tmp * tmp;
+          const float tmp = c0[k] - cj[k];
+          d += tmp * tmp;
         }
-        if (j != i) mindist = (mindist < dist) ? mindist : dist;
+        dist[s][mi * kCeps + j] = d;
+        dist[s][j * kCeps + mi] = d;
       }
-      mind[i] = mindist;
     }
     __syncthreads();
-    if (tid == 0) {
+    if (tid < S && act[tid]) {
+      const int s = tid;
       float sv = 0;
-      for (int i = 0; i < kCeps; i++) sv += mind[i];
-      feat[41] = (float)(sv / kCeps - 2.1);
-      int mid = memid + 1;
+      for (int i = 0; i < kCeps; i++) {
+        float mindist = 1e15f;
+        for (int j = 0; j < kCeps; j++)
+          if (j != i) mindist = (mindist < dist[s][i * kCeps + j]) ? mindist : dist[s][i * kCeps + j];
+        sv += mindist;
+      }
+      featT[41 * S + s] = (float)(sv / kCeps - 2.1);
+      int mid = memid[s] + 1;
       if (mid == kCeps) mid = 0;
-      memid_s = mid;
+      memid[s] = mid;
     }
     __syncthreads();
     // compute_rnn
-    dense_layer<NT>(M.in_dense, feat, dout, tt, tid);
+    rnn_mat<0, S, G, NT>(W, featT, nullptr, doutT, ra[0], tt, tid);
     __syncthreads();
-    gru_gates<NT>(M.vad, dout, gv, zr, tt, tid);
+    rnn_mat<1, S, G, NT>(W, doutT, gvT, zrT, kActSigmoid, tt, tid);
     __syncthreads();
-    gru_out<NT>(M.vad, dout, gv, zr, hb, tt, tid);
+    rnn_h<2, S, G, NT>(W, doutT, gvT, zrT, hT, ra[2], tt, tid);
     __syncthreads();
-    {
-      const int nd = M.in_dense.nout, nvd = M.vad.nout;
-      for (int i = tid; i < nvd; i += NT) gv[i] = hb[i];
-      __syncthreads();
-      for (int i = tid; i < nd + nvd + kFeat; i += NT)
-        rin[i] = (i < nd) ? dout[i] : (i < nd + nvd) ? gv[i - nd] : feat[i - nd - nvd];
-      if (tid == NT - 1) {
-        const DevDense &d = M.vad_out;
-        float sum = d.b[0];
-        for (int j = 0; j < d.nin; j++) sum += d.w[j * d.nout] * gv[j];
-        vad_s = activate(tt, d.act, kWs * sum);
-      }
+    for (int idx = tid; idx < 24 * S; idx += NT)
+      if (act[idx % S]) gvT[idx] = hT[idx];
+    __syncthreads();
+    // noise_input = [dense_out, vad_state, features]; vad_output alongside
+    for (int idx = tid; idx < 90 * S; idx += NT) {
+      const int j = idx / S;
+      rinT[idx] = (j < 24) ? doutT[idx] : (j < 48) ? gvT[idx - 24 * S] : featT[idx - 48 * S];
+    }
+    if (tid >= NT - S) {
+      const int s = tid - (NT - S);
+      constexpr int ob = rnnimg::off_b(8), ow = rnnimg::off_w(8);
+      float sum = (float)W[ob];
+      for (int j = 0; j < 24; j++) sum += (float)W[ow + j] * gvT[j * S + s];
+      vad_s[s] = activate(tt, ra[8], kWs * sum);
     }
     __syncthreads();
-    gru_gates<NT>(M.noise, rin, gn, zr, tt, tid);
+    rnn_mat<3, S, G, NT>(W, rinT, gnT, zrT, kActSigmoid, tt, tid);
     __syncthreads();
-    gru_out<NT>(M.noise, rin, gn, zr, hb, tt, tid);
+    rnn_h<4, S, G, NT>(W, rinT, gnT, zrT, hT, ra[4], tt, tid);
     __syncthreads();
-    {
-      const int nvd = M.vad.nout, nn = M.noise.nout;
-      for (int i = tid; i < nn; i += NT) gn[i] = hb[i];
-      __syncthreads();
-      for (int i = tid; i < nvd + nn + kFeat; i += NT)
-        rin[i] = (i < nvd) ? gv[i] : (i < nvd + nn) ? gn[i - nvd] : feat[i - nvd - nn];
+    for (int idx = tid; idx < 48 * S; idx += NT)
+      if (act[idx % S]) gnT[idx] = hT[idx];
+    __syncthreads();
+    // denoise_input = [vad_state, noise_state, features]
+    for (int idx = tid; idx < 114 * S; idx += NT) {
+      const int j = idx / S;
+      rinT[idx] = (j < 24) ? gvT[idx] : (j < 72) ? gnT[idx - 24 * S] : featT[idx - 72 * S];
     }
     __syncthreads();
-    gru_gates<NT>(M.den, rin, gd, zr, tt, tid);
+    rnn_mat<5, S, G, NT>(W, rinT, gdT, zrT, kActSigmoid, tt, tid);
     __syncthreads();
-    gru_out<NT>(M.den, rin, gd, zr, hb, tt, tid);
+    rnn_h<6, S, G, NT>(W, rinT, gdT, zrT, hT, ra[6], tt, tid);
     __syncthreads();
-    for (int i = tid; i < M.den.nout; i += NT) gd[i] = hb[i];
+    for (int idx = tid; idx < 96 * S; idx += NT)
+      if (act[idx % S]) gdT[idx] = hT[idx];
     __syncthreads();
-    dense_layer<NT>(M.den_out, gd, g, tt, tid);
+    rnn_mat<7, S, G, NT>(W, gdT, nullptr, zrT, ra[7], tt, tid);  // gains g[22][S] (zrT reused)
     __syncthreads();
-    // pitch_filter
-    if (tid < kBands) {
-      const int i = tid;
-      float r;
-      if (Exp[i] > g[i])
-        r = 1;
-      else
-        r = (float)((double)((Exp[i] * Exp[i]) * (1 - (g[i] * g[i]))) /
-                    (.001 + (double)((g[i] * g[i]) * (1 - (Exp[i] * Exp[i])))));
-      float cl = (0 > r) ? 0 : r;
-      cl = (1 < cl) ? 1 : cl;
-      r = (float)sqrt((double)cl);
-      r = (float)((double)r * sqrt((double)Ex[i] / (1e-8 + (double)Ep[i])));
-      rr[i] = r;
-    }
-    if (tid == 0) a.vadf[f] = vad_s;
-    __syncthreads();
-    {
-      const float2 *Pg = a.P + f * kFreq;
-      for (int k = tid; k < kFreq; k += NT) {
-        const float rf = interp_gain(rr, P, k);
-        const float2 pk = Pg[k];
-        Xl[k].x += rf * pk.x;
-        Xl[k].y += rf * pk.y;
-      }
-    }
-    __syncthreads();
-    if (tid < kBands) newE[tid] = band_sum(Xl, Xl, P, tid);
-    __syncthreads();
-    if (tid < kBands) {
-      const int i = tid;
-      nrm[i] = (float)sqrt((double)Ex[i] / (1e-8 + (double)newE[i]));
-      const float al = .6f * lastg[i];
-      const float gi = (g[i] > al) ? g[i] : al;
-      g[i] = gi;
-      lastg[i] = gi;
-    }
-    __syncthreads();
-    {
-      float2 *Xg = a.X + f * kFreq;
-      for (int k = tid; k < kFreq; k += NT) {
-        const float nf2 = interp_gain(nrm, P, k);
-        float2 val = Xl[k];
-        val.x *= nf2;
-        val.y *= nf2;
-        const float gf = interp_gain(g, P, k);
-        val.x *= gf;
-        val.y *= gf;
-        Xg[k] = val;
-      }
+    // gain smoothing g = max(g, .6*lastg) (denoise.c); outputs
+    for (int idx = tid; idx < S * kBands; idx += NT) {
+      const int s = idx / kBands, i = idx - s * kBands;
+      if (!act[s]) continue;
+      const long long f = fbase[s] + v;
+      const float gi = zrT[i * S + s];
+      const float al = .6f * lastg[s][i];
+      const float gs = (gi > al) ? gi : al;
+      lastg[s][i] = gs;
+      a.gr[f * kBands + i] = gi;
+      a.gs[f * kBands + i] = gs;
+      if (i == 0) a.vadf[f] = vad_s[s];
     }
     __syncthreads();
   }
-  for (int i = tid; i < kCeps * kBands; i += NT) stp[st::kCepsMem + i] = ceps[i];
-  for (int i = tid; i < kBands; i += NT) stp[st::kLastG + i] = lastg[i];
-  for (int i = tid; i < kMaxNeurons; i += NT) {
-    stp[st::kVadGru + i] = gv[i];
-    stp[st::kNoiseGru + i] = gn[i];
-    stp[st::kDenGru + i] = gd[i];
+  // state <- LDS
+  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
+    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
+    if (sb + s < a.n_streams && nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] = ceps[s][i];
   }
-  if (tid == 0) istp[st::kMemId] = memid_s;
+  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
+    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
+    if (sb + s < a.n_streams && nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] = dist[s][i];
+  }
+  for (int idx = tid; idx < S * kBands; idx += NT) {
+    const int s = idx / kBands, i = idx - s * kBands;
+    if (sb + s < a.n_streams && nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] = lastg[s][i];
+  }
+  for (int idx = tid; idx < S * 96; idx += NT) {
+    const int s = idx / 96, i = idx - s * 96;
+    if (sb + s >= a.n_streams || nfs[s] <= 0) continue;
+    float *stp = a.state + (size_t)(sb + s) * st::kWords;
+    if (i < 24) stp[st::kVadGru + i] = gvT[i * S + s];
+    if (i < 48) stp[st::kNoiseGru + i] = gnT[i * S + s];
+    stp[st::kDenGru + i] = gdT[i * S + s];
+  }
+  if (tid < S && sb + tid < a.n_streams && nfs[tid] > 0)
+    reinterpret_cast<int *>(a.state)[(size_t)(sb + tid) * st::kWords + st::kMemId] = memid[tid];
 }
 
 // ---------------------------------------------------------------------------
-// k_synth: inverse transform (forward FFT of the Hermitian extension), window
+// k_synth: pitch_filter + gain application (no recurrence left once g / the
+// smoothed gains are known), then the inverse transform (forward FFT of the
+// Hermitian extension) and the synthesis window
 // ---------------------------------------------------------------------------
 template <int NT>
 __global__ void __launch_bounds__(NT) k_synth(StagedArgs a) {
   __shared__ __attribute__((aligned(16))) float2 W[kWin];
+  __shared__ __attribute__((aligned(16))) float2 Xl[kFreq + 1];
+  __shared__ float rr[kBands + 2], nrm[kBands + 2], gs[kBands + 2], newE[kBands + 2];
+  __shared__ int sil;
   const int tid = threadIdx.x;
   const Plan *__restrict__ P = a.plan;
   const float2 *__restrict__ tw = reinterpret_cast<const float2 *>(P->tw960);
@@ -831,12 +1004,57 @@ __global__ void __launch_bounds__(NT) k_synth(StagedArgs a) {
     const int s = f / V, v = f - s * V;
     if (v >= ticks_of(a, s) * a.n_channels) continue;
     const float2 *Xg = a.X + (size_t)f * kFreq;
+    for (int k = tid; k < kFreq; k += NT) Xl[k] = Xg[k];
+    if (tid == 0) sil = a.silence[f];
+    __syncthreads();
+    if (!sil) {
+      if (tid < kBands) {
+        const int i = tid;
+        const float Exp = a.Exp[(size_t)f * kBands + i], g = a.gr[(size_t)f * kBands + i];
+        const float Ex = a.Ex[(size_t)f * kBands + i], Ep = a.Ep[(size_t)f * kBands + i];
+        float r;
+        if (Exp > g)
+          r = 1;
+        else
+          r = (float)((double)((Exp * Exp) * (1 - (g * g))) / (.001 + (double)((g * g) * (1 - (Exp * Exp)))));
+        float cl = (0 > r) ? 0 : r;
+        cl = (1 < cl) ? 1 : cl;
+        r = (float)sqrt((double)cl);
+        r = (float)((double)r * sqrt((double)Ex / (1e-8 + (double)Ep)));
+        rr[i] = r;
+        gs[i] = a.gs[(size_t)f * kBands + i];
+      }
+      __syncthreads();
+      const float2 *Pg = a.P + (size_t)f * kFreq;
+      for (int k = tid; k < kFreq; k += NT) {
+        const float rf = interp_gain(rr, P, k);
+        const float2 pk = Pg[k];
+        Xl[k].x += rf * pk.x;
+        Xl[k].y += rf * pk.y;
+      }
+      __syncthreads();
+      if (tid < kBands) newE[tid] = band_sum(Xl, Xl, P, tid);
+      __syncthreads();
+      if (tid < kBands) nrm[tid] = (float)sqrt((double)a.Ex[(size_t)f * kBands + tid] / (1e-8 + (double)newE[tid]));
+      __syncthreads();
+      for (int k = tid; k < kFreq; k += NT) {
+        const float nf = interp_gain(nrm, P, k);
+        float2 val = Xl[k];
+        val.x *= nf;
+        val.y *= nf;
+        const float gf = interp_gain(gs, P, k);
+        val.x *= gf;
+        val.y *= gf;
+        Xl[k] = val;
+      }
+      __syncthreads();
+    }
     for (int i = tid; i < kWin; i += NT) {
       float2 val;
       if (i < kFreq) {
-        val = Xg[i];
+        val = Xl[i];
       } else {
-        const float2 c = Xg[kWin - i];
+        const float2 c = Xl[kWin - i];
         val = make_float2(c.x, -c.y);
       }
       W[P->bitrev960[i]] = make_float2(kScale960 * val.x, kScale960 * val.y);
@@ -890,7 +1108,7 @@ __global__ void __launch_bounds__(256) k_ola(StagedArgs a) {
 // k_winmeta: window completion bookkeeping (VAD.zig:298-348), lane per stream
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
-  const int s = blockIdx.x * 64 + threadIdx.x;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.n_streams) return;
   const int nt = ticks_of(a, s);
   int *wt = a.win_tick + (size_t)s * a.wmax;
@@ -1018,7 +1236,9 @@ const char *staged_kernel_name(int i) {
 
 hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t stream, hipEvent_t *ev) {
   constexpr int NT = 256;
-  const int lane_blocks = (a.n_streams + 63) / 64;
+  // lane-per-stream kernels: 16 streams per workgroup spreads the serial
+  // chains over more CUs (each chain is latency-bound, not lane-bound)
+  const int lane_blocks = (a.n_streams + 15) / 16;
   const long long frames = (long long)a.n_streams * a.V;
   const int g = (int)std::min<long long>(frames, grid_frames);
   (void)hipGetLastError();
@@ -1026,7 +1246,10 @@ hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t strea
     if (ev) (void)hipEventRecord(ev[k], stream);
   };
   rec(0);
-  hipLaunchKernelGGL(k_prep2, dim3(lane_blocks), dim3(64), 0, stream, a);
+  {
+    const int S = kPrepSlots / a.n_channels;
+    hipLaunchKernelGGL(k_prep2, dim3((a.n_streams + S - 1) / S), dim3(256), 0, stream, a);
+  }
   rec(1);
   hipLaunchKernelGGL(k_fftA<NT>, dim3(g), dim3(NT), 0, stream, a);
   rec(2);
@@ -1044,18 +1267,19 @@ hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t strea
       hipLaunchKernelGGL(k_pitch<kPitchFrames>, dim3(gp), dim3(256), 0, stream, a);
   }
   rec(3);
-  hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(4);
   hipLaunchKernelGGL(k_pspec<NT>, dim3(g), dim3(NT), 0, stream, a);
   rec(5);
-  hipLaunchKernelGGL(k_rnn<NT>, dim3(a.n_streams), dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL((k_rnn<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
+                     stream, a);
   rec(6);
   hipLaunchKernelGGL(k_synth<NT>, dim3(g), dim3(NT), 0, stream, a);
   rec(7);
   const long long ola_threads = frames * kFrame;
   hipLaunchKernelGGL(k_ola, dim3((unsigned)((ola_threads + 255) / 256)), dim3(256), 0, stream, a);
   rec(8);
-  hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(9);
   hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
   rec(10);
