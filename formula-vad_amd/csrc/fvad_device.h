@@ -143,6 +143,123 @@ __device__ void fft960_stages(float2 *W, const float2 *__restrict__ tw, int tid)
   __syncthreads();
 }
 
+// The same transform for persistent 256-thread workgroups: every twiddle a
+// thread needs in the five stages is loaded once into registers (Fft960Tw)
+// and reused for every frame the workgroup processes.  Butterfly assignment
+// and arithmetic are exactly fft960_stages<256>'s.
+struct Fft960Tw {
+  float2 s2[3], s3[3], s4a[2], s4b[2], s5[4];
+  float2 epi3, ya, yb;
+};
+__device__ __forceinline__ void fft960_load(Fft960Tw &t, const float2 *__restrict__ tw, int tid) {
+  const int j2 = tid & 3, j3 = tid & 15, k4 = tid & 63;
+  t.s2[0] = tw[j2 * 60];
+  t.s2[1] = tw[j2 * 120];
+  t.s2[2] = tw[j2 * 180];
+  t.s3[0] = tw[j3 * 15];
+  t.s3[1] = tw[j3 * 30];
+  t.s3[2] = tw[j3 * 45];
+  t.s4a[0] = tw[k4 * 5];  // q = tid and q = tid + 256 share k = q & 63
+  t.s4a[1] = tw[k4 * 10];
+  t.s4b[0] = t.s4a[0];
+  t.s4b[1] = t.s4a[1];
+  const int u = tid < 192 ? tid : 0;
+  t.s5[0] = tw[u];
+  t.s5[1] = tw[2 * u];
+  t.s5[2] = tw[3 * u];
+  t.s5[3] = tw[4 * u];
+  t.epi3 = tw[320];
+  t.ya = tw[192];
+  t.yb = tw[384];
+}
+// F independent 960-point transforms W[fr][960], fr < F, by one 256-thread
+// workgroup: a thread owns the same butterfly index in every frame, so its
+// twiddles stay in registers and each stage costs one barrier for F frames.
+template <int F>
+__device__ __forceinline__ void fft960_run(const Fft960Tw &t, float2 (*W)[kWin], int tid) {
+  if (tid < 240) {  // radix 4, m = 1
+#pragma unroll
+    for (int fr = 0; fr < F; fr++) {
+      float2 *Fp = W[fr] + 4 * tid;
+      float2 f0 = Fp[0];
+      const float2 f1 = Fp[1], f2 = Fp[2], f3 = Fp[3];
+      const float2 s0 = csub(f0, f2);
+      f0 = cadd(f0, f2);
+      float2 s1 = cadd(f1, f3);
+      Fp[2] = csub(f0, s1);
+      Fp[0] = cadd(f0, s1);
+      s1 = csub(f1, f3);
+      Fp[1] = make_float2(s0.x + s1.y, s0.y - s1.x);
+      Fp[3] = make_float2(s0.x - s1.y, s0.y + s1.x);
+    }
+  }
+  __syncthreads();
+  if (tid < 240) {
+#pragma unroll
+    for (int fr = 0; fr < F; fr++) bfly4(W[fr] + (tid >> 2) * 16 + (tid & 3), 4, t.s2[0], t.s2[1], t.s2[2]);
+  }
+  __syncthreads();
+  if (tid < 240) {
+#pragma unroll
+    for (int fr = 0; fr < F; fr++) bfly4(W[fr] + (tid >> 4) * 64 + (tid & 15), 16, t.s3[0], t.s3[1], t.s3[2]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int fr = 0; fr < F; fr++) {
+    bfly3(W[fr] + (tid >> 6) * 192 + (tid & 63), 64, t.s4a[0], t.s4a[1], t.epi3);
+    if (tid < 64) bfly3(W[fr] + ((tid + 256) >> 6) * 192 + (tid & 63), 64, t.s4b[0], t.s4b[1], t.epi3);
+  }
+  __syncthreads();
+  if (tid < 192) {
+#pragma unroll
+    for (int fr = 0; fr < F; fr++) bfly5(W[fr] + tid, 192, t.s5[0], t.s5[1], t.s5[2], t.s5[3], t.ya, t.yb);
+  }
+  __syncthreads();
+}
+
+// Band tables of one persistent workgroup, staged in LDS.
+struct BandTab {
+  float frac[400];
+  int of[400];
+  int e4[kBands + 2];
+  float dct[kBands * kBands];
+};
+__device__ __forceinline__ void bandtab_load(BandTab &b, const Plan *__restrict__ P, int tid, int nt) {
+  for (int i = tid; i < 400; i += nt) {
+    b.frac[i] = P->band_frac[i];
+    b.of[i] = P->band_of[i];
+  }
+  for (int i = tid; i < kBands; i += nt) b.e4[i] = P->eband4[i];
+  for (int i = tid; i < kBands * kBands; i += nt) b.dct[i] = P->dct[i];
+}
+__device__ __forceinline__ float band_sum_t(const float2 *A, const float2 *B, const BandTab &T, int b) {
+  float acc = 0;
+  if (b >= 1) {
+#pragma unroll 4
+    for (int k = T.e4[b - 1]; k < T.e4[b]; k++) {
+      float tmp = A[k].x * B[k].x;
+      tmp += A[k].y * B[k].y;
+      acc += T.frac[k] * tmp;
+    }
+  }
+  if (b <= kBands - 2) {
+#pragma unroll 4
+    for (int k = T.e4[b]; k < T.e4[b + 1]; k++) {
+      float tmp = A[k].x * B[k].x;
+      tmp += A[k].y * B[k].y;
+      acc += (1 - T.frac[k]) * tmp;
+    }
+  }
+  if (b == 0 || b == kBands - 1) acc *= 2;
+  return acc;
+}
+__device__ __forceinline__ float interp_gain_t(const float *bandE, const BandTab &T, int k) {
+  if (k >= 400) return 0.0f;
+  const int b = T.of[k];
+  const float frac = T.frac[k];
+  return (1 - frac) * bandE[b] + frac * bandE[b + 1];
+}
+
 // compute_band_energy / compute_band_corr: one lane per band, C summation order.
 __device__ __forceinline__ float band_sum(const float2 *A, const float2 *B, const Plan *__restrict__ P, int b) {
   float acc = 0;

@@ -305,7 +305,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
       return bail(rc);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "device query failed"));
-    e->grid_frames = prop.multiProcessorCount * 8;
+    e->grid_frames = prop.multiProcessorCount;  // CUs; persistent grids are sized per kernel
   }
   if ((rc = fvad_engine_reset(e))) return bail(rc);
   *out = e;

@@ -51,7 +51,7 @@ struct StagedArgs {
 
 // Launch the 10 kernels on `stream`; when ev != nullptr, ev[0..10] are
 // recorded around them (per-kernel timing).
-hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t stream, hipEvent_t *ev);
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev);
 const char *staged_kernel_name(int i);
 
 }  // namespace fvad

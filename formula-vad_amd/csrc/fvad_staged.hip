@@ -177,62 +177,123 @@ __global__ void __launch_bounds__(256) k_prep2(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Persistent 256-thread frame kernels (k_fftA, k_pspec, k_synth) work on F
+// frames per workgroup iteration: each phase covers all F frames, so the
+// per-band serial sums (band energies, the Ly chain, DCTs) of F frames share
+// wave instructions and every barrier is amortised over F frames.  Per-thread
+// setup, loaded once: the element indices a thread owns in the 960-point
+// windowed scatter (i = tid + 256 r), their digit-reversed destinations and
+// window values, and the FFT twiddles.
+// ---------------------------------------------------------------------------
+constexpr int kFftFrames = 4;
+
+struct FrameCtx {
+  Fft960Tw tw;
+  int dst[4];
+  float win[4];
+};
+__device__ __forceinline__ void frame_ctx_load(FrameCtx &c, const Plan *__restrict__ P, int tid) {
+  fft960_load(c.tw, reinterpret_cast<const float2 *>(P->tw960), tid);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int i = tid + 256 * r;
+    c.dst[r] = i < kWin ? P->bitrev960[i] : 0;
+    c.win[r] = i < kWin ? win960(P->half_window, i) : 0.0f;
+  }
+}
+
+// frame indices of group g (-1: past the end or beyond the stream's valid ticks)
+template <int F>
+__device__ __forceinline__ void group_frames(const StagedArgs &a, long long g, int tid, int *fidx) {
+  if (tid < F) {
+    const long long f = g * F + tid;
+    int ok = -1;
+    if (f < (long long)a.n_streams * a.V) {
+      const int s = (int)(f / a.V), v = (int)(f - (long long)s * a.V);
+      if (v < ticks_of(a, s) * a.n_channels) ok = (int)f;
+    }
+    fidx[tid] = ok;
+  }
+}
+__device__ __forceinline__ const float *frame_pb(const StagedArgs &a, int f) {
+  const int s = f / a.V, v = f - s * a.V;
+  return a.xs + (size_t)s * a.L + (size_t)v * kFrame;
+}
+
+// ---------------------------------------------------------------------------
 // k_fftA: X, Ex, Ly chain, silence, DCT(Ly)
 // ---------------------------------------------------------------------------
-template <int NT>
-__global__ void __launch_bounds__(NT) k_fftA(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[kWin];
-  __shared__ float Ly[kBands + 2];
-  __shared__ int sil;
+template <int F>
+__global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 W[F][kWin];
+  __shared__ BandTab T;
+  __shared__ float Ly[F][kBands + 2], Exl[F][kBands + 2];
+  __shared__ int sil[F], fidx[F];
   const int tid = threadIdx.x;
-  const Plan *__restrict__ P = a.plan;
-  const float2 *__restrict__ tw = reinterpret_cast<const float2 *>(P->tw960);
-  const float *__restrict__ hw = P->half_window;
-  const int V = a.V, total = a.n_streams * V;
-  for (int f = blockIdx.x; f < total; f += gridDim.x) {
-    const int s = f / V, v = f - s * V;
-    if (v >= ticks_of(a, s) * a.n_channels) continue;
-    const float *pb = a.xs + (size_t)s * a.L + (size_t)v * kFrame;
-    for (int i = tid; i < kWin; i += NT) {
-      float val = pb[kPitchBuf - kWin + i];
-      val *= win960(hw, i);
-      W[P->bitrev960[i]] = make_float2(kScale960 * val, kScale960 * 0.0f);
+  FrameCtx cx;
+  frame_ctx_load(cx, a.plan, tid);
+  bandtab_load(T, a.plan, tid, 256);
+  const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
+  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    group_frames<F>(a, g, tid, fidx);
+    __syncthreads();
+#pragma unroll
+    for (int fr = 0; fr < F; fr++) {
+      const int f = fidx[fr];
+      if (f < 0) continue;
+      const float *pb = frame_pb(a, f) + (kPitchBuf - kWin);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int i = tid + 256 * r;
+        if (i < kWin) {
+          float val = pb[i];
+          val *= cx.win[r];
+          W[fr][cx.dst[r]] = make_float2(kScale960 * val, kScale960 * 0.0f);
+        }
+      }
     }
     __syncthreads();
-    fft960_stages<NT>(W, tw, tid);
-    float2 *Xg = a.X + (size_t)f * kFreq;
-    for (int k = tid; k < kFreq; k += NT) Xg[k] = W[k];
-    if (tid < kBands) {
-      const float ex = band_sum(W, W, P, tid);
-      a.Ex[(size_t)f * kBands + tid] = ex;
-      Ly[tid] = (float)log10(1e-2 + (double)ex);
+    fft960_run<F>(cx.tw, W, tid);
+    for (int idx = tid; idx < F * kFreq; idx += 256) {
+      const int fr = idx / kFreq, k = idx - fr * kFreq;
+      if (fidx[fr] >= 0) a.X[(size_t)fidx[fr] * kFreq + k] = W[fr][k];
+    }
+    if (tid < F * kBands) {
+      const int fr = tid / kBands, b = tid - fr * kBands;
+      const float ex = band_sum_t(W[fr], W[fr], T, b);
+      Exl[fr][b] = ex;
+      if (fidx[fr] >= 0) a.Ex[(size_t)fidx[fr] * kBands + b] = ex;
+      Ly[fr][b] = (float)log10(1e-2 + (double)ex);
     }
     __syncthreads();
-    if (tid == 0) {
+    if (tid < F) {
+      const int fr = tid;
       float logMax = -2, follow = -2, E = 0;
-      const float *ex = a.Ex + (size_t)f * kBands;
       for (int i = 0; i < kBands; i++) {
-        const float ly0 = Ly[i];
+        const float ly0 = Ly[fr][i];
         const double bb = (follow - 1.5 > (double)ly0) ? follow - 1.5 : (double)ly0;
         const double aa = ((double)(logMax - 7) > bb) ? (double)(logMax - 7) : bb;
         const float ly = (float)aa;
-        Ly[i] = ly;
+        Ly[fr][i] = ly;
         logMax = (logMax > ly) ? logMax : ly;
         follow = (float)((follow - 1.5 > (double)ly) ? follow - 1.5 : (double)ly);
-        E += ex[i];
+        E += Exl[fr][i];
       }
-      sil = ((double)E < 0.04) ? 1 : 0;
-      a.silence[f] = sil;
+      sil[fr] = ((double)E < 0.04) ? 1 : 0;
+      if (fidx[fr] >= 0) a.silence[fidx[fr]] = sil[fr];
     }
     __syncthreads();
-    if (!sil && tid < kBands) {
-      float sum = 0;
+    if (tid < F * kBands) {
+      const int fr = tid / kBands, b = tid - fr * kBands;
+      if (fidx[fr] >= 0 && !sil[fr]) {
+        float sum = 0;
 #pragma unroll
-      for (int j = 0; j < kBands; j++) sum += Ly[j] * P->dct[j * kBands + tid];
-      float val = (float)(sum * sqrt(2. / 22));
-      if (tid == 0) val -= 12;
-      if (tid == 1) val -= 4;
-      a.Lyf[(size_t)f * kBands + tid] = val;
+        for (int j = 0; j < kBands; j++) sum += Ly[fr][j] * T.dct[j * kBands + b];
+        float val = (float)(sum * sqrt(2. / 22));
+        if (b == 0) val -= 12;
+        if (b == 1) val -= 4;
+        a.Lyf[(size_t)fidx[fr] * kBands + b] = val;
+      }
     }
     __syncthreads();
   }
@@ -640,55 +701,82 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
 // ---------------------------------------------------------------------------
 // k_pspec: pitch spectrum P, Ep, normalised Exp, DCT(Exp)[0..5], feature 40
 // ---------------------------------------------------------------------------
-template <int NT>
-__global__ void __launch_bounds__(NT) k_pspec(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[kWin];
-  __shared__ __attribute__((aligned(16))) float2 Xl[kFreq + 1];
-  __shared__ float Ep[kBands + 2], Exp[kBands + 2];
+template <int F>
+__global__ void __launch_bounds__(256) k_pspec(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 W[F][kWin];
+  __shared__ __attribute__((aligned(16))) float2 Xl[F][kFreq + 1];
+  __shared__ BandTab T;
+  __shared__ float Ep[F][kBands + 2], Exp[F][kBands + 2];
+  __shared__ int fidx[F], pit[F];
   const int tid = threadIdx.x;
-  const Plan *__restrict__ P = a.plan;
-  const float2 *__restrict__ tw = reinterpret_cast<const float2 *>(P->tw960);
-  const float *__restrict__ hw = P->half_window;
-  const int V = a.V, total = a.n_streams * V;
-  for (int f = blockIdx.x; f < total; f += gridDim.x) {
-    const int s = f / V, v = f - s * V;
-    if (v >= ticks_of(a, s) * a.n_channels) continue;
-    const int pitch = a.pitch[f];
-    const float *pb = a.xs + (size_t)s * a.L + (size_t)v * kFrame;
-    for (int i = tid; i < kWin; i += NT) {
-      float val = pb[kPitchBuf - kWin - pitch + i];
-      val *= win960(hw, i);
-      W[P->bitrev960[i]] = make_float2(kScale960 * val, kScale960 * 0.0f);
-    }
-    const float2 *Xg = a.X + (size_t)f * kFreq;
-    for (int k = tid; k < kFreq; k += NT) Xl[k] = Xg[k];
+  FrameCtx cx;
+  frame_ctx_load(cx, a.plan, tid);
+  bandtab_load(T, a.plan, tid, 256);
+  const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
+  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    group_frames<F>(a, g, tid, fidx);
     __syncthreads();
-    fft960_stages<NT>(W, tw, tid);
-    float2 *Pg = a.P + (size_t)f * kFreq;
-    for (int k = tid; k < kFreq; k += NT) Pg[k] = W[k];
-    if (tid < kBands)
-      Ep[tid] = band_sum(W, W, P, tid);
-    else if (tid >= 32 && tid < 32 + kBands)
-      Exp[tid - 32] = band_sum(Xl, W, P, tid - 32);
+    if (tid < F) pit[tid] = fidx[tid] >= 0 ? a.pitch[fidx[tid]] : 0;
     __syncthreads();
-    if (tid < kBands) {
-      const float ex = a.Ex[(size_t)f * kBands + tid];
-      const float e = (float)((double)Exp[tid] / sqrt(.001 + (double)(ex * Ep[tid])));
-      Exp[tid] = e;
-      a.Ep[(size_t)f * kBands + tid] = Ep[tid];
-      a.Exp[(size_t)f * kBands + tid] = e;
-    }
-    __syncthreads();
-    if (tid < 6) {
-      float sum = 0;
 #pragma unroll
-      for (int j = 0; j < kBands; j++) sum += Exp[j] * P->dct[j * kBands + tid];
-      float val = (float)(sum * sqrt(2. / 22));
-      if (tid == 0) val = (float)(val - 1.3);
-      if (tid == 1) val = (float)(val - 0.9);
-      a.f34[(size_t)f * 8 + tid] = val;
-    } else if (tid == 32) {
-      a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pitch - 300));
+    for (int fr = 0; fr < F; fr++) {
+      const int f = fidx[fr];
+      if (f < 0) continue;
+      const float *pb = frame_pb(a, f) + (kPitchBuf - kWin - pit[fr]);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int i = tid + 256 * r;
+        if (i < kWin) {
+          float val = pb[i];
+          val *= cx.win[r];
+          W[fr][cx.dst[r]] = make_float2(kScale960 * val, kScale960 * 0.0f);
+        }
+      }
+    }
+    for (int idx = tid; idx < F * kFreq; idx += 256) {
+      const int fr = idx / kFreq, k = idx - fr * kFreq;
+      if (fidx[fr] >= 0) Xl[fr][k] = a.X[(size_t)fidx[fr] * kFreq + k];
+    }
+    __syncthreads();
+    fft960_run<F>(cx.tw, W, tid);
+    for (int idx = tid; idx < F * kFreq; idx += 256) {
+      const int fr = idx / kFreq, k = idx - fr * kFreq;
+      if (fidx[fr] >= 0) a.P[(size_t)fidx[fr] * kFreq + k] = W[fr][k];
+    }
+    if (tid < 2 * F * kBands) {
+      const int h = tid / (F * kBands), r = tid - h * (F * kBands), fr = r / kBands, b = r - fr * kBands;
+      if (h == 0)
+        Ep[fr][b] = band_sum_t(W[fr], W[fr], T, b);
+      else
+        Exp[fr][b] = band_sum_t(Xl[fr], W[fr], T, b);
+    }
+    __syncthreads();
+    if (tid < F * kBands) {
+      const int fr = tid / kBands, b = tid - fr * kBands;
+      const int f = fidx[fr];
+      if (f >= 0) {
+        const float ex = a.Ex[(size_t)f * kBands + b];
+        const float e = (float)((double)Exp[fr][b] / sqrt(.001 + (double)(ex * Ep[fr][b])));
+        Exp[fr][b] = e;
+        a.Ep[(size_t)f * kBands + b] = Ep[fr][b];
+        a.Exp[(size_t)f * kBands + b] = e;
+      }
+    }
+    __syncthreads();
+    if (tid < F * 8) {
+      const int fr = tid >> 3, i = tid & 7;
+      const int f = fidx[fr];
+      if (f >= 0 && i < 6) {
+        float sum = 0;
+#pragma unroll
+        for (int j = 0; j < kBands; j++) sum += Exp[fr][j] * T.dct[j * kBands + i];
+        float val = (float)(sum * sqrt(2. / 22));
+        if (i == 0) val = (float)(val - 1.3);
+        if (i == 1) val = (float)(val - 0.9);
+        a.f34[(size_t)f * 8 + i] = val;
+      } else if (f >= 0 && i == 6) {
+        a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pit[fr] - 300));
+      }
     }
     __syncthreads();
   }
@@ -989,82 +1077,110 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
 // smoothed gains are known), then the inverse transform (forward FFT of the
 // Hermitian extension) and the synthesis window
 // ---------------------------------------------------------------------------
-template <int NT>
-__global__ void __launch_bounds__(NT) k_synth(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[kWin];
-  __shared__ __attribute__((aligned(16))) float2 Xl[kFreq + 1];
-  __shared__ float rr[kBands + 2], nrm[kBands + 2], gs[kBands + 2], newE[kBands + 2];
-  __shared__ int sil;
+template <int F>
+__global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 W[F][kWin];
+  __shared__ __attribute__((aligned(16))) float2 Xl[F][kFreq + 1];
+  __shared__ BandTab T;
+  __shared__ float rr[F][kBands + 2], nrm[F][kBands + 2], gs[F][kBands + 2], newE[F][kBands + 2];
+  __shared__ int fidx[F], fil[F];
   const int tid = threadIdx.x;
-  const Plan *__restrict__ P = a.plan;
-  const float2 *__restrict__ tw = reinterpret_cast<const float2 *>(P->tw960);
-  const float *__restrict__ hw = P->half_window;
-  const int V = a.V, total = a.n_streams * V;
-  for (int f = blockIdx.x; f < total; f += gridDim.x) {
-    const int s = f / V, v = f - s * V;
-    if (v >= ticks_of(a, s) * a.n_channels) continue;
-    const float2 *Xg = a.X + (size_t)f * kFreq;
-    for (int k = tid; k < kFreq; k += NT) Xl[k] = Xg[k];
-    if (tid == 0) sil = a.silence[f];
+  FrameCtx cx;
+  frame_ctx_load(cx, a.plan, tid);
+  bandtab_load(T, a.plan, tid, 256);
+  const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
+  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    group_frames<F>(a, g, tid, fidx);
     __syncthreads();
-    if (!sil) {
-      if (tid < kBands) {
-        const int i = tid;
-        const float Exp = a.Exp[(size_t)f * kBands + i], g = a.gr[(size_t)f * kBands + i];
-        const float Ex = a.Ex[(size_t)f * kBands + i], Ep = a.Ep[(size_t)f * kBands + i];
+    if (tid < F) fil[tid] = fidx[tid] >= 0 && !a.silence[fidx[tid]];  // silent frames: X passes through
+    for (int idx = tid; idx < F * kFreq; idx += 256) {
+      const int fr = idx / kFreq, k = idx - fr * kFreq;
+      if (fidx[fr] >= 0) Xl[fr][k] = a.X[(size_t)fidx[fr] * kFreq + k];
+    }
+    __syncthreads();
+    if (tid < F * kBands) {
+      const int fr = tid / kBands, i = tid - fr * kBands;
+      if (fil[fr]) {
+        const size_t o = (size_t)fidx[fr] * kBands + i;
+        const float Exp = a.Exp[o], gg = a.gr[o], Ex = a.Ex[o], Ep = a.Ep[o];
         float r;
-        if (Exp > g)
+        if (Exp > gg)
           r = 1;
         else
-          r = (float)((double)((Exp * Exp) * (1 - (g * g))) / (.001 + (double)((g * g) * (1 - (Exp * Exp)))));
+          r = (float)((double)((Exp * Exp) * (1 - (gg * gg))) / (.001 + (double)((gg * gg) * (1 - (Exp * Exp)))));
         float cl = (0 > r) ? 0 : r;
         cl = (1 < cl) ? 1 : cl;
         r = (float)sqrt((double)cl);
         r = (float)((double)r * sqrt((double)Ex / (1e-8 + (double)Ep)));
-        rr[i] = r;
-        gs[i] = a.gs[(size_t)f * kBands + i];
+        rr[fr][i] = r;
+        gs[fr][i] = a.gs[o];
       }
-      __syncthreads();
-      const float2 *Pg = a.P + (size_t)f * kFreq;
-      for (int k = tid; k < kFreq; k += NT) {
-        const float rf = interp_gain(rr, P, k);
-        const float2 pk = Pg[k];
-        Xl[k].x += rf * pk.x;
-        Xl[k].y += rf * pk.y;
-      }
-      __syncthreads();
-      if (tid < kBands) newE[tid] = band_sum(Xl, Xl, P, tid);
-      __syncthreads();
-      if (tid < kBands) nrm[tid] = (float)sqrt((double)a.Ex[(size_t)f * kBands + tid] / (1e-8 + (double)newE[tid]));
-      __syncthreads();
-      for (int k = tid; k < kFreq; k += NT) {
-        const float nf = interp_gain(nrm, P, k);
-        float2 val = Xl[k];
-        val.x *= nf;
-        val.y *= nf;
-        const float gf = interp_gain(gs, P, k);
-        val.x *= gf;
-        val.y *= gf;
-        Xl[k] = val;
-      }
-      __syncthreads();
-    }
-    for (int i = tid; i < kWin; i += NT) {
-      float2 val;
-      if (i < kFreq) {
-        val = Xl[i];
-      } else {
-        const float2 c = Xl[kWin - i];
-        val = make_float2(c.x, -c.y);
-      }
-      W[P->bitrev960[i]] = make_float2(kScale960 * val.x, kScale960 * val.y);
     }
     __syncthreads();
-    fft960_stages<NT>(W, tw, tid);
-    float *y = a.ys + (size_t)f * kWin;
-    for (int i = tid; i < kWin; i += NT) {
-      const float yv = (i == 0) ? kWin * W[0].x : kWin * W[kWin - i].x;
-      y[i] = yv * win960(hw, i);
+    for (int idx = tid; idx < F * kFreq; idx += 256) {
+      const int fr = idx / kFreq, k = idx - fr * kFreq;
+      if (fil[fr]) {
+        const float rf = interp_gain_t(rr[fr], T, k);
+        const float2 pk = a.P[(size_t)fidx[fr] * kFreq + k];
+        Xl[fr][k].x += rf * pk.x;
+        Xl[fr][k].y += rf * pk.y;
+      }
+    }
+    __syncthreads();
+    if (tid < F * kBands) {
+      const int fr = tid / kBands, i = tid - fr * kBands;
+      if (fil[fr]) {
+        newE[fr][i] = band_sum_t(Xl[fr], Xl[fr], T, i);
+        nrm[fr][i] = (float)sqrt((double)a.Ex[(size_t)fidx[fr] * kBands + i] / (1e-8 + (double)newE[fr][i]));
+      }
+    }
+    __syncthreads();
+    for (int idx = tid; idx < F * kFreq; idx += 256) {
+      const int fr = idx / kFreq, k = idx - fr * kFreq;
+      if (fil[fr]) {
+        const float nf = interp_gain_t(nrm[fr], T, k);
+        float2 val = Xl[fr][k];
+        val.x *= nf;
+        val.y *= nf;
+        const float gf = interp_gain_t(gs[fr], T, k);
+        val.x *= gf;
+        val.y *= gf;
+        Xl[fr][k] = val;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int fr = 0; fr < F; fr++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int i = tid + 256 * r;
+        if (i < kWin) {
+          float2 val;
+          if (i < kFreq) {
+            val = Xl[fr][i];
+          } else {
+            const float2 c = Xl[fr][kWin - i];
+            val = make_float2(c.x, -c.y);
+          }
+          W[fr][cx.dst[r]] = make_float2(kScale960 * val.x, kScale960 * val.y);
+        }
+      }
+    }
+    __syncthreads();
+    fft960_run<F>(cx.tw, W, tid);
+#pragma unroll
+    for (int fr = 0; fr < F; fr++) {
+      const int f = fidx[fr];
+      if (f < 0) continue;
+      float *y = a.ys + (size_t)f * kWin;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int i = tid + 256 * r;
+        if (i < kWin) {
+          const float yv = (i == 0) ? kWin * W[fr][0].x : kWin * W[fr][kWin - i].x;
+          y[i] = yv * cx.win[r];
+        }
+      }
     }
     __syncthreads();
   }
@@ -1234,13 +1350,30 @@ const char *staged_kernel_name(int i) {
   return (i >= 0 && i < kStagedKernels) ? names[i] : nullptr;
 }
 
-hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t stream, hipEvent_t *ev) {
+namespace {
+// persistent grids: exactly the resident capacity (blocks per CU from the
+// occupancy calculator x CUs), so no workgroup starts late and leaves a tail
+template <typename K>
+int resident_blocks(K kernel, int threads, int n_cu) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  return per_cu * n_cu;
+}
+}  // namespace
+
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev) {
   constexpr int NT = 256;
+  constexpr int FF = kFftFrames;
+  static const int g_fftA = resident_blocks(k_fftA<FF>, 256, n_cu);
+  static const int g_pspec = resident_blocks(k_pspec<FF>, 256, n_cu);
+  static const int g_synth = resident_blocks(k_synth<FF>, 256, n_cu);
+  static const int g_pitch4 = resident_blocks(k_pitch<4>, 256, n_cu);
+  static const int g_pitch8 = resident_blocks(k_pitch<8>, 256, n_cu);
   // lane-per-stream kernels: 16 streams per workgroup spreads the serial
   // chains over more CUs (each chain is latency-bound, not lane-bound)
   const int lane_blocks = (a.n_streams + 15) / 16;
   const long long frames = (long long)a.n_streams * a.V;
-  const int g = (int)std::min<long long>(frames, grid_frames);
+  auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
   (void)hipGetLastError();
   auto rec = [&](int k) {
     if (ev) (void)hipEventRecord(ev[k], stream);
@@ -1251,7 +1384,8 @@ hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t strea
     hipLaunchKernelGGL(k_prep2, dim3((a.n_streams + S - 1) / S), dim3(256), 0, stream, a);
   }
   rec(1);
-  hipLaunchKernelGGL(k_fftA<NT>, dim3(g), dim3(NT), 0, stream, a);
+  const long long fgroups = (frames + FF - 1) / FF;
+  hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, stream, a);
   rec(2);
   {
     // frames per k_pitch workgroup: 4 (default) or 8 (FVAD_PITCH_FRAMES=8, tuning only)
@@ -1260,21 +1394,20 @@ hipError_t launch_staged(const StagedArgs &a, int grid_frames, hipStream_t strea
       return (e && atoi(e) == 8) ? 8 : kPitchFrames;
     }();
     const long long groups = (frames + fp - 1) / fp;
-    const unsigned gp = (unsigned)std::min<long long>(groups, grid_frames);
     if (fp == 8)
-      hipLaunchKernelGGL(k_pitch<8>, dim3(gp), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL(k_pitch<8>, grid(groups, g_pitch8), dim3(256), 0, stream, a);
     else
-      hipLaunchKernelGGL(k_pitch<kPitchFrames>, dim3(gp), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL(k_pitch<4>, grid(groups, g_pitch4), dim3(256), 0, stream, a);
   }
   rec(3);
   hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(4);
-  hipLaunchKernelGGL(k_pspec<NT>, dim3(g), dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
   rec(5);
   hipLaunchKernelGGL((k_rnn<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
                      stream, a);
   rec(6);
-  hipLaunchKernelGGL(k_synth<NT>, dim3(g), dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
   rec(7);
   const long long ola_threads = frames * kFrame;
   hipLaunchKernelGGL(k_ola, dim3((unsigned)((ola_threads + 255) / 256)), dim3(256), 0, stream, a);
