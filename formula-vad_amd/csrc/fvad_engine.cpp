@@ -121,12 +121,17 @@ int dalloc(T **p, size_t count) {
   return FVAD_OK;
 }
 
-// int8 GRU-stack image for k_rnn (layout: fvad_internal.h rnnimg)
+// int8 GRU-stack image for k_rnn (layout: fvad_internal.h rnnimg).  Term j of
+// a column's C-order sum lives in segment g at seg_off(g) + (j - start of g).
 void build_rnn_image(const fvad::HostModel &hm, std::vector<int8_t> &img, int *act) {
   namespace R = fvad::rnnimg;
   img.assign(R::kBytes, 0);
   const int8_t *b = hm.blob;
-  auto put = [&](int m, int c, int j, int8_t v) { img[R::off_w(m) + c * R::stride(m) + j] = v; };
+  auto put = [&](int m, int c, int j, int8_t v) {
+    int g = 0, base = 0;
+    while (j >= base + R::kSegs[m][g]) base += R::kSegs[m][g++];
+    img[R::off_w(m) + c * R::stride(m) + R::seg_off(m, g) + (j - base)] = v;
+  };
   auto dense = [&](int m, int l) {
     const fvad::HostLayer &L = hm.layers[l];
     for (int c = 0; c < L.nout; c++) {
@@ -423,6 +428,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.out_den = e->d_den;
   a.out_win_flag = e->d_wflag;
   a.raw_s16 = e->raw_s16;
+  a.stamps = e->d_stamps;
   HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr));
   return FVAD_OK;
 }

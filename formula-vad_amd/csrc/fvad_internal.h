@@ -63,8 +63,19 @@ constexpr int kMats = 9;
 constexpr int kCols[kMats] = {24, 48, 24, 96, 48, 192, 96, 22, 1};
 constexpr int kKin[kMats] = {42, 24, 24, 90, 90, 114, 114, 96, 24};  // input-vector part of K
 constexpr int kK[kMats] = {42, 48, 48, 138, 138, 210, 210, 96, 24};
+// Summation segments of a column (inputs in concatenation order, then the
+// GRU state); each starts 8-byte aligned so 8 weights are one 64-bit LDS read.
+constexpr int kSegs[kMats][4] = {{42, 0, 0, 0},   {24, 24, 0, 0},  {24, 24, 0, 0},
+                                 {24, 24, 42, 48}, {24, 24, 42, 48}, {24, 48, 42, 96},
+                                 {24, 48, 42, 96}, {96, 0, 0, 0},   {24, 0, 0, 0}};
+constexpr int pad8(int x) { return (x + 7) & ~7; }
 constexpr int pad16(int x) { return (x + 15) & ~15; }
-constexpr int stride(int m) { return (kK[m] + 3) & ~3; }  // bytes per column
+constexpr int seg_off(int m, int g) {  // byte offset of segment g inside a column
+  int o = 0;
+  for (int i = 0; i < g; i++) o += pad8(kSegs[m][i]);
+  return o;
+}
+constexpr int stride(int m) { return seg_off(m, 4); }  // bytes per column
 constexpr int off_b(int m) {
   int o = 0;
   for (int i = 0; i < m; i++) o += pad16(kCols[i]) + pad16(kCols[i] * stride(i));

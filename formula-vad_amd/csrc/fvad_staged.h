@@ -47,6 +47,7 @@ struct StagedArgs {
   float *out_vad, *out_win_ratio, *out_win_vad, *out_band, *out_den;
   int *out_win_flag;
   int raw_s16;
+  unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn
 };
 
 // Launch the 10 kernels on `stream`; when ev != nullptr, ev[0..10] are

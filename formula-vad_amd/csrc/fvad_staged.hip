@@ -789,79 +789,173 @@ __global__ void __launch_bounds__(256) k_pspec(StagedArgs a) {
 // weights never come from L2 per frame.  A matrix column = one neuron's C-order
 // sum: lane (column, stream group) accumulates SL streams of that column with
 // one weight fetch per term; per-stream vectors are stored [j][S] so the SL
-// inputs of a term are one 16-byte LDS read.  Per frame and stream:
+// inputs of a term are one LDS read.  GRU inputs are read in place from their
+// segments (no concatenation copies), GRU states ping-pong between two
+// buffers (no copy-back phase), and the next frame's features are prefetched
+// into registers while the current frame runs.  Per frame and stream:
 // cepstral memory + deltas, spectral variability (distance matrix kept in the
 // state, only the new row recomputed), compute_rnn, and the gain recurrence
-// lastg; the pitch filter and gain application move to k_synth (they depend
-// on nothing recurrent once g and the smoothed gains are known).
+// lastg; the pitch filter and gain application are in k_synth (nothing
+// recurrent is left in them once g and the smoothed gains are known).
 // ---------------------------------------------------------------------------
 constexpr int kRnnS = 8;   // streams per workgroup
-constexpr int kRnnG = 2;   // lanes per column (stream groups)
-constexpr int kRnnNT = 512;
+constexpr int kRnnG = 4;   // lanes per column (stream groups of S/G = 2)
+constexpr int kRnnNT = 1024;
+constexpr int kRnnPf = 30; // prefetched words per stream and frame: Lyf[22], f34[7], silence
 
-template <int S, int SL>
-__device__ __forceinline__ void mv_terms(const int8_t *__restrict__ wc, int j0, int j1, const float *vT, int jv0,
-                                         int s0, float (&acc)[SL]) {
-  // acc[q] += w[j] * v[j - j0 + jv0][s0 + q], j in [j0, j1), C order
-#pragma unroll 8
-  for (int j = j0; j < j1; j++) {
-    const float w = (float)wc[j];
-    const float *v = vT + (jv0 + j - j0) * S + s0;
-#pragma unroll
-    for (int q = 0; q < SL; q++) acc[q] = acc[q] + w * v[q];
+// Diagnostic build only (-DFVAD_STAMPS): per-phase s_memtime totals of thread 0
+#ifdef FVAD_STAMPS
+#define RSTAMP(id)                                                \
+  do {                                                            \
+    if (tid == 0) {                                               \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+      st_acc[id] += t_ - st_last;                                 \
+      st_last = t_;                                               \
+    }                                                             \
+  } while (0)
+#else
+#define RSTAMP(id) \
+  do {             \
+  } while (0)
+#endif
+
+// acc[q] += w[j] * v[j][s0 + q] for the n terms of one segment, C order.  The
+// segment's weights start 8-byte aligned: 8 terms = one 64-bit LDS read plus
+// eight SL-float input reads, all issued before the arithmetic.
+template <int SL>
+struct VecT;
+template <>
+struct VecT<2> {
+  typedef float2 T;
+};
+template <>
+struct VecT<4> {
+  typedef float4 T;
+};
+__device__ __forceinline__ float wbyte(uint2 w8, int u) {
+  return (float)(signed char)((u < 4 ? w8.x : w8.y) >> (8 * (u & 3)));
+}
+template <int SL>
+__device__ __forceinline__ void mac(float (&acc)[SL], float w, const typename VecT<SL>::T &v) {
+  acc[0] = acc[0] + w * v.x;
+  acc[1] = acc[1] + w * v.y;
+  if constexpr (SL == 4) {
+    acc[2] = acc[2] + w * v.z;
+    acc[3] = acc[3] + w * v.w;
+  }
+}
+template <int SL>
+__device__ __forceinline__ void mac_r(float (&acc)[SL], float w, const typename VecT<SL>::T &sv,
+                                      const typename VecT<SL>::T &rv) {
+  acc[0] = acc[0] + w * sv.x * rv.x;
+  acc[1] = acc[1] + w * sv.y * rv.y;
+  if constexpr (SL == 4) {
+    acc[2] = acc[2] + w * sv.z * rv.z;
+    acc[3] = acc[3] + w * sv.w * rv.w;
   }
 }
 
-// dense / GRU gate matrix m: out[c][s] = act(kWs * (b[c] + sum_j w[c][j] * in[j][s]))
-// (for gates the input is [in ; state] with the state part starting at kKin[m])
+template <int n, int S, int SL>
+__device__ __forceinline__ void mv_seg(const int8_t *__restrict__ wc, const float *vT, int s0, float (&acc)[SL]) {
+  typedef typename VecT<SL>::T V;
+  constexpr int nb = n / 8, r = n % 8;
+#pragma unroll 1
+  for (int jb = 0; jb < nb; jb++) {
+    const uint2 w8 = *reinterpret_cast<const uint2 *>(wc + jb * 8);
+    V v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const V *>(vT + (jb * 8 + u) * S + s0);
+#pragma unroll
+    for (int u = 0; u < 8; u++) mac<SL>(acc, wbyte(w8, u), v[u]);
+  }
+  if (r) {
+    const uint2 w8 = *reinterpret_cast<const uint2 *>(wc + nb * 8);
+#pragma unroll
+    for (int u = 0; u < r; u++) mac<SL>(acc, wbyte(w8, u), *reinterpret_cast<const V *>(vT + (nb * 8 + u) * S + s0));
+  }
+}
+
+// GRU candidate recurrent segment: acc[q] += (w[j] * state[j][q]) * r[j][q]
+template <int n, int S, int SL>
+__device__ __forceinline__ void mv_seg_r(const int8_t *__restrict__ wc, const float *sT, const float *rT, int s0,
+                                         float (&acc)[SL]) {
+  typedef typename VecT<SL>::T V;
+  static_assert(n % 8 == 0, "recurrent segment shape");
+#pragma unroll 1
+  for (int jb = 0; jb < n / 8; jb++) {
+    const uint2 w8 = *reinterpret_cast<const uint2 *>(wc + jb * 8);
+    V sv[8], rv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      sv[u] = *reinterpret_cast<const V *>(sT + (jb * 8 + u) * S + s0);
+      rv[u] = *reinterpret_cast<const V *>(rT + (jb * 8 + u) * S + s0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) mac_r<SL>(acc, wbyte(w8, u), sv[u], rv[u]);
+  }
+}
+
+// Input of one matrix: its input-vector segments in concatenation order.
+struct RnnIn {
+  const float *v0, *v1, *v2;
+};
+
+template <int m, int S, int SL>
+__device__ __forceinline__ void rnn_inputs(const int8_t *wc, const RnnIn &in, int s0, float (&acc)[SL]) {
+  constexpr int n0 = rnnimg::kSegs[m][0];
+  mv_seg<n0, S, SL>(wc, in.v0, s0, acc);
+  if constexpr (m == 3 || m == 4 || m == 5 || m == 6) {
+    constexpr int n1 = rnnimg::kSegs[m][1], n2 = rnnimg::kSegs[m][2];
+    mv_seg<n1, S, SL>(wc + rnnimg::seg_off(m, 1), in.v1, s0, acc);
+    mv_seg<n2, S, SL>(wc + rnnimg::seg_off(m, 2), in.v2, s0, acc);
+  }
+}
+
+// dense layer / GRU z|r gates of image matrix m:
+//   out[c][s] = act(kWs * (b[c] + sum_j w[c][j] * [in ; state][j][s]))
 template <int m, int S, int G, int NT>
-__device__ void rnn_mat(const int8_t *W, const float *inT, const float *stT, float *outT, int act,
-                        const float *tt, int tid) {
-  constexpr int SL = S / G, cols = rnnimg::kCols[m], kin = rnnimg::kKin[m], K = rnnimg::kK[m];
+__device__ __forceinline__ void rnn_gates(const int8_t *W, const RnnIn &in, const float *stT, float *outT, int act,
+                                          const float *tt, int tid) {
+  constexpr int SL = S / G, cols = rnnimg::kCols[m];
   constexpr int ob = rnnimg::off_b(m), ow = rnnimg::off_w(m), ws = rnnimg::stride(m);
+  constexpr int gst = (m == 1) ? 1 : (m == 3 || m == 5) ? 3 : -1;  // state segment of z|r matrices
   for (int t = tid; t < cols * G; t += NT) {
     const int c = t / G, s0 = (t - c * G) * SL;
     const int8_t *wc = W + ow + c * ws;
-    const float b = (float)W[ob + c];
     float acc[SL];
+    const float b = (float)W[ob + c];
 #pragma unroll
     for (int q = 0; q < SL; q++) acc[q] = b;
-    mv_terms<S, SL>(wc, 0, kin, inT, 0, s0, acc);
-    if (K > kin) mv_terms<S, SL>(wc, kin, K, stT, 0, s0, acc);
+    rnn_inputs<m, S, SL>(wc, in, s0, acc);
+    if constexpr (gst >= 0) mv_seg<rnnimg::kSegs[m][gst], S, SL>(wc + rnnimg::seg_off(m, gst), stT, s0, acc);
 #pragma unroll
     for (int q = 0; q < SL; q++) outT[c * S + s0 + q] = activate(tt, act, kWs * acc[q]);
   }
 }
 
-// GRU candidate matrix m (h part): sum = b + sum_j w*in[j] + sum_j (w*state[j])*r[j];
-// h = z*state + (1-z)*act(kWs*sum)
+// GRU candidate of image matrix m: sum = b + sum_j w*in[j] + sum_j (w*state[j])*r[j];
+// new[c][s] = z*state + (1-z)*act(kWs*sum) for active streams, state otherwise
 template <int m, int S, int G, int NT>
-__device__ void rnn_h(const int8_t *W, const float *inT, const float *stT, const float *zrT, float *hT, int act,
-                      const float *tt, int tid) {
-  constexpr int SL = S / G, cols = rnnimg::kCols[m], kin = rnnimg::kKin[m], K = rnnimg::kK[m];
+__device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const float *stT, const float *zrT,
+                                         float *newT, const int *actv, int act, const float *tt, int tid) {
+  constexpr int SL = S / G, cols = rnnimg::kCols[m], N = cols;
   constexpr int ob = rnnimg::off_b(m), ow = rnnimg::off_w(m), ws = rnnimg::stride(m);
-  constexpr int N = cols;
+  constexpr int gst = (m == 2) ? 1 : 3;
   for (int t = tid; t < cols * G; t += NT) {
     const int c = t / G, s0 = (t - c * G) * SL;
     const int8_t *wc = W + ow + c * ws;
-    const float b = (float)W[ob + c];
     float acc[SL];
+    const float b = (float)W[ob + c];
 #pragma unroll
     for (int q = 0; q < SL; q++) acc[q] = b;
-    mv_terms<S, SL>(wc, 0, kin, inT, 0, s0, acc);
-#pragma unroll 8
-    for (int j = kin; j < K; j++) {
-      const float w = (float)wc[j];
-      const float *sv = stT + (j - kin) * S + s0;
-      const float *rv = zrT + (N + j - kin) * S + s0;
-#pragma unroll
-      for (int q = 0; q < SL; q++) acc[q] = acc[q] + w * sv[q] * rv[q];
-    }
+    rnn_inputs<m, S, SL>(wc, in, s0, acc);
+    mv_seg_r<rnnimg::kSegs[m][gst], S, SL>(wc + rnnimg::seg_off(m, gst), stT, zrT + N * S, s0, acc);
 #pragma unroll
     for (int q = 0; q < SL; q++) {
+      const int o = c * S + s0 + q;
       const float sum = activate(tt, act, kWs * acc[q]);
-      const float z = zrT[c * S + s0 + q];
-      hT[c * S + s0 + q] = z * stT[c * S + s0 + q] + (1 - z) * sum;
+      const float z = zrT[o];
+      newT[o] = actv[s0 + q] ? z * stT[o] + (1 - z) * sum : stT[o];
     }
   }
 }
@@ -873,22 +967,21 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
   __shared__ __attribute__((aligned(16))) float featT[44 * S];
   __shared__ float ceps[S][kCeps * kBands];
   __shared__ float dist[S][kCeps * kCeps];
-  __shared__ __attribute__((aligned(16))) float doutT[24 * S], gvT[24 * S], gnT[48 * S], gdT[96 * S];
-  __shared__ __attribute__((aligned(16))) float zrT[192 * S], hT[96 * S], rinT[116 * S];
+  __shared__ __attribute__((aligned(16))) float doutT[24 * S], gvT[2][24 * S], gnT[2][48 * S], gdT[2][96 * S];
+  __shared__ __attribute__((aligned(16))) float zrT[192 * S];
   __shared__ float lastg[S][kBands];
+  __shared__ float pf[S][kRnnPf];  // features of the current frame (prefetched)
   __shared__ int memid[S], act[S], nfs[S];
   __shared__ long long fbase[S];
   __shared__ float vad_s[S];
   const int tid = threadIdx.x;
   const int sb = blockIdx.x * S;
-  // GRU image + tansig table -> LDS
   {
     const int4 *src = reinterpret_cast<const int4 *>(a.rnn_img);
     int4 *dst = reinterpret_cast<int4 *>(W);
     for (int i = tid; i < rnnimg::kBytes / 16; i += NT) dst[i] = src[i];
     for (int i = tid; i < 201; i += NT) tt[i] = a.plan->tansig[i];
   }
-  // per-stream state -> LDS
   for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
     const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
     ceps[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] : 0.0f;
@@ -905,9 +998,9 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
     const int s = idx / 96, i = idx - s * 96;
     const bool ok = sb + s < a.n_streams;
     const float *stp = a.state + (size_t)(sb + s) * st::kWords;
-    if (i < 24) gvT[i * S + s] = ok ? stp[st::kVadGru + i] : 0.0f;
-    if (i < 48) gnT[i * S + s] = ok ? stp[st::kNoiseGru + i] : 0.0f;
-    gdT[i * S + s] = ok ? stp[st::kDenGru + i] : 0.0f;
+    if (i < 24) gvT[0][i * S + s] = ok ? stp[st::kVadGru + i] : 0.0f;
+    if (i < 48) gnT[0][i * S + s] = ok ? stp[st::kNoiseGru + i] : 0.0f;
+    gdT[0][i * S + s] = ok ? stp[st::kDenGru + i] : 0.0f;
   }
   if (tid < S) {
     const int s = sb + tid;
@@ -920,58 +1013,70 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
   int maxnf = 0;
 #pragma unroll
   for (int s = 0; s < S; s++) maxnf = max(maxnf, nfs[s]);
+  // prefetch lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (as 1.0 / 0.0)
+  const int pfs = tid / kRnnPf, pfi = tid - pfs * kRnnPf;
+  const bool pf_lane = tid < S * kRnnPf;
+  auto fetch = [&](int v) -> float {
+    if (!pf_lane || v >= nfs[pfs]) return 1.0f;  // past the end: treated as silent (inactive)
+    const long long f = fbase[pfs] + v;
+    if (pfi < kBands) return a.Lyf[f * kBands + pfi];
+    if (pfi < kBands + 7) return a.f34[f * 8 + (pfi - kBands)];
+    return a.silence[f] ? 1.0f : 0.0f;
+  };
+  // frame 0's silence must be known before its Lyf (which k_fftA leaves unwritten for silent frames) is used
+  if (pf_lane) pf[pfs][pfi] = fetch(0);
+  __syncthreads();
+  if (tid < S) {
+    act[tid] = (0 < nfs[tid]) && pf[tid][kRnnPf - 1] == 0.0f;
+    if (0 < nfs[tid] && !act[tid]) a.vadf[fbase[tid]] = 0;
+  }
+  float pf_next = fetch(1);
   const int *ra = a.rnn_act;
+  __syncthreads();
+#ifdef FVAD_STAMPS
+  unsigned long long st_acc[16] = {};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
   for (int v = 0; v < maxnf; v++) {
-    if (tid < S) {
-      int ok = 0;
-      if (v < nfs[tid]) {
-        const long long f = fbase[tid] + v;
-        ok = !a.silence[f];
-        if (!ok) a.vadf[f] = 0;  // silent frame: X passes through, state untouched
-      }
-      act[tid] = ok;
-    }
-    __syncthreads();
-    // features 0..21 = DCT(Ly) (k_fftA), 34..40 (k_pspec); cepstral memory
-    for (int idx = tid; idx < S * 29; idx += NT) {
-      const int s = idx / 29, i = idx - s * 29;
-      if (!act[s]) continue;
-      const long long f = fbase[s] + v;
-      if (i < kBands) {
-        const float val = a.Lyf[f * kBands + i];
-        ceps[s][memid[s] * kBands + i] = val;
-        featT[i * S + s] = val;
-      } else {
-        featT[(34 + i - kBands) * S + s] = a.f34[f * 8 + (i - kBands)];
-      }
-    }
-    __syncthreads();
-    // deltas (features 0..5, 22..33) and the new row of the distance matrix
-    for (int idx = tid; idx < S * 14; idx += NT) {
-      const int s = idx / 14, i = idx - s * 14;
+    const int cur = v & 1, nxt = cur ^ 1;
+    // C: features 0..21 = DCT(Ly) (k_fftA) -> cepstral memory, deltas, the new
+    //    row of the distance matrix, features 34..40 (k_pspec)
+    for (int idx = tid; idx < S * (kBands + 7 + kCeps); idx += NT) {
+      const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
       if (!act[s]) continue;
       const int mi = memid[s];
-      const float *c0 = ceps[s] + mi * kBands;
-      if (i < 6) {
-        const float *c1 = ceps[s] + ((mi < 1) ? kCeps + mi - 1 : mi - 1) * kBands;
-        const float *c2 = ceps[s] + ((mi < 2) ? kCeps + mi - 2 : mi - 2) * kBands;
-        featT[i * S + s] = c0[i] + c1[i] + c2[i];
-        featT[(kBands + i) * S + s] = c0[i] - c2[i];
-        featT[(kBands + 6 + i) * S + s] = c0[i] - 2 * c1[i] + c2[i];
-      } else {
-        const int j = i - 6;
-        const float *cj = ceps[s] + j * kBands;
-        float d = 0;
-#pragma unroll
-        for (int k = 0; k < kBands; k++) {
-          const float tmp = c0[k] - cj[k];
-          d += tmp * tmp;
+      const float *c0 = pf[s];  // ceps_0 (the row being written at memid)
+      if (i < kBands) {
+        ceps[s][mi * kBands + i] = c0[i];
+        if (i < 6) {
+          const float *c1 = ceps[s] + ((mi < 1) ? kCeps + mi - 1 : mi - 1) * kBands;
+          const float *c2 = ceps[s] + ((mi < 2) ? kCeps + mi - 2 : mi - 2) * kBands;
+          featT[i * S + s] = c0[i] + c1[i] + c2[i];
+          featT[(kBands + i) * S + s] = c0[i] - c2[i];
+          featT[(kBands + 6 + i) * S + s] = c0[i] - 2 * c1[i] + c2[i];
+        } else {
+          featT[i * S + s] = c0[i];
         }
-        dist[s][mi * kCeps + j] = d;
-        dist[s][j * kCeps + mi] = d;
+      } else if (i < kBands + 7) {
+        featT[(34 + i - kBands) * S + s] = c0[i];
+      } else {
+        const int j = i - kBands - 7;
+        if (j != mi) {
+          const float *cj = ceps[s] + j * kBands;
+          float d = 0;
+#pragma unroll
+          for (int k = 0; k < kBands; k++) {
+            const float tmp = c0[k] - cj[k];
+            d += tmp * tmp;
+          }
+          dist[s][mi * kCeps + j] = d;
+          dist[s][j * kCeps + mi] = d;
+        }
       }
     }
     __syncthreads();
+    RSTAMP(0);
+    // D: spectral variability
     if (tid < S && act[tid]) {
       const int s = tid;
       float sv = 0;
@@ -987,67 +1092,76 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
       memid[s] = mid;
     }
     __syncthreads();
+    RSTAMP(1);
     // compute_rnn
-    rnn_mat<0, S, G, NT>(W, featT, nullptr, doutT, ra[0], tt, tid);
+    rnn_gates<0, S, G, NT>(W, RnnIn{featT, nullptr, nullptr}, nullptr, doutT, ra[0], tt, tid);
     __syncthreads();
-    rnn_mat<1, S, G, NT>(W, doutT, gvT, zrT, kActSigmoid, tt, tid);
+    RSTAMP(2);
+    rnn_gates<1, S, G, NT>(W, RnnIn{doutT, nullptr, nullptr}, gvT[cur], zrT, kActSigmoid, tt, tid);
     __syncthreads();
-    rnn_h<2, S, G, NT>(W, doutT, gvT, zrT, hT, ra[2], tt, tid);
+    RSTAMP(3);
+    rnn_cand<2, S, G, NT>(W, RnnIn{doutT, nullptr, nullptr}, gvT[cur], zrT, gvT[nxt], act, ra[2], tt,
+                          tid);
     __syncthreads();
-    for (int idx = tid; idx < 24 * S; idx += NT)
-      if (act[idx % S]) gvT[idx] = hT[idx];
-    __syncthreads();
+    RSTAMP(4);
     // noise_input = [dense_out, vad_state, features]; vad_output alongside
-    for (int idx = tid; idx < 90 * S; idx += NT) {
-      const int j = idx / S;
-      rinT[idx] = (j < 24) ? doutT[idx] : (j < 48) ? gvT[idx - 24 * S] : featT[idx - 48 * S];
-    }
+    rnn_gates<3, S, G, NT>(W, RnnIn{doutT, gvT[nxt], featT}, gnT[cur], zrT, kActSigmoid, tt, tid);
     if (tid >= NT - S) {
       const int s = tid - (NT - S);
       constexpr int ob = rnnimg::off_b(8), ow = rnnimg::off_w(8);
       float sum = (float)W[ob];
-      for (int j = 0; j < 24; j++) sum += (float)W[ow + j] * gvT[j * S + s];
+      for (int j = 0; j < 24; j++) sum += (float)W[ow + j] * gvT[nxt][j * S + s];
       vad_s[s] = activate(tt, ra[8], kWs * sum);
     }
     __syncthreads();
-    rnn_mat<3, S, G, NT>(W, rinT, gnT, zrT, kActSigmoid, tt, tid);
+    RSTAMP(5);
+    rnn_cand<4, S, G, NT>(W, RnnIn{doutT, gvT[nxt], featT}, gnT[cur], zrT, gnT[nxt], act, ra[4],
+                          tt, tid);
     __syncthreads();
-    rnn_h<4, S, G, NT>(W, rinT, gnT, zrT, hT, ra[4], tt, tid);
-    __syncthreads();
-    for (int idx = tid; idx < 48 * S; idx += NT)
-      if (act[idx % S]) gnT[idx] = hT[idx];
-    __syncthreads();
+    RSTAMP(6);
     // denoise_input = [vad_state, noise_state, features]
-    for (int idx = tid; idx < 114 * S; idx += NT) {
-      const int j = idx / S;
-      rinT[idx] = (j < 24) ? gvT[idx] : (j < 72) ? gnT[idx - 24 * S] : featT[idx - 72 * S];
-    }
+    rnn_gates<5, S, G, NT>(W, RnnIn{gvT[nxt], gnT[nxt], featT}, gdT[cur], zrT, kActSigmoid, tt,
+                           tid);
     __syncthreads();
-    rnn_mat<5, S, G, NT>(W, rinT, gdT, zrT, kActSigmoid, tt, tid);
+    RSTAMP(7);
+    rnn_cand<6, S, G, NT>(W, RnnIn{gvT[nxt], gnT[nxt], featT}, gdT[cur], zrT, gdT[nxt], act, ra[6],
+                          tt, tid);
     __syncthreads();
-    rnn_h<6, S, G, NT>(W, rinT, gdT, zrT, hT, ra[6], tt, tid);
+    RSTAMP(8);
+    rnn_gates<7, S, G, NT>(W, RnnIn{gdT[nxt], nullptr, nullptr}, nullptr, zrT, ra[7], tt, tid);
     __syncthreads();
-    for (int idx = tid; idx < 96 * S; idx += NT)
-      if (act[idx % S]) gdT[idx] = hT[idx];
-    __syncthreads();
-    rnn_mat<7, S, G, NT>(W, gdT, nullptr, zrT, ra[7], tt, tid);  // gains g[22][S] (zrT reused)
-    __syncthreads();
-    // gain smoothing g = max(g, .6*lastg) (denoise.c); outputs
+    RSTAMP(9);
+    // gain smoothing g = max(g, .6*lastg) (denoise.c) and outputs of frame v;
+    // the prefetched features of frame v+1 land in LDS
     for (int idx = tid; idx < S * kBands; idx += NT) {
       const int s = idx / kBands, i = idx - s * kBands;
       if (!act[s]) continue;
       const long long f = fbase[s] + v;
       const float gi = zrT[i * S + s];
       const float al = .6f * lastg[s][i];
-      const float gs = (gi > al) ? gi : al;
-      lastg[s][i] = gs;
+      const float gsm = (gi > al) ? gi : al;
+      lastg[s][i] = gsm;
       a.gr[f * kBands + i] = gi;
-      a.gs[f * kBands + i] = gs;
+      a.gs[f * kBands + i] = gsm;
       if (i == 0) a.vadf[f] = vad_s[s];
     }
+    if (pf_lane) pf[pfs][pfi] = pf_next;
+    pf_next = fetch(v + 2);
     __syncthreads();
+    RSTAMP(10);
+    if (tid < S) {
+      const bool valid = v + 1 < nfs[tid];
+      act[tid] = valid && pf[tid][kRnnPf - 1] == 0.0f;
+      if (valid && !act[tid]) a.vadf[fbase[tid] + v + 1] = 0;  // silent: X passes through, state untouched
+    }
+    __syncthreads();
+    RSTAMP(11);
   }
-  // state <- LDS
+#ifdef FVAD_STAMPS
+  if (tid == 0 && a.stamps)
+    for (int i = 0; i < 12; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+#endif
+  const int fin = maxnf & 1;  // buffer holding the latest GRU states
   for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
     const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
     if (sb + s < a.n_streams && nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] = ceps[s][i];
@@ -1064,9 +1178,9 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
     const int s = idx / 96, i = idx - s * 96;
     if (sb + s >= a.n_streams || nfs[s] <= 0) continue;
     float *stp = a.state + (size_t)(sb + s) * st::kWords;
-    if (i < 24) stp[st::kVadGru + i] = gvT[i * S + s];
-    if (i < 48) stp[st::kNoiseGru + i] = gnT[i * S + s];
-    stp[st::kDenGru + i] = gdT[i * S + s];
+    if (i < 24) stp[st::kVadGru + i] = gvT[fin][i * S + s];
+    if (i < 48) stp[st::kNoiseGru + i] = gnT[fin][i * S + s];
+    stp[st::kDenGru + i] = gdT[fin][i * S + s];
   }
   if (tid < S && sb + tid < a.n_streams && nfs[tid] > 0)
     reinterpret_cast<int *>(a.state)[(size_t)(sb + tid) * st::kWords + st::kMemId] = memid[tid];

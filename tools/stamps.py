@@ -1,5 +1,6 @@
-"""Diagnostic: per-phase cycle shares of k_frame from the FVAD_STAMPS build.
-Usage: FVAD_LIB=formula-vad_amd/lib/libfvad_stamps.so python tools/stamps.py [streams] [ticks]
+"""Diagnostic: per-phase cycle shares of k_frame (fused mode) or k_rnn
+(staged mode) from the FVAD_STAMPS build.
+Usage: FVAD_LIB=formula-vad_amd/lib/libfvad_stamps.so python tools/stamps.py [streams] [ticks] [fused|staged]
 Shares only — the stamp build's fences distort absolute time."""
 import ctypes as C
 import os
@@ -15,11 +16,15 @@ NAMES = ["load state", "pitch shift", "analysis window+scatter", "FFT A (X) + co
          "pitch filter + gains", "synthesis", "tick end + FFT B"]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+MODE = sys.argv[3] if len(sys.argv) > 3 else "fused"
+if MODE == "staged":
+    NAMES = ["features+deltas+dist row", "spectral variability", "dense", "vad z|r", "vad h", "noise z|r + vad_out",
+             "noise h", "denoise z|r", "denoise h", "denoise_output", "gains + outputs + prefetch", "next act"]
 L = fvad.lib()
 L.fvad_engine_stamps.restype = C.c_int
 L.fvad_engine_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
 m = fvad.Model(seed=1)
-e = fvad.Engine(m, B, 2, max_ticks=T)
+e = fvad.Engine(m, B, 2, max_ticks=T, mode=MODE)
 e.load_synthetic(T)
 e.run_resident(T)
 e.sync()
@@ -30,7 +35,10 @@ buf = (C.c_ulonglong * 24)()
 assert L.fvad_engine_stamps(e.h, buf, 24) == 0
 tot = sum(buf)
 frames = B * 2 * T
-print("total stamped cycles per channel-frame per WG: %.0f" % (tot / frames))
-for i, n in enumerate(NAMES):
+if MODE == "staged":
+    frames = (B // 8) * 2 * T  # k_rnn: one workgroup per 8 streams, stamps = frame steps of thread 0
+print("total stamped cycles per frame step per WG: %.0f" % (tot / frames))
+for i, n in enumerate(NAMES[:24]):
     print("%2d %-28s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[i] / tot, buf[i] / frames))
-print("   %-28s %6.2f%%" % ("store state", 100.0 * buf[23] / tot if len(buf) > 23 else 0))
+if MODE == "fused":
+    print("   %-28s %6.2f%%" % ("store state", 100.0 * buf[23] / tot if len(buf) > 23 else 0))
