@@ -38,6 +38,38 @@
 
 namespace fvad {
 
+// Diagnostic build only (-DFVAD_STAMPS): per-phase s_memtime totals of
+// thread 0 (it joins every barrier, so a phase's stamp is its critical path),
+// accumulated into a.stamps[base + id]; no other code reads them.
+#ifdef FVAD_STAMPS
+#define STAMP_INIT()                \
+  unsigned long long st_acc[16] = {}; \
+  unsigned long long st_last = __builtin_amdgcn_s_memtime()
+#define RSTAMP(id)                                                \
+  do {                                                            \
+    if (tid == 0) {                                               \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+      st_acc[id] += t_ - st_last;                                 \
+      st_last = t_;                                               \
+    }                                                             \
+  } while (0)
+#define STAMP_FLUSH(base, n)                                                  \
+  do {                                                                        \
+    if (tid == 0 && a.stamps)                                                 \
+      for (int i_ = 0; i_ < (n); i_++) atomicAdd(&a.stamps[(base) + i_], st_acc[i_]); \
+  } while (0)
+#else
+#define STAMP_INIT() \
+  do {               \
+  } while (0)
+#define RSTAMP(id) \
+  do {             \
+  } while (0)
+#define STAMP_FLUSH(base, n) \
+  do {                       \
+  } while (0)
+#endif
+
 namespace {
 constexpr int kHist = kPitchBuf - kFrame;  // 1248
 #ifndef FVAD_PITCH_FRAMES
@@ -122,8 +154,12 @@ __global__ void __launch_bounds__(256) k_prep2(StagedArgs a) {
               const float v0 = x[i];
               const float xi = a.raw_s16 ? v0 : v0 * scalar;
               const float yi = xi + mem0;
-              mem0 = (float)(mem1 + (b0 * (double)xi - a0 * (double)yi));
-              mem1 = (float)(b1 * (double)xi - a1 * (double)yi);
+              // b*x and a*y are exact in double (24-bit x 24-bit significands), so
+              // one fma rounds b*x - a*y exactly once, as the C expression does;
+              // it shortens the serial chain by one dependent f64 operation
+              const double yd = (double)yi;
+              mem0 = (float)((double)mem1 + __builtin_fma(-(double)a0, yd, b0 * (double)xi));
+              mem1 = (float)__builtin_fma(-(double)a1, yd, b1 * (double)xi);
               y[i] = yi;
             }
           }
@@ -219,6 +255,28 @@ __device__ __forceinline__ const float *frame_pb(const StagedArgs &a, int f) {
   const int s = f / a.V, v = f - s * a.V;
   return a.xs + (size_t)s * a.L + (size_t)v * kFrame;
 }
+// frame index of slot fr of group g, or -1 (same rule as group_frames)
+__device__ __forceinline__ int frame_of(const StagedArgs &a, long long g, int F, int fr) {
+  const long long f = g * F + fr;
+  if (f >= (long long)a.n_streams * a.V) return -1;
+  const int s = (int)(f / a.V), v = (int)(f - (long long)s * a.V);
+  return v < ticks_of(a, s) * a.n_channels ? (int)f : -1;
+}
+// This thread's 4 samples of the 960-sample analysis window of every frame of
+// group g (issued one group ahead so the HBM latency hides behind the work)
+template <int F>
+__device__ __forceinline__ void load_window(const StagedArgs &a, long long g, int tid, int back, float (&buf)[F][4]) {
+#pragma unroll
+  for (int fr = 0; fr < F; fr++) {
+    const int f = frame_of(a, g, F, fr);
+    const float *pb = f >= 0 ? frame_pb(a, f) + (kPitchBuf - kWin) : nullptr;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = tid + 256 * r;
+      buf[fr][r] = (pb && i < kWin) ? pb[i - back] : 0.0f;
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // k_fftA: X, Ex, Ly chain, silence, DCT(Ly)
@@ -234,26 +292,36 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
   frame_ctx_load(cx, a.plan, tid);
   bandtab_load(T, a.plan, tid, 256);
   const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
+  STAMP_INIT();
+  float win_cur[F][4];
+  if (blockIdx.x < ngroups) load_window<F>(a, blockIdx.x, tid, 0, win_cur);
   for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
     group_frames<F>(a, g, tid, fidx);
+    float win_nxt[F][4];
+    if (g + gridDim.x < ngroups) load_window<F>(a, g + gridDim.x, tid, 0, win_nxt);
     __syncthreads();
+    RSTAMP(0);
 #pragma unroll
     for (int fr = 0; fr < F; fr++) {
-      const int f = fidx[fr];
-      if (f < 0) continue;
-      const float *pb = frame_pb(a, f) + (kPitchBuf - kWin);
+      if (fidx[fr] < 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int i = tid + 256 * r;
         if (i < kWin) {
-          float val = pb[i];
+          float val = win_cur[fr][r];
           val *= cx.win[r];
           W[fr][cx.dst[r]] = make_float2(kScale960 * val, kScale960 * 0.0f);
         }
       }
     }
+#pragma unroll
+    for (int fr = 0; fr < F; fr++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) win_cur[fr][r] = win_nxt[fr][r];
     __syncthreads();
+    RSTAMP(1);
     fft960_run<F>(cx.tw, W, tid);
+    RSTAMP(2);
     for (int idx = tid; idx < F * kFreq; idx += 256) {
       const int fr = idx / kFreq, k = idx - fr * kFreq;
       if (fidx[fr] >= 0) a.X[(size_t)fidx[fr] * kFreq + k] = W[fr][k];
@@ -266,6 +334,7 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
       Ly[fr][b] = (float)log10(1e-2 + (double)ex);
     }
     __syncthreads();
+    RSTAMP(3);
     if (tid < F) {
       const int fr = tid;
       float logMax = -2, follow = -2, E = 0;
@@ -283,6 +352,7 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
       if (fidx[fr] >= 0) a.silence[fidx[fr]] = sil[fr];
     }
     __syncthreads();
+    RSTAMP(4);
     if (tid < F * kBands) {
       const int fr = tid / kBands, b = tid - fr * kBands;
       if (fidx[fr] >= 0 && !sil[fr]) {
@@ -296,7 +366,9 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
       }
     }
     __syncthreads();
+    RSTAMP(5);
   }
+  STAMP_FLUSH(16, 6);
 }
 
 // ---------------------------------------------------------------------------
@@ -803,21 +875,6 @@ constexpr int kRnnG = 4;   // lanes per column (stream groups of S/G = 2)
 constexpr int kRnnNT = 1024;
 constexpr int kRnnPf = 30; // prefetched words per stream and frame: Lyf[22], f34[7], silence
 
-// Diagnostic build only (-DFVAD_STAMPS): per-phase s_memtime totals of thread 0
-#ifdef FVAD_STAMPS
-#define RSTAMP(id)                                                \
-  do {                                                            \
-    if (tid == 0) {                                               \
-      const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-      st_acc[id] += t_ - st_last;                                 \
-      st_last = t_;                                               \
-    }                                                             \
-  } while (0)
-#else
-#define RSTAMP(id) \
-  do {             \
-  } while (0)
-#endif
 
 // acc[q] += w[j] * v[j][s0 + q] for the n terms of one segment, C order.  The
 // segment's weights start 8-byte aligned: 8 terms = one 64-bit LDS read plus
@@ -1033,10 +1090,7 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
   float pf_next = fetch(1);
   const int *ra = a.rnn_act;
   __syncthreads();
-#ifdef FVAD_STAMPS
-  unsigned long long st_acc[16] = {};
-  unsigned long long st_last = __builtin_amdgcn_s_memtime();
-#endif
+  STAMP_INIT();
   for (int v = 0; v < maxnf; v++) {
     const int cur = v & 1, nxt = cur ^ 1;
     // C: features 0..21 = DCT(Ly) (k_fftA) -> cepstral memory, deltas, the new
@@ -1157,10 +1211,7 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
     __syncthreads();
     RSTAMP(11);
   }
-#ifdef FVAD_STAMPS
-  if (tid == 0 && a.stamps)
-    for (int i = 0; i < 12; i++) atomicAdd(&a.stamps[i], st_acc[i]);
-#endif
+  STAMP_FLUSH(0, 12);
   const int fin = maxnf & 1;  // buffer holding the latest GRU states
   for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
     const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);

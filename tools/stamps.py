@@ -20,6 +20,8 @@ MODE = sys.argv[3] if len(sys.argv) > 3 else "fused"
 if MODE == "staged":
     NAMES = ["features+deltas+dist row", "spectral variability", "dense", "vad z|r", "vad h", "noise z|r + vad_out",
              "noise h", "denoise z|r", "denoise h", "denoise_output", "gains + outputs + prefetch", "next act"]
+    FFTA = ["group setup", "window scatter (global loads)", "FFT 960 x F", "X store + band sums + log10",
+            "Ly chain + silence", "DCT(Ly)"]
 L = fvad.lib()
 L.fvad_engine_stamps.restype = C.c_int
 L.fvad_engine_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
@@ -31,9 +33,9 @@ e.sync()
 assert L.fvad_engine_stamps(e.h, None, 0) == 0  # allocate + zero
 e.run_resident(T)
 e.sync()
-buf = (C.c_ulonglong * 24)()
-assert L.fvad_engine_stamps(e.h, buf, 24) == 0
-tot = sum(buf)
+buf = (C.c_ulonglong * 64)()
+assert L.fvad_engine_stamps(e.h, buf, 64) == 0
+tot = sum(buf[:24]) if MODE == "fused" else sum(buf[:12])
 frames = B * 2 * T
 if MODE == "staged":
     frames = (B // 8) * 2 * T  # k_rnn: one workgroup per 8 streams, stamps = frame steps of thread 0
@@ -42,3 +44,10 @@ for i, n in enumerate(NAMES[:24]):
     print("%2d %-28s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[i] / tot, buf[i] / frames))
 if MODE == "fused":
     print("   %-28s %6.2f%%" % ("store state", 100.0 * buf[23] / tot if len(buf) > 23 else 0))
+
+if MODE == "staged":
+    groups = B * 2 * T / 4.0
+    ft = sum(buf[16:22])
+    print("k_fftA: stamped cycles per 4-frame group per WG: %.0f" % (ft / groups * 0 + ft / max(1, groups)))
+    for i, n in enumerate(FFTA):
+        print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[16 + i] / max(1, ft), buf[16 + i] / groups))
