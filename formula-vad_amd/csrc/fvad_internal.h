@@ -97,6 +97,7 @@ struct Plan {
   int eband4[kBands];            // eband5ms[i] << 2
   float tw960[2 * kWin];         // celt twiddles (r,i)
   int bitrev960[kWin];           // celt bit-reverse table
+  int ibitrev960[kWin];          // its inverse: ibitrev960[bitrev960[i]] = i
   // FFT B (kissfft real FFT of size nfft_b)
   int nfft_b;                    // real size (2048)
   int ncfft_b;                   // nfft_b / 2

@@ -87,6 +87,7 @@ void build_plan(Plan *p, int nfft_b) {
   }
   const int celt_factors[10] = {5, 192, 3, 64, 4, 16, 4, 4, 4, 1};
   celt_digit_reverse(0, p->bitrev960, 1, celt_factors);
+  for (int i = 0; i < kWin; i++) p->ibitrev960[p->bitrev960[i]] = i;
   // kissfft real FFT B
   p->nfft_b = nfft_b;
   p->ncfft_b = nfft_b / 2;

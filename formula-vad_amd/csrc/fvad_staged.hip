@@ -225,8 +225,10 @@ constexpr int kFftFrames = 4;
 
 struct FrameCtx {
   Fft960Tw tw;
-  int dst[4];
-  float win[4];
+  int dst[4];      // scatter form: W[dst[r]] <- element tid + 256 r
+  float win[4];    //   and its window value
+  int src[4];      // gather form: W[tid + 256 r] <- element src[r]
+  float wsrc[4];   //   and its window value
 };
 __device__ __forceinline__ void frame_ctx_load(FrameCtx &c, const Plan *__restrict__ P, int tid) {
   fft960_load(c.tw, reinterpret_cast<const float2 *>(P->tw960), tid);
@@ -235,6 +237,8 @@ __device__ __forceinline__ void frame_ctx_load(FrameCtx &c, const Plan *__restri
     const int i = tid + 256 * r;
     c.dst[r] = i < kWin ? P->bitrev960[i] : 0;
     c.win[r] = i < kWin ? win960(P->half_window, i) : 0.0f;
+    c.src[r] = i < kWin ? P->ibitrev960[i] : 0;
+    c.wsrc[r] = i < kWin ? win960(P->half_window, c.src[r]) : 0.0f;
   }
 }
 
@@ -264,8 +268,10 @@ __device__ __forceinline__ int frame_of(const StagedArgs &a, long long g, int F,
 }
 // This thread's 4 samples of the 960-sample analysis window of every frame of
 // group g (issued one group ahead so the HBM latency hides behind the work)
+// (gathered in digit-reversed order: sample src[r] lands in W[tid + 256 r])
 template <int F>
-__device__ __forceinline__ void load_window(const StagedArgs &a, long long g, int tid, int back, float (&buf)[F][4]) {
+__device__ __forceinline__ void load_window(const StagedArgs &a, long long g, int tid, const FrameCtx &cx,
+                                            float (&buf)[F][4]) {
 #pragma unroll
   for (int fr = 0; fr < F; fr++) {
     const int f = frame_of(a, g, F, fr);
@@ -273,7 +279,7 @@ __device__ __forceinline__ void load_window(const StagedArgs &a, long long g, in
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int i = tid + 256 * r;
-      buf[fr][r] = (pb && i < kWin) ? pb[i - back] : 0.0f;
+      buf[fr][r] = (pb && i < kWin) ? pb[cx.src[r]] : 0.0f;
     }
   }
 }
@@ -294,11 +300,11 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
   const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
   STAMP_INIT();
   float win_cur[F][4];
-  if (blockIdx.x < ngroups) load_window<F>(a, blockIdx.x, tid, 0, win_cur);
+  if (blockIdx.x < ngroups) load_window<F>(a, blockIdx.x, tid, cx, win_cur);
   for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
     group_frames<F>(a, g, tid, fidx);
     float win_nxt[F][4];
-    if (g + gridDim.x < ngroups) load_window<F>(a, g + gridDim.x, tid, 0, win_nxt);
+    if (g + gridDim.x < ngroups) load_window<F>(a, g + gridDim.x, tid, cx, win_nxt);
     __syncthreads();
     RSTAMP(0);
 #pragma unroll
@@ -309,8 +315,8 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
         const int i = tid + 256 * r;
         if (i < kWin) {
           float val = win_cur[fr][r];
-          val *= cx.win[r];
-          W[fr][cx.dst[r]] = make_float2(kScale960 * val, kScale960 * 0.0f);
+          val *= cx.wsrc[r];
+          W[fr][i] = make_float2(kScale960 * val, kScale960 * 0.0f);
         }
       }
     }
@@ -799,9 +805,9 @@ __global__ void __launch_bounds__(256) k_pspec(StagedArgs a) {
       for (int r = 0; r < 4; r++) {
         const int i = tid + 256 * r;
         if (i < kWin) {
-          float val = pb[i];
-          val *= cx.win[r];
-          W[fr][cx.dst[r]] = make_float2(kScale960 * val, kScale960 * 0.0f);
+          float val = pb[cx.src[r]];
+          val *= cx.wsrc[r];
+          W[fr][i] = make_float2(kScale960 * val, kScale960 * 0.0f);
         }
       }
     }

@@ -51,3 +51,12 @@ if MODE == "staged":
     print("k_fftA: stamped cycles per 4-frame group per WG: %.0f" % (ft / groups * 0 + ft / max(1, groups)))
     for i, n in enumerate(FFTA):
         print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[16 + i] / max(1, ft), buf[16 + i] / groups))
+
+if MODE == "staged":
+    PIT = ["P0 x_lp", "P1 autocorr", "P2 LPC", "P3 FIR", "P4 Syy/yy chains + coarse xcorr", "P5 coarse scan",
+           "P6 fine xcorr", "P7 fine scan", "P8 remove_doubling dots"]
+    groups = B * 2 * T / 4.0
+    pt = sum(buf[32:41])
+    print("k_pitch: stamped cycles per 4-frame group per WG: %.0f" % (pt / max(1, groups)))
+    for i, n in enumerate(PIT):
+        print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[32 + i] / max(1, pt), buf[32 + i] / groups))
