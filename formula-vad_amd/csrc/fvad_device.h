@@ -291,15 +291,51 @@ __device__ __forceinline__ float interp_gain(const float *bandE, const Plan *__r
   return (1 - frac) * bandE[b] + frac * bandE[b + 1];
 }
 
+// Sequential dot product acc = ((acc + a[0]*b[0]) + a[1]*b[1]) + ... in C
+// order over LDS operands (strides sa / sb, n a multiple of 4, n >= 8), with
+// the loads of the next two 4-term blocks issued before the current block's
+// arithmetic: the serial add chain no longer waits on LDS latency per block.
+__device__ __forceinline__ float dot_seq(float acc, const float *a, int sa, const float *b, int sb, int n) {
+  float a0[4], b0[4], a1[4], b1[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    a0[u] = a[u * sa];
+    b0[u] = b[u * sb];
+    a1[u] = a[(4 + u) * sa];
+    b1[u] = b[(4 + u) * sb];
+  }
+  int i = 0;
+  for (; i + 8 < n; i += 4) {
+    float a2[4], b2[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      a2[u] = a[(i + 8 + u) * sa];
+      b2[u] = b[(i + 8 + u) * sb];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc = acc + a0[u] * b0[u];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      a0[u] = a1[u];
+      b0[u] = b1[u];
+      a1[u] = a2[u];
+      b1[u] = b2[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; u++) acc = acc + a0[u] * b0[u];
+#pragma unroll
+  for (int u = 0; u < 4; u++) acc = acc + a1[u] * b1[u];
+  return acc;
+}
+
 // find_best_pitch (pitch.c) split in two: the Syy energy recurrence depends
 // only on y, so syy_sequence() produces the value Syy holds at every lag i
 // (before its update), and best_pitch_visit() replays the selection for one
 // lag.  Visiting the lags in increasing order reproduces find_best_pitch
 // exactly; lags with xcorr <= 0 only advance Syy and may be skipped.
 __device__ void syy_sequence(const float *y, int ys, int len, int max_pitch, float *syy) {
-  float Syy = 1;
-#pragma unroll 8
-  for (int j = 0; j < len; j++) Syy = Syy + y[j * ys] * y[j * ys];
+  float Syy = dot_seq(1.0f, y, ys, y, ys, len);
 #pragma unroll 4
   for (int i = 0; i < max_pitch; i++) {
     syy[i] = Syy;
@@ -311,25 +347,18 @@ __device__ void syy_sequence(const float *y, int ys, int len, int max_pitch, flo
 
 __device__ __forceinline__ void best_pitch_visit(float xc, float Syy, int i, float &bn0, float &bn1, float &bd0,
                                                  float &bd1, int *best) {
-  if (xc > 0) {
-    float xcorr16 = xc;
-    xcorr16 *= 1e-12f;
-    const float num = xcorr16 * xcorr16;
-    if (num * bd1 > bn1 * Syy) {
-      if (num * bd0 > bn0 * Syy) {
-        bn1 = bn0;
-        bd1 = bd0;
-        best[1] = best[0];
-        bn0 = num;
-        bd0 = Syy;
-        best[0] = i;
-      } else {
-        bn1 = num;
-        bd1 = Syy;
-        best[1] = i;
-      }
-    }
-  }
+  // branch-free form of find_best_pitch's update: same comparisons, same values
+  float xcorr16 = xc;
+  xcorr16 *= 1e-12f;
+  const float num = xcorr16 * xcorr16;
+  const bool c1 = (xc > 0) && (num * bd1 > bn1 * Syy);
+  const bool c2 = c1 && (num * bd0 > bn0 * Syy);
+  bn1 = c2 ? bn0 : (c1 ? num : bn1);
+  bd1 = c2 ? bd0 : (c1 ? Syy : bd1);
+  best[1] = c2 ? best[0] : (c1 ? i : best[1]);
+  bn0 = c2 ? num : bn0;
+  bd0 = c2 ? Syy : bd0;
+  best[0] = c2 ? i : best[0];
 }
 
 __device__ __forceinline__ float pitch_gain(float xy, float xx, float yy) { return xy / sqrtf(1 + xx * yy); }

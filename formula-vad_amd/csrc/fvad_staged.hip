@@ -405,7 +405,7 @@ static_assert(rec::kSize == kPitchRecord, "pitch record size");
 template <int F>
 struct PitchGeom {
   static constexpr int kXS = 868;                    // padded x row (floats)
-  static constexpr int kR = (F * 147 + 127) / 128;   // coarse lags per lane
+  static constexpr int kR = 2 * ((F * 147 + 255) / 256);  // coarse lags per lane (pairs)
   static constexpr int kTPF = (147 + kR - 1) / kR;   // coarse lanes per frame
   static constexpr int kG3 = 59;                     // remove_doubling dots per frame
   static_assert(F * kTPF <= 128, "coarse xcorr lanes exceed waves 2-3");
@@ -459,9 +459,7 @@ __global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
       const int fr = tid / 5, k = tid - 5 * fr;
       const float *x = scr[fr];
       const int fastN = kXlp - 4;
-      float acc = 0;
-#pragma unroll 8
-      for (int i = 0; i < fastN; i++) acc = acc + x[i] * x[i + k];
+      const float acc = dot_seq(0.0f, x, 1, x + k, 1, fastN);
       float d = 0;
       for (int i = k + fastN; i < kXlp; i++) d = d + x[i] * x[i - k];
       ac[fr][k] = acc + d;
@@ -529,9 +527,7 @@ __global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
     } else if (wave == 1) {
       if (lane < F) {
         const float *x = xf[lane] + (kPitchMax >> 1);
-        float xx = 0;
-#pragma unroll 8
-        for (int i = 0; i < 480; i++) xx = xx + x[i] * x[i];
+        const float xx = dot_seq(0.0f, x, 1, x, 1, 480);
         xxs[lane] = xx;
         float yy = xx;
         float *yo = scr[lane] + oYy;
@@ -549,17 +545,23 @@ __global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
         const int k0 = blk * R;
         const float *xr = xf[fr] + (kPitchMax >> 1);
         const float *yr = xf[fr] + 2 * k0;
-        float acc[R];
+        // two lags per packed f32 multiply / add (v_pk_mul_f32, v_pk_add_f32)
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        f2v acc[R / 2];
 #pragma unroll
-        for (int m = 0; m < R; m++) acc[m] = 0;
+        for (int p = 0; p < R / 2; p++) acc[p] = f2v{0.0f, 0.0f};
+#pragma unroll 4
         for (int j = 0; j < 240; j++) {
           const float xv = xr[2 * j];
+          const f2v xb = f2v{xv, xv};
 #pragma unroll
-          for (int m = 0; m < R; m++) acc[m] = acc[m] + xv * yr[2 * (j + m)];
+          for (int p = 0; p < R / 2; p++) acc[p] = acc[p] + xb * f2v{yr[2 * (j + 2 * p)], yr[2 * (j + 2 * p + 1)]};
         }
 #pragma unroll
-        for (int m = 0; m < R; m++)
-          if (k0 + m < 147) scr[fr][oXc + k0 + m] = acc[m];
+        for (int p = 0; p < R / 2; p++) {
+          if (k0 + 2 * p < 147) scr[fr][oXc + k0 + 2 * p] = acc[p].x;
+          if (k0 + 2 * p + 1 < 147) scr[fr][oXc + k0 + 2 * p + 1] = acc[p].y;
+        }
       }
     }
     __syncthreads();
@@ -581,9 +583,7 @@ __global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
       const bool dup = t >= 5 && abs(i - 2 * bp0) <= 2;
       if (i >= 0 && i < 294 && !dup) {
         const float *xl = xf[fr] + (kPitchMax >> 1), *y = xf[fr] + i;
-        float sum = 0;
-#pragma unroll 8
-        for (int j = 0; j < 480; j++) sum = sum + xl[j] * y[j];
+        const float sum = dot_seq(0.0f, xl, 1, y, 1, 480);
         fine[fr][t] = (-1 > sum) ? -1 : sum;
       }
     }
@@ -679,9 +679,7 @@ __global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
       }
       if (lag >= 0) {
         const float *xl = xf[fr] + (kPitchMax >> 1);
-        float acc = 0;
-#pragma unroll 8
-        for (int i = 0; i < 480; i++) acc = acc + xl[i] * xl[i - lag];
+        const float acc = dot_seq(0.0f, xl, 1, xl - lag, 1, 480);
         a.rec[(g * F + fr) * rec::kSize + slot] = acc;
       }
     }
