@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--ticks", type=int, default=50)
     ap.add_argument("--mode", choices=("staged", "fused"), default="staged")
+    ap.add_argument("--no-vadm", action="store_true", help="staged: do not run the device VADMachine (k_vadm)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on this host (rank 0)")
     ap.add_argument("--cpu-streams", type=int, default=256)
     ap.add_argument("--cpu-ticks", type=int, default=200)
@@ -145,6 +146,8 @@ def main():
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     model = fvad.Model(seed=1)
     eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=args.mode)
+    if args.mode == "staged" and not args.no_vadm:
+        eng.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
     base, _ = stream_partition(rank, B)
     eng.load_synthetic(T, base=base)
 
@@ -188,7 +191,9 @@ def main():
         kernels[name] = {"ms": round(ms, 4), "tflops": round(c["flops"] * frames_launch / sec / 1e12, 3),
                          "gbs": round(c["bytes"] * frames_launch / sec / 1e9, 1),
                          "intensity": round(c["flops"] / c["bytes"], 2) if c["bytes"] else None}
-    dom = max(kt["kernels"], key=lambda n: kt["kernels"][n])
+    # k_vadm_hbm runs on the engine's side stream, overlapped with the next
+    # push: timed and listed, but not a candidate for the pipeline's bottleneck
+    dom = max((n for n in kt["kernels"] if n != "k_vadm_hbm"), key=lambda n: kt["kernels"][n])
     c = per_k[dom]
     dom_s = kt["kernels"][dom] / 1000.0
     alg_flops = c["flops"] * frames_launch
@@ -235,7 +240,8 @@ def main():
                                "(%d at %d GPU), %d ticks (480 samples/ch) per step, fp32 weights, bit-exact path"
                                % (B, Ch, B * world, world, T),
                    "streams_per_gpu": B, "channels": Ch, "ticks_per_step": T, "fft_size": 2048,
-                   "parallelism": "stream-partition x%d (no collectives)" % world, "mode": args.mode},
+                   "parallelism": "stream-partition x%d (no collectives)" % world, "mode": args.mode,
+                   "vad_machine": "device" if (args.mode == "staged" and not args.no_vadm) else "none"},
         "realtime_streams": round(value / (100.0 * Ch), 1),
         "roofline": roofline,
         "cpu_baseline": cpu,

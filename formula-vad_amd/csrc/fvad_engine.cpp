@@ -68,15 +68,35 @@ struct fvad_engine {
   int *d_sil = nullptr, *d_pitch = nullptr, *d_wtick = nullptr;
   float *d_gr = nullptr, *d_gs = nullptr;
   int8_t *d_rnn_img = nullptr;
+  // device VADMachines (fvad_engine_attach_vadm)
+  fvad::VadmArgs vadm{};
+  // k_vadm runs on a side stream over copies of one push's window outputs,
+  // overlapped with the next push (it only depends on its own state)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_copy = nullptr, ev_vadm = nullptr, ev_vt[2][2] = {};  // [slot][begin/end] timing pairs
+  int32_t *d_vflag = nullptr, *d_vticks = nullptr;
+  float *d_vwratio = nullptr, *d_vwvad = nullptr, *d_vband = nullptr;
+  bool vadm_overlap = true;
+  double vadm_ms_sum = 0;
+  int vadm_timed = 0;
+  bool vadm_pending[2] = {false, false};
+  int vadm_slot = 0;
+  std::vector<fvad::VadmState> vadm_init;  // [m][stream] initial states
+  size_t vadm_buf_len = 0;
   int rnn_act[fvad::rnnimg::kMats] = {};
   long long *d_wstart = nullptr;
   int V = 0, L = 0, wmax = 0, grid_frames = 0;
   int resident_ticks = 0;
   int n_kernels = 0;
-  hipEvent_t ev[FVAD_MAX_TIMES] = {};
+  // per-kernel timing events, two sets used alternately so the host reads
+  // push k's events while push k+1 is already queued (no launch gap)
+  hipEvent_t evs[2][FVAD_MAX_TIMES] = {};
+  hipEvent_t *ev = evs[0];
+  int ev_slot = 0;
+  bool slot_pending[2] = {false, false};
   double ms_sum[FVAD_MAX_TIMES] = {};
   int n_timed = 0;
-  bool timing_pending = false;
+  bool timing_pending = false;  // unused (kept for layout clarity)
   int raw_s16 = 0;  // rnnoise compat mode (s16-scaled I/O)
   unsigned long long *d_stamps = nullptr;  // diagnostic stamp buffer (FVAD_STAMPS builds)
 };
@@ -217,19 +237,32 @@ void free_all(fvad_engine *e) {
                   e->d_vad,  e->d_wratio,  e->d_wvad,  e->d_band, e->d_den,   e->d_wflag, e->d_ticks,
                   e->d_model, e->d_stamps, e->d_xs,    e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_vadf,  e->d_ys,    e->d_sil,
-                  e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img};
+                  e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->vadm.st, e->vadm.buf,
+                  e->vadm.seg, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
-  for (auto &ev : e->ev)
+  for (auto &set : e->evs)
+    for (auto &ev : set)
+      if (ev) (void)hipEventDestroy(ev);
+  hipEvent_t evs[] = {e->ev_copy, e->ev_vadm, e->ev_vt[0][0], e->ev_vt[0][1], e->ev_vt[1][0], e->ev_vt[1][1]};
+  for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
+  if (e->side) (void)hipStreamDestroy(e->side);
   if (e->stream) (void)hipStreamDestroy(e->stream);
 }
 
 }  // namespace
 
+int vadm_reset(fvad_engine *e);
+
 extern "C" int fvad_engine_reset(fvad_engine *e) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (e->vadm.n > 0) {
+    HIP_TRY(hipStreamSynchronize(e->side));
+    const int rc = vadm_reset(e);
+    if (rc) return rc;
+  }
   HIP_TRY(hipMemsetAsync(e->d_state, 0, sizeof(float) * fvad::st::kWords * (size_t)e->cfg.n_streams, e->stream));
   HIP_TRY(hipMemsetAsync(e->d_ring, 0,
                          sizeof(float) * (size_t)e->ring_len * e->cfg.n_channels * e->cfg.n_streams, e->stream));
@@ -275,7 +308,8 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
   for (int i = 0; i <= e->n_kernels; i++)
-    if (hipEventCreate(&e->ev[i]) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipEventCreate failed"));
+    if (hipEventCreate(&e->evs[0][i]) != hipSuccess || hipEventCreate(&e->evs[1][i]) != hipSuccess)
+      return bail(fail(FVAD_EDEVICE, "hipEventCreate failed"));
   fvad::Plan *plan = new fvad::Plan();
   fvad::build_plan(plan, c.fft_size);
   int rc = dalloc(&e->d_plan, 1);
@@ -321,6 +355,7 @@ extern "C" void fvad_engine_destroy(fvad_engine *e) {
   if (!e) return;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->side) (void)hipStreamSynchronize(e->side);
   free_all(e);
   delete e;
 }
@@ -428,31 +463,86 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.out_den = e->d_den;
   a.out_win_flag = e->d_wflag;
   a.raw_s16 = e->raw_s16;
+  a.vadm = e->vadm;
   a.stamps = e->d_stamps;
   HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr));
+  if (e->vadm.n > 0) {
+    const fvad_engine_config &c = e->cfg;
+    const size_t TB = (size_t)n_ticks * c.n_streams;
+    // the copies may be overwritten only once the previous k_vadm has read them
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm, 0));
+    HIP_TRY(hipMemcpyAsync(e->d_vflag, e->d_wflag, TB * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_vwratio, e->d_wratio, TB * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_vwvad, e->d_wvad, TB * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_vband, e->d_band, TB * c.n_channels * c.n_bands * 4, hipMemcpyDeviceToDevice,
+                           e->stream));
+    if (use_ticks)
+      HIP_TRY(hipMemcpyAsync(e->d_vticks, e->d_ticks, (size_t)c.n_streams * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipEventRecord(e->ev_copy, e->stream));
+    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_copy, 0));
+    fvad::StagedArgs v = a;
+    v.out_win_flag = e->d_vflag;
+    v.out_win_ratio = e->d_vwratio;
+    v.out_win_vad = e->d_vwvad;
+    v.out_band = e->d_vband;
+    v.ticks_valid = use_ticks ? e->d_vticks : nullptr;
+    // k_vadm timing never blocks the host (it would serialise the overlap):
+    // two event pairs alternate and are read once complete
+    const int slot = e->vadm_slot ^= 1;
+    if (timed) {
+      e->vadm_pending[slot] = false;  // an unread older sample in this slot is dropped
+      HIP_TRY(hipEventRecord(e->ev_vt[slot][0], e->side));
+    }
+    HIP_TRY(fvad::launch_vadm(v, e->vadm_overlap, e->side));
+    if (timed) {
+      HIP_TRY(hipEventRecord(e->ev_vt[slot][1], e->side));
+      e->vadm_pending[slot] = true;
+    }
+    HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
+  }
   return FVAD_OK;
 }
 
 int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   const int rc = e->cfg.mode == FVAD_MODE_FUSED ? launch_fused(e, n_ticks, use_ticks, timed)
                                                  : launch_staged(e, n_ticks, use_ticks, timed);
-  if (!rc && timed) e->timing_pending = true;
+  if (!rc && timed) e->slot_pending[e->ev_slot] = true;
   return rc;
 }
 
-int collect_timing(fvad_engine *e) {
-  if (!e->timing_pending) return FVAD_OK;
-  HIP_TRY(hipEventSynchronize(e->ev[e->n_kernels]));
+int collect_slot(fvad_engine *e, int slot) {
+  if (!e->slot_pending[slot]) return FVAD_OK;
+  hipEvent_t *ev = e->evs[slot];
+  HIP_TRY(hipEventSynchronize(ev[e->n_kernels]));
   float total = 0;
   for (int i = 0; i < e->n_kernels; i++) {
     float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
+    HIP_TRY(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
     e->ms_sum[1 + i] += ms;
     total += ms;
   }
   e->ms_sum[0] += total;
   e->n_timed++;
-  e->timing_pending = false;
+  e->slot_pending[slot] = false;
+  return FVAD_OK;
+}
+
+int collect_timing(fvad_engine *e) {
+  int rc = collect_slot(e, e->ev_slot ^ 1);
+  if (!rc) rc = collect_slot(e, e->ev_slot);
+  return rc;
+}
+
+// k_vadm samples whose end event has completed (non-blocking)
+int collect_vadm_timing(fvad_engine *e) {
+  for (int k = 0; k < 2; k++) {
+    if (!e->vadm_pending[k] || hipEventQuery(e->ev_vt[k][1]) != hipSuccess) continue;
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev_vt[k][0], e->ev_vt[k][1]));
+    e->vadm_ms_sum += ms;
+    e->vadm_timed++;
+    e->vadm_pending[k] = false;
+  }
   return FVAD_OK;
 }
 
@@ -534,7 +624,11 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   if (n_ticks < 1 || n_ticks > e->resident_ticks) return fail(FVAD_EINVAL, "n_ticks exceeds resident input");
   HIP_TRY(hipSetDevice(e->cfg.device));
-  int rc = collect_timing(e);
+  // the set this push will record into was used two pushes ago: read it (it
+  // is long finished) before reusing it; the previous push keeps running
+  e->ev_slot ^= 1;
+  e->ev = e->evs[e->ev_slot];
+  int rc = collect_slot(e, e->ev_slot);
   if (rc) return rc;
   return launch(e, n_ticks, false, true);
 }
@@ -543,6 +637,11 @@ extern "C" int fvad_engine_sync(fvad_engine *e) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->side) {
+    HIP_TRY(hipStreamSynchronize(e->side));
+    const int rc = collect_vadm_timing(e);
+    if (rc) return rc;
+  }
   return collect_timing(e);
 }
 
@@ -552,6 +651,10 @@ extern "C" int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_r
   if (rc) return rc;
   for (int i = 0; i < FVAD_MAX_TIMES; i++)
     ms_avg[i] = (e->n_timed && i <= e->n_kernels) ? e->ms_sum[i] / e->n_timed : 0.0;
+  // k_vadm (side stream, overlapped with the next push): reported after the
+  // pipeline kernels, not part of [0]
+  if (e->vadm.n > 0 && e->n_kernels + 1 < FVAD_MAX_TIMES)
+    ms_avg[e->n_kernels + 1] = e->vadm_timed ? e->vadm_ms_sum / e->vadm_timed : 0.0;
   if (n_runs) *n_runs = e->n_timed;
   return FVAD_OK;
 }
@@ -561,6 +664,8 @@ extern "C" int fvad_engine_clear_times(fvad_engine *e) {
   int rc = fvad_engine_sync(e);
   if (rc) return rc;
   for (double &v : e->ms_sum) v = 0;
+  e->vadm_ms_sum = 0;
+  e->vadm_timed = 0;
   e->n_timed = 0;
   return FVAD_OK;
 }
@@ -573,7 +678,134 @@ extern "C" int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out)
 }
 
 extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
+  if (e && i == e->n_kernels && e->vadm.n > 0) return e->vadm_overlap ? "k_vadm_hbm" : "k_vadm";
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
   if (e->cfg.mode == FVAD_MODE_FUSED) return i == 0 ? "k_prep" : "k_frame";
   return fvad::staged_kernel_name(i);
+}
+
+// ---------------------------------------------------------------------------
+// Device VADMachines (VADMachine.zig:126-230 on the GPU)
+// ---------------------------------------------------------------------------
+namespace {
+// RollingAverage(count, init) initial state (RollingAverage.zig:16-32)
+double initial_avg(size_t n, double init) {
+  double a = 0.0;
+  const double scalar = 1.0 / (double)n;
+  for (size_t i = 0; i < n; i++) a += init * scalar;
+  return a;
+}
+}  // namespace
+
+int vadm_reset(fvad_engine *e) {
+  std::vector<float> buf(e->vadm_buf_len, 0.0f);  // initial entries are K.init, tracked by lt_nw
+  HIP_TRY(hipMemcpy(e->vadm.buf, buf.data(), buf.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->vadm.st, e->vadm_init.data(), e->vadm_init.size() * sizeof(fvad::VadmState),
+                    hipMemcpyHostToDevice));
+  return FVAD_OK;
+}
+
+extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *cfgs, int n, int seg_capacity) {
+  if (!e || !cfgs || n < 1 || n > FVAD_MAX_BANDS || seg_capacity < 1) return fail(FVAD_EINVAL, "invalid argument");
+  if (e->cfg.mode != FVAD_MODE_STAGED) return fail(FVAD_EINVAL, "device VADMachines need the staged engine");
+  if (e->vadm.n > 0) return fail(FVAD_EINVAL, "VADMachines already attached");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int B = e->cfg.n_streams;
+  const float sr = (float)e->cfg.sample_rate;
+  const float eval_per_sec = sr / (float)e->cfg.fft_size;
+  auto len_of = [&](float sec) { return std::max<size_t>(1, (size_t)(eval_per_sec * sec)); };
+  auto freq_to_bin = [&](float f) { return (int)std::round(f / (sr / (float)e->cfg.fft_size)); };
+  fvad::VadmArgs v{};
+  v.n = n;
+  v.seg_cap = seg_capacity;
+  long long off = 0;
+  std::vector<fvad::VadmState> init((size_t)n * B);
+  for (int m = 0; m < n; m++) {
+    const fvad_vadm_config &c = cfgs[m];
+    fvad::VadmConst &K = v.c[m];
+    const int lo = freq_to_bin(c.speech_min_freq), hi = freq_to_bin(c.speech_max_freq);
+    K.slot = -1;
+    for (int b = 0; b < e->cfg.n_bands; b++)
+      if (e->cfg.band_lo[b] == lo && e->cfg.band_hi[b] == hi) K.slot = b;
+    if (K.slot < 0) return fail(FVAD_EINVAL, "no engine band matches the machine's speech band");
+    K.n_lt = (int)len_of(c.long_term_speech_avg_sec);
+    K.n_st = (int)len_of(c.short_term_speech_avg_sec);
+    K.n_r = (int)len_of(c.channel_vol_ratio_avg_sec);
+    K.lt_off = off;
+    off += (long long)K.n_lt * B;
+    K.st_off = off;
+    off += (long long)K.n_st * B;
+    K.r_off = off;
+    off += (long long)K.n_r * B;
+    K.min_open = (unsigned long long)(size_t)(sr * c.min_consecutive_sec_to_open);
+    K.max_gap = (unsigned long long)(size_t)(sr * c.max_speech_gap_sec);
+    K.rec_pad = (unsigned long long)(sr * 2);
+    K.thr_factor = c.speech_threshold_factor;
+    K.ratio_thr = c.channel_vol_ratio_threshold;
+    K.min_dur = c.min_vad_duration_sec;
+    K.sr = sr;
+    K.has_init = c.has_initial_long_term_avg != 0;
+    K.init = c.initial_long_term_avg;
+    fvad::VadmState s0{};
+    if (K.has_init) {
+      // RollingAverage(initial_avg): data = init (a double, VADMachine.zig:89-94)
+      s0.lt_count = (unsigned)K.n_lt;
+      s0.lt_last = initial_avg((size_t)K.n_lt, K.init);
+      s0.lt_has = 1;
+      s0.lt_pre_ok = 1;  // next write is at 0: the next pass starts from 0.0
+      s0.lt_pre = 0.0;
+    }
+    for (int s = 0; s < B; s++) init[(size_t)m * B + s] = s0;
+  }
+  int rc;
+  if ((rc = dalloc(&v.st, init.size())) || (rc = dalloc(&v.buf, (size_t)off)) ||
+      (rc = dalloc(&v.seg, (size_t)n * B * seg_capacity))) {
+    void *ptrs[] = {v.st, v.buf, v.seg};
+    for (void *p : ptrs)
+      if (p) (void)hipFree(p);
+    return rc;
+  }
+  e->vadm = v;
+  e->vadm_init = std::move(init);
+  e->vadm_buf_len = (size_t)off;
+  const size_t TB = (size_t)e->cfg.max_ticks * B;
+  if ((rc = dalloc(&e->d_vflag, TB)) || (rc = dalloc(&e->d_vwratio, TB)) || (rc = dalloc(&e->d_vwvad, TB)) ||
+      (rc = dalloc(&e->d_vband, TB * e->cfg.n_channels * e->cfg.n_bands)) || (rc = dalloc(&e->d_vticks, (size_t)B)))
+    return rc;
+  if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_copy, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_vadm, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&e->ev_vt[0][0]) != hipSuccess || hipEventCreate(&e->ev_vt[0][1]) != hipSuccess ||
+      hipEventCreate(&e->ev_vt[1][0]) != hipSuccess || hipEventCreate(&e->ev_vt[1][1]) != hipSuccess)
+    return fail(FVAD_EDEVICE, "side stream / event creation failed");
+  HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
+  const char *ov = getenv("FVAD_VADM_LDS");  // tuning: run the LDS variant in-line instead
+  e->vadm_overlap = !(ov && atoi(ov) == 1);
+  return vadm_reset(e);
+}
+
+extern "C" size_t fvad_engine_segments(fvad_engine *e, int stream, int machine, fvad_segment *out, size_t cap) {
+  if (!e || e->vadm.n == 0 || stream < 0 || stream >= e->cfg.n_streams || machine < 0 || machine >= e->vadm.n)
+    return 0;
+  if (hipSetDevice(e->cfg.device) != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->side) != hipSuccess)
+    return 0;
+  const size_t idx = (size_t)machine * e->cfg.n_streams + stream;
+  fvad::VadmState st;
+  if (hipMemcpy(&st, e->vadm.st + idx, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  const size_t n = std::min<size_t>(st.n_segs, (size_t)e->vadm.seg_cap);
+  const size_t k = std::min(n, cap);
+  if (out && k) {
+    std::vector<fvad::VadmSeg> tmp(k);
+    if (hipMemcpy(tmp.data(), e->vadm.seg + idx * e->vadm.seg_cap, k * sizeof(fvad::VadmSeg),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+      return 0;
+    for (size_t i = 0; i < k; i++) {
+      out[i].sample_from = tmp[i].sample_from;
+      out[i].sample_to = tmp[i].sample_to;
+      out[i].debug_rnn_vad = tmp[i].debug_rnn_vad;
+      out[i].debug_avg_speech_vol_ratio = tmp[i].debug_avg_speech_vol_ratio;
+    }
+  }
+  return st.n_segs;
 }

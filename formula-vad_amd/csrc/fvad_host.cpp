@@ -22,6 +22,9 @@
 
 namespace {
 
+constexpr int kPipelineSegCap = 1 << 16;  // device segment slots per machine (one stream)
+constexpr int kMultiSegCap = 1024;        // per stream and machine in the multi-stream core
+
 // ---------------- RollingAverage ----------------
 struct RollingAverage {
   std::vector<double> data;
@@ -326,7 +329,14 @@ extern "C" int fvad_pipeline_create(int sample_rate, int n_channels, const fvad_
   p->ec.max_ticks = 100;
   int rc = assign_bands(p->sm.machines, p->ec);
   if (!rc) rc = fvad_engine_create(&p->ec, model, &p->engine);
+  if (!rc) {
+    // the machines run on the device after every push (k_vadm)
+    std::vector<fvad_vadm_config> cfgs;
+    for (auto &m : p->sm.machines) cfgs.push_back(m.cfg);
+    rc = fvad_engine_attach_vadm(p->engine, cfgs.data(), (int)cfgs.size(), kPipelineSegCap);
+  }
   if (rc) {
+    if (p->engine) fvad_engine_destroy(p->engine);
     delete p;
     return rc;
   }
@@ -358,10 +368,8 @@ extern "C" int fvad_pipeline_push(fvad_pipeline *p, const float *const *pcm, siz
       for (int c = 0; c < C; c++)
         std::memcpy(&p->pcm[((size_t)t * C + c) * fvad::kFrame], &p->pending[c][consumed + (size_t)t * fvad::kFrame],
                     fvad::kFrame * sizeof(float));
-    fvad_outputs o = p->tb.outputs();
-    int rc = fvad_engine_push(p->engine, p->pcm.data(), nt, nullptr, &o);
+    int rc = fvad_engine_push(p->engine, p->pcm.data(), nt, nullptr, nullptr);
     if (rc) return rc;
-    consume(sm, p->tb, nt, 1, C, p->ec.n_bands, p->ec.fft_size, nullptr);
     consumed += (size_t)nt * fvad::kFrame;
     avail -= nt;
   }
@@ -372,9 +380,7 @@ extern "C" int fvad_pipeline_push(fvad_pipeline *p, const float *const *pcm, siz
 extern "C" size_t fvad_pipeline_segments(const fvad_pipeline *p, int alt, fvad_segment *out, size_t cap) {
   const size_t idx = alt < 0 ? 0 : (size_t)alt + 1;
   if (!p || idx >= p->sm.machines.size()) return 0;
-  const auto &segs = p->sm.machines[idx].segments;
-  for (size_t i = 0; i < segs.size() && i < cap; i++) out[i] = segs[i];
-  return segs.size();
+  return fvad_engine_segments(p->engine, 0, (int)idx, out, cap);
 }
 
 // ---------------------------------------------------------------------------
@@ -421,8 +427,10 @@ extern "C" int fvad_multi_create(int n_streams, int n_channels, const fvad_model
     std::vector<VADMachine> tmp{m->sm[p.s0].machines[0]};
     assign_bands(tmp, p.ec);
     for (int s = p.s0; s < p.s1; s++) m->sm[s].machines[0].band_slot = tmp[0].band_slot;
-    const int rc = fvad_engine_create(&p.ec, model, &p.engine);
+    int rc = fvad_engine_create(&p.ec, model, &p.engine);
+    if (!rc) rc = fvad_engine_attach_vadm(p.engine, &m->cfg, 1, kMultiSegCap);
     if (rc) {
+      if (p.engine) fvad_engine_destroy(p.engine);
       fvad_multi_destroy(m);
       return rc;
     }
@@ -451,10 +459,6 @@ extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size
       for (int s = p.s0; s < p.s1; s++) max_frames = std::max(max_frames, len[s] / fvad::kFrame);
       std::vector<float> buf((size_t)T * B * C * fvad::kFrame, 0.0f);
       std::vector<int32_t> valid(B);
-      TickBuffers tb;
-      tb.resize((size_t)T * B, C, p.ec.n_bands);
-      std::vector<StreamMachines *> sm;
-      for (int s = p.s0; s < p.s1; s++) sm.push_back(&m->sm[s]);
       for (size_t f0 = 0; f0 < max_frames; f0 += T) {
         const int nt = (int)std::min<size_t>(T, max_frames - f0);
         for (int b = 0; b < B; b++) {
@@ -466,13 +470,12 @@ extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size
               std::memcpy(&buf[(((size_t)t * B + b) * C + c) * fvad::kFrame],
                           pcm[s] + (size_t)c * len[s] + (f0 + t) * fvad::kFrame, fvad::kFrame * sizeof(float));
         }
-        fvad_outputs o = tb.outputs();
-        const int rc = fvad_engine_push(p.engine, buf.data(), nt, valid.data(), &o);
+        // VADMachines run on the device (k_vadm); no per-tick outputs come back
+        const int rc = fvad_engine_push(p.engine, buf.data(), nt, valid.data(), nullptr);
         if (rc) {
           rcs[pi] = rc;
           return;
         }
-        consume(sm, tb, nt, B, C, p.ec.n_bands, p.ec.fft_size, valid.data());
       }
     });
   }
@@ -484,9 +487,9 @@ extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size
 
 extern "C" size_t fvad_multi_segments(const fvad_multi *m, int stream, fvad_segment *out, size_t cap) {
   if (!m || stream < 0 || stream >= m->n_streams) return 0;
-  const auto &segs = m->sm[stream].machines[0].segments;
-  for (size_t i = 0; i < segs.size() && i < cap; i++) out[i] = segs[i];
-  return segs.size();
+  for (const auto &p : m->parts)
+    if (stream >= p.s0 && stream < p.s1) return fvad_engine_segments(p.engine, stream - p.s0, 0, out, cap);
+  return 0;
 }
 
 // ---------------------------------------------------------------------------

@@ -12,6 +12,36 @@ namespace fvad {
 constexpr int kStagedKernels = 10;
 constexpr int kPitchRecord = 144;  // floats per frame of k_pitch output
 
+// Device VADMachine (VADMachine.zig:126-230), one lane per stream.
+struct VadmConst {
+  int n_lt, n_st, n_r, slot;           // RollingAverage lengths, engine band slot
+  long long lt_off, st_off, r_off;     // buffer offsets (doubles), layout [i][stream]
+  unsigned long long min_open, max_gap, rec_pad;
+  float thr_factor, ratio_thr, min_dur, sr;
+  int has_init;
+  double init;
+};
+struct VadmState {
+  unsigned long long speech_start, speech_end, windows_done;
+  double lt_last, st_last, r_last, lt_pre;  // lt_pre: cached prefix (see ra_push_long)
+  unsigned lt_widx, lt_count, st_widx, st_count, r_widx, r_count, lt_nw, pad1;  // lt_nw: entries pushed
+  int lt_has, st_has, r_has, state, lt_pre_ok, pad0;
+  float rnn_vad, vol_ratio;
+  unsigned rnn_vad_count, vol_ratio_count, n_segs, pad;
+};
+struct VadmSeg {
+  unsigned long long sample_from, sample_to;
+  float debug_rnn_vad, debug_avg_speech_vol_ratio;
+};
+struct VadmArgs {
+  int n;  // machines (0: k_vadm not launched)
+  VadmConst c[kMaxBandCfg];
+  VadmState *st;  // [m][stream]
+  float *buf;     // rolling-average data (f32: each entry is a pushed f32)
+  VadmSeg *seg;   // [m][stream][seg_cap]
+  int seg_cap;
+};
+
 struct StagedArgs {
   int n_streams, n_channels, n_ticks;
   int V;                   // frame-row stride per stream (= max_ticks * C)
@@ -47,6 +77,7 @@ struct StagedArgs {
   float *out_vad, *out_win_ratio, *out_win_vad, *out_band, *out_den;
   int *out_win_flag;
   int raw_s16;
+  VadmArgs vadm;
   unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn
 };
 
@@ -54,5 +85,8 @@ struct StagedArgs {
 // recorded around them (per-kernel timing).
 hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev);
 const char *staged_kernel_name(int i);
+// Device VADMachines over the window outputs a.out_* of one push: overlap =
+// the light HBM variant meant to co-run with the next push on a side stream.
+hipError_t launch_vadm(const StagedArgs &a, bool overlap, hipStream_t stream);
 
 }  // namespace fvad

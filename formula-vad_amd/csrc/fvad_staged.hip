@@ -1511,6 +1511,233 @@ __global__ void __launch_bounds__(NT) k_fftb(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_vadm: VADMachine.run (VADMachine.zig:126-230) for every completed FFT-B
+// window of the push, one lane per stream, every attached machine.
+// RollingAverage.avg (RollingAverage.zig:34-56) recomputes the mean over the
+// whole buffer in array order on every push, in f64 - reproduced as is (an
+// incremental mean would round differently).  Buffers are stored [i][stream]
+// so the lanes of a wave read one contiguous line per term.
+// ---------------------------------------------------------------------------
+// Short rolling averages: the plain recompute.
+__device__ __forceinline__ double ra_push(float *buf, int B, int n, unsigned &widx, unsigned &count, double &last,
+                                          int &has, float sample) {
+  buf[(size_t)widx * B] = sample;  // stored as f32: (double)f32 is exact
+  widx = (widx + 1) % (unsigned)n;
+  if (count < (unsigned)n) count++;
+  double acc = 0.0;
+  const double scalar = 1.0 / (double)count;
+  for (unsigned i = 0; i < count; i++) acc += (double)buf[(size_t)i * B] * scalar;
+  last = acc;
+  has = 1;
+  return acc;
+}
+
+// The long-term average (4218 entries by default).  Same operation sequence as
+// the full recompute, two savings that keep it bit-identical:
+//  * once the buffer is full the scalar 1/n no longer changes, so the running
+//    sum over the entries before the write position is exactly what the
+//    previous pass had accumulated there (those entries have not changed) -
+//    the pass starts from that cached prefix;
+//  * entries are read 32 ahead of the f64 add chain (register double buffer),
+//    so the chain does not wait on memory per term.
+// acc += entry[i] * scalar for i in [i0, i1), C order; entries are pushed f32
+// values (read 8 ahead of the add chain) or, for never-written entries, the
+// initial average (a double).
+__device__ __forceinline__ double lt_sum(double acc, const float *buf, size_t bs, unsigned i0, unsigned i1,
+                                         double scalar) {
+  unsigned i = i0;
+  for (; i + 8 <= i1; i += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = buf[(size_t)(i + u) * bs];
+    double p[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) p[u] = (double)v[u] * scalar;
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += p[u];
+  }
+  for (; i < i1; i++) acc += (double)buf[(size_t)i * bs] * scalar;
+  return acc;
+}
+__device__ __forceinline__ double lt_sum_init(double acc, double term, unsigned n) {
+  for (unsigned i = 0; i < n; i++) acc += term;
+  return acc;
+}
+__device__ __forceinline__ double lt_range(double acc, const float *buf, size_t bs, unsigned p, unsigned q,
+                                           unsigned nw, double init, double scalar) {
+  const unsigned mid = min(max(nw, p), q);  // [p, mid) written, [mid, q) initial
+  acc = lt_sum(acc, buf, bs, p, mid, scalar);
+  return lt_sum_init(acc, init * scalar, q - mid);
+}
+
+// The long-term average (4218 entries by default).  Same operation sequence as
+// the full recompute, with one exact saving: once the buffer is full the
+// scalar 1/n no longer changes, so the running sum over the entries before the
+// write position is exactly what the previous pass had accumulated there
+// (those entries have not changed) - the pass starts from that cached prefix.
+// Entries never written since the machine started hold the initial average
+// (a double, RollingAverage.zig init): entry i is a pushed f32 iff i < nw.
+__device__ __forceinline__ double ra_push_long(float *buf, size_t bs, int n, unsigned &widx, unsigned &count,
+                                               unsigned &nw, double init, double &last, int &has, double &pre,
+                                               int &pre_ok, float sample) {
+  const unsigned w = widx;
+  buf[(size_t)w * bs] = sample;
+  widx = (w + 1) % (unsigned)n;
+  if (count < (unsigned)n) count++;
+  if (nw < (unsigned)n) nw++;
+  const double scalar = 1.0 / (double)count;
+  const unsigned start = pre_ok ? w : 0u;
+  double acc = pre_ok ? pre : 0.0;
+  const unsigned save_at = widx;  // the next pass starts at the next write position
+  double save = 0.0;              // (save_at == 0: it starts from 0.0)
+  if (save_at > start && save_at < count) {
+    acc = lt_range(acc, buf, bs, start, save_at, nw, init, scalar);
+    save = acc;
+    acc = lt_range(acc, buf, bs, save_at, count, nw, init, scalar);
+  } else {
+    if (save_at == start) save = acc;
+    acc = lt_range(acc, buf, bs, start, count, nw, init, scalar);
+  }
+  pre = save;
+  pre_ok = count == (unsigned)n;
+  last = acc;
+  has = 1;
+  return acc;
+}
+
+constexpr int kVadmS = 8;        // streams per workgroup
+constexpr int kVadmLds = 4225;   // LDS-resident long-term buffer length (odd: no bank conflicts)
+
+// One machine over all completed windows of the push for one stream; `lt`
+// points at entry 0 of the stream's long-term buffer, `lts` is its stride.
+__device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t lts) {
+  const int B = a.n_streams, C = a.n_channels, nb = a.n_bands;
+  const int nt = ticks_of(a, s);
+  const unsigned long long fft = (unsigned long long)a.plan->nfft_b;
+  enum { kClosed = 0, kOpening = 1, kOpen = 2, kClosing = 3 };
+  const VadmConst &K = a.vadm.c[m];
+  VadmState S = a.vadm.st[(size_t)m * B + s];
+  float *st = a.vadm.buf + K.st_off + s, *rb = a.vadm.buf + K.r_off + s;
+  VadmSeg *seg = a.vadm.seg + ((size_t)m * B + s) * a.vadm.seg_cap;
+  for (int t = 0; t < nt; t++) {
+    const size_t o = (size_t)t * B + s;
+    if (!a.out_win_flag[o]) continue;
+    const unsigned long long index = S.windows_done * fft;
+    S.windows_done++;
+    float min_v = 999, max_v = 0;
+    for (int c = 0; c < C; c++) {
+      const float v = a.out_band[(o * C + c) * nb + K.slot];
+      if (v < min_v) min_v = v;
+      if (v > max_v) max_v = v;
+    }
+    const float vad = a.out_win_vad[o], vr = a.out_win_ratio[o];
+    const double st_avg = ra_push(st, B, K.n_st, S.st_widx, S.st_count, S.st_last, S.st_has, min_v);
+    const double r_avg = ra_push(rb, B, K.n_r, S.r_widx, S.r_count, S.r_last, S.r_has, vr);
+    double base;
+    if (S.lt_has)
+      base = S.lt_last;
+    else if (K.has_init)
+      base = K.init;
+    else
+      base = st_avg;
+    const double threshold = base * (double)K.thr_factor;
+    const bool met = st_avg > threshold && r_avg > (double)K.ratio_thr;
+    if (!met)
+      ra_push_long(lt, lts, K.n_lt, S.lt_widx, S.lt_count, S.lt_nw, K.init, S.lt_last, S.lt_has, S.lt_pre,
+                   S.lt_pre_ok, min_v);
+    const int from = S.state;
+    bool ended = false;
+    switch (from) {
+      case kClosed:
+        if (met) {
+          S.state = kOpening;
+          S.speech_start = index;
+        }
+        break;
+      case kOpening:
+        if (met && index - S.speech_start >= K.min_open)
+          S.state = kOpen;
+        else if (!met)
+          S.state = kClosed;
+        break;
+      case kOpen:
+        if (!met) {
+          S.state = kClosing;
+          S.speech_end = index;
+        }
+        break;
+      default:  // kClosing
+        if (met) {
+          S.state = kOpen;
+        } else if (index - S.speech_end >= K.max_gap) {
+          S.state = kClosed;
+          ended = true;
+        }
+        break;
+    }
+    if (ended) {  // onSpeechEnd (before the tracking update of this window, as in VADMachine.zig)
+      const unsigned long long len = S.speech_end - S.speech_start;
+      const float len_rt = (float)len / K.sr;
+      if (len_rt >= K.min_dur) {
+        if (S.n_segs < (unsigned)a.vadm.seg_cap) {
+          VadmSeg g;
+          g.sample_from = K.rec_pad > S.speech_start ? 0ull : S.speech_start - K.rec_pad;
+          g.sample_to = S.speech_end + K.rec_pad;
+          g.debug_rnn_vad = S.rnn_vad / (float)S.rnn_vad_count;
+          g.debug_avg_speech_vol_ratio = S.vol_ratio / (float)S.vol_ratio_count;
+          seg[S.n_segs] = g;
+        }
+        S.n_segs++;
+      }
+    }
+    // track(vad, vr, from, to)
+    if (from == kClosed && S.state == kOpening) {
+      S.rnn_vad = vad;
+      S.rnn_vad_count = 1;
+      S.vol_ratio = vr;
+      S.vol_ratio_count = 1;
+    } else if (from == kOpening || from == kOpen) {
+      S.rnn_vad += vad;
+      S.rnn_vad_count += 1;
+      S.vol_ratio += vr;
+      S.vol_ratio_count += 1;
+    }
+  }
+  a.vadm.st[(size_t)m * B + s] = S;
+}
+
+// One 64-thread workgroup per 8 streams.  Default-length long-term buffers
+// (4218 entries) of the 8 streams live in LDS for the whole push: loaded once
+// with all lanes, walked by the 8 stream lanes window after window, stored
+// back once.  Longer configurations walk them in HBM.  (The engine normally
+// runs k_vadm_hbm instead, on a side stream overlapped with the next push.)
+__global__ void __launch_bounds__(64) k_vadm(StagedArgs a) {
+  __shared__ float ltl[kVadmS][kVadmLds];
+  const int tid = threadIdx.x, sb = blockIdx.x * kVadmS;
+  const int B = a.n_streams, ns = min(kVadmS, B - sb);
+  if (ns <= 0) return;
+  for (int m = 0; m < a.vadm.n; m++) {
+    const VadmConst &K = a.vadm.c[m];
+    if (K.n_lt <= kVadmLds) {
+      for (int idx = tid; idx < ns * K.n_lt; idx += 64) {
+        const int i = idx / ns, j = idx - i * ns;
+        ltl[j][i] = a.vadm.buf[K.lt_off + (size_t)i * B + sb + j];
+      }
+      __syncthreads();
+      if (tid < ns && ticks_of(a, sb + tid) > 0) vadm_stream(a, m, sb + tid, ltl[tid], 1);
+      __syncthreads();
+      for (int idx = tid; idx < ns * K.n_lt; idx += 64) {
+        const int i = idx / ns, j = idx - i * ns;
+        a.vadm.buf[K.lt_off + (size_t)i * B + sb + j] = ltl[j][i];
+      }
+      __syncthreads();
+    } else if (tid < ns && ticks_of(a, sb + tid) > 0) {
+      vadm_stream(a, m, sb + tid, a.vadm.buf + K.lt_off + sb + tid, (size_t)B);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launcher
 // ---------------------------------------------------------------------------
 const char *staged_kernel_name(int i) {
@@ -1585,6 +1812,25 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   rec(9);
   hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
   rec(10);
+  return hipGetLastError();
+}
+
+// k_vadm_hbm: the same machine, long-term buffers walked in HBM, no LDS, 16
+// lanes per workgroup: a light kernel that co-runs with the next push's
+// pipeline on the engine's side stream.
+__global__ void __launch_bounds__(64) k_vadm_hbm(StagedArgs a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.n_streams || ticks_of(a, s) <= 0) return;
+  for (int m = 0; m < a.vadm.n; m++)
+    vadm_stream(a, m, s, a.vadm.buf + a.vadm.c[m].lt_off + s, (size_t)a.n_streams);
+}
+
+hipError_t launch_vadm(const StagedArgs &a, bool overlap, hipStream_t stream) {
+  (void)hipGetLastError();
+  if (overlap)
+    hipLaunchKernelGGL(k_vadm_hbm, dim3((a.n_streams + 15) / 16), dim3(16), 0, stream, a);
+  else
+    hipLaunchKernelGGL(k_vadm, dim3((a.n_streams + kVadmS - 1) / kVadmS), dim3(64), 0, stream, a);
   return hipGetLastError();
 }
 

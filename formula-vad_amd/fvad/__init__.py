@@ -122,6 +122,8 @@ SYMBOLS = [
     ("fvad_engine_sync", C.c_int, [C.c_void_p]),
     ("fvad_engine_kernel_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("fvad_engine_kernel_name", C.c_char_p, [C.c_void_p, C.c_int]),
+    ("fvad_engine_attach_vadm", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+    ("fvad_engine_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
     ("fvad_engine_clear_times", C.c_int, [C.c_void_p]),
     ("fvad_engine_fetch", C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     ("fvad_vadm_config_default", None, [C.c_void_p]),
@@ -282,6 +284,19 @@ class Engine:
 
     def clear_times(self):
         _check(lib().fvad_engine_clear_times(self.h), "fvad_engine_clear_times")
+
+    def attach_vadm(self, cfgs=None, seg_capacity=256):
+        """Run VADMachines on the device after every push (default config if None)."""
+        cfgs = list(cfgs) if cfgs else [VadmConfig.default()]
+        arr = (VadmConfig * len(cfgs))(*cfgs)
+        self._vadm_keep = arr
+        _check(lib().fvad_engine_attach_vadm(self.h, arr, len(cfgs), seg_capacity), "fvad_engine_attach_vadm")
+
+    def segments(self, stream, machine=0):
+        n = lib().fvad_engine_segments(self.h, stream, machine, None, 0)
+        buf = (Segment * max(1, n))()
+        lib().fvad_engine_segments(self.h, stream, machine, buf, n)
+        return [(s.sample_from, s.sample_to, s.debug_rnn_vad, s.debug_avg_speech_vol_ratio) for s in buf[:n]]
 
     def fetch(self, n_ticks, denoised=False):
         o, s = self._alloc_out(n_ticks, denoised)

@@ -62,7 +62,15 @@ def phases(n_channels=2, fft_size=2048):
     p["pitch filter + gains"] = 22 * 20 + 481 * 7 + _band_sum() + 22 * 6 + 481 * (2 * 3 + 4)
     p["synthesis (scale, FFT A, window, OLA, 1/32767)"] = 1920 + _fft960() + 960 + 960 + 480 + 480
     p["re-block + FFT B share"] = _fftb_per_window(fft_size) * FRAME / fft_size + 4
+    p["VADMachine share"] = _vadm_per_window() * FRAME / fft_size / n_channels
     return p
+
+
+def _vadm_per_window(n_lt=4218, n_st=4, n_r=11):
+    """VADMachine.run per window and stream: the three RollingAverage means are
+    recomputed over their whole buffers (mul + add per entry, f64); the
+    long-term one only outside speech (counted as always, the upper bound)."""
+    return 2 * (n_lt + n_st + n_r) + 24
 
 
 def flops_per_channel_frame(n_channels=2, fft_size=2048):
@@ -116,7 +124,9 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_ola": (960, 960 * 4 + 480 * 4 + 4.0 / C),
         "k_winmeta": (0.0, 4 * 4.0 / C),
         "k_fftb": (p["re-block + FFT B share"], 480 * 4 + 4),
+        "k_vadm": (p["VADMachine share"], (4218 + 4 + 11 + 2) * 4 * FRAME / fft_size / C + 16),
     }
+    k["k_vadm_hbm"] = k["k_vadm"]
     return {n: {"flops": f, "bytes": b} for n, (f, b) in k.items()}
 
 

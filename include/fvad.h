@@ -195,6 +195,15 @@ void fvad_vadm_bins(const fvad_vadm *v, int *lo, int *hi);
 int fvad_vadm_run(fvad_vadm *v, uint64_t index, const float *band_per_channel, float vad, float vol_ratio);
 size_t fvad_vadm_segments(const fvad_vadm *v, fvad_segment *out, size_t cap);
 
+/* Device VADMachines (VADMachine.zig:126-230 run on the GPU, one lane per
+ * stream, after FFT B of every push).  Staged engines only.
+ * Each config's speech band (FFT.freqToBin of speech_min/max_freq) must be one
+ * of the engine's bands.  Up to FVAD_MAX_BANDS machines; segments accumulate
+ * on the device, seg_capacity per (stream, machine); a reset clears them. */
+int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *cfgs, int n, int seg_capacity);
+/* total segments of (stream, machine) so far; copies min(total, capacity, cap) */
+size_t fvad_engine_segments(fvad_engine *e, int stream, int machine, fvad_segment *out, size_t cap);
+
 /* AudioPipeline (AudioPipeline.zig:20-26,39-120) for one stream, backed by a
  * 1-stream engine.  n_alt alternative VADMachine configs (VAD.zig:20-23). */
 typedef struct fvad_pipeline fvad_pipeline;

@@ -1,0 +1,56 @@
+"""Device VADMachine (k_vadm, VADMachine.zig:126-230 on the GPU) against the
+host restatement (fvad_vadm_*, itself checked against the oracle in
+test_host_cpu.py) fed the same engine outputs: segments and their debug
+averages must be identical, for the default and an alternative config, over
+ragged pushes of several streams."""
+import numpy as np
+import pytest
+
+import parity_util as pu
+
+pytestmark = pytest.mark.gpu
+
+
+def host_segments(fvad_mod, outs, cfg, C, slot, stream):
+    vm = fvad_mod.VADMachine(cfg, n_channels=C)
+    wd = 0
+    for o, valid in outs:
+        for t in range(valid[stream]):
+            if not o["win_flag"][t, stream]:
+                continue
+            vm.run(wd * 2048, o["band"][t, stream, :, slot], float(o["win_vad"][t, stream]),
+                   float(o["win_ratio"][t, stream]))
+            wd += 1
+    return vm.segments()
+
+
+def test_device_vadm_matches_host(fvad_mod):
+    m = fvad_mod.Model(seed=1)
+    alt = fvad_mod.VadmConfig.default()
+    alt.speech_min_freq, alt.speech_max_freq = 300.0, 3000.0
+    alt.min_vad_duration_sec = 0.3
+    ids, secs = [0, 4, 19, 42, 7], [70.0, 55.5, 40.0, 66.0, 12.0]
+    streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip(ids, secs)]
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=64, bands=((4, 64), (13, 128)))
+    eng.attach_vadm([fvad_mod.VadmConfig.default(), alt])
+    B, C = len(streams), 2
+    lens = [x.shape[1] // 480 for x in streams]
+    outs = []
+    for t0 in range(0, max(lens), 64):
+        nt = min(64, max(lens) - t0)
+        pcm = np.zeros((nt, B, C, 480), np.float32)
+        valid = np.zeros(B, np.int32)
+        for s, x in enumerate(streams):
+            v = max(0, min(nt, lens[s] - t0))
+            valid[s] = v
+            if v:
+                pcm[:v, s] = x[:, t0 * 480:(t0 + v) * 480].reshape(C, v, 480).transpose(1, 0, 2)
+        outs.append((eng.push(pcm, ticks_valid=valid), valid))
+    total = 0
+    for s in range(B):
+        for mi, (cfg, slot) in enumerate(((fvad_mod.VadmConfig.default(), 0), (alt, 1))):
+            ref = host_segments(fvad_mod, outs, cfg, C, slot, s)
+            got = eng.segments(s, mi)
+            assert got == ref, (s, mi, got[:3], ref[:3])
+            total += len(ref)
+    assert total > 0
