@@ -64,7 +64,7 @@ struct fvad_engine {
   int *d_wflag = nullptr, *d_ticks = nullptr;
   // staged-mode intermediates
   float *d_xs = nullptr, *d_X = nullptr, *d_P = nullptr, *d_Ex = nullptr, *d_Ep = nullptr, *d_Exp = nullptr,
-        *d_Lyf = nullptr, *d_f34 = nullptr, *d_rec = nullptr, *d_vadf = nullptr, *d_ys = nullptr;
+        *d_Lyf = nullptr, *d_f34 = nullptr, *d_rec = nullptr, *d_ptile = nullptr, *d_vadf = nullptr, *d_ys = nullptr;
   int *d_sil = nullptr, *d_pitch = nullptr, *d_wtick = nullptr;
   float *d_gr = nullptr, *d_gs = nullptr;
   int8_t *d_rnn_img = nullptr;
@@ -236,7 +236,7 @@ void free_all(fvad_engine *e) {
   void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm,   e->d_xbuf, e->d_ratio,
                   e->d_vad,  e->d_wratio,  e->d_wvad,  e->d_band, e->d_den,   e->d_wflag, e->d_ticks,
                   e->d_model, e->d_stamps, e->d_xs,    e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
-                  e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_vadf,  e->d_ys,    e->d_sil,
+                  e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->vadm.st, e->vadm.buf,
                   e->vadm.seg, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband};
   for (void *p : ptrs)
@@ -337,7 +337,9 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
         (rc = dalloc(&e->d_P, F * fvad::kFreq * 2)) || (rc = dalloc(&e->d_Ex, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Ep, F * fvad::kBands)) || (rc = dalloc(&e->d_Exp, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Lyf, F * fvad::kBands)) || (rc = dalloc(&e->d_f34, F * 8)) ||
-        (rc = dalloc(&e->d_rec, F * fvad::kPitchRecord)) || (rc = dalloc(&e->d_vadf, F)) ||
+        (rc = dalloc(&e->d_rec, F * fvad::kPitchRecord)) ||
+        (rc = dalloc(&e->d_ptile, (B + fvad::ptile::kTile - 1) / fvad::ptile::kTile * e->V * fvad::ptile::kTile *
+                                      fvad::ptile::kRows)) || (rc = dalloc(&e->d_vadf, F)) ||
         (rc = dalloc(&e->d_ys, F * fvad::kWin)) || (rc = dalloc(&e->d_sil, F)) || (rc = dalloc(&e->d_pitch, F)) ||
         (rc = dalloc(&e->d_wtick, B * e->wmax)) || (rc = dalloc(&e->d_wstart, B * e->wmax)) ||
         (rc = dalloc(&e->d_gr, F * fvad::kBands)) || (rc = dalloc(&e->d_gs, F * fvad::kBands)))
@@ -440,6 +442,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.f34 = e->d_f34;
   a.silence = e->d_sil;
   a.rec = e->d_rec;
+  a.ptile = e->d_ptile;
   a.pitch = e->d_pitch;
   a.vadf = e->d_vadf;
   a.gr = e->d_gr;

@@ -9,8 +9,21 @@
 
 namespace fvad {
 
-constexpr int kStagedKernels = 10;
-constexpr int kPitchRecord = 144;  // floats per frame of k_pitch output
+constexpr int kStagedKernels = 11;
+constexpr int kPitchRecord = 144;  // floats per frame of the pitch record (k_pcorr -> k_select)
+
+// Pitch tile buffer (k_plpc -> k_pcorr): a tile is 64 streams at one frame
+// position; each quarter (16 streams) is one contiguous block of kRows rows of
+// 16 floats.
+namespace ptile {
+constexpr int kTile = 64, kQuarter = 16;
+constexpr int kXf = 0;              // xf[0..863]: x_lp after celt_fir5
+constexpr int kSc = 864;            // Syy before step i of the coarse find_best_pitch, i < 147
+constexpr int kSf = kSc + 147;      // Syy of the fine find_best_pitch, i < 294
+constexpr int kYy = kSf + 294;      // yy_lookup[0..384] (remove_doubling)
+constexpr int kXx = kYy + 385;      // xx
+constexpr int kRows = kXx + 1;
+}  // namespace ptile
 
 // Device VADMachine (VADMachine.zig:126-230), one lane per stream.
 struct VadmConst {
@@ -58,6 +71,7 @@ struct StagedArgs {
   float *f34;              // [f][8] features 34..40
   int *silence;            // [f]
   float *rec;              // [f][kPitchRecord]
+  float *ptile;            // [tile][quarter][ptile::kRows][16]
   int *pitch;              // [f] selected pitch index
   float *vadf;             // [f] per-frame vad probability
   float *gr, *gs;          // [f][22] GRU gains g and smoothed gains max(g, .6*lastg)
@@ -81,7 +95,7 @@ struct StagedArgs {
   unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn
 };
 
-// Launch the 10 kernels on `stream`; when ev != nullptr, ev[0..10] are
+// Launch the 11 kernels on `stream`; when ev != nullptr, ev[0..11] are
 // recorded around them (per-kernel timing).
 hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev);
 const char *staged_kernel_name(int i);

@@ -8,10 +8,11 @@
 //                           of pitch history in front of the launch's frames
 //   k_fftA    wg/frame      analysis window + FFT A, band energies Ex, the
 //                           log/floor chain (Ly, E, silence gate), DCT(Ly)
-//   k_pitch   wg/frame      pitch_downsample (autocorr, LPC, FIR5), coarse and
-//                           fine xcorr + find_best_pitch, every remove_doubling
-//                           inner product for every candidate period (the
-//                           final 3-lag xcorr speculatively for all 15)
+//   k_plpc    lane/frame    pitch_downsample (x_lp, autocorr, LPC, FIR5) and
+//                           every serial energy recurrence (Syy, xx, yy)
+//   k_pcorr   wg/16 frames  coarse and fine xcorr + find_best_pitch, every
+//                           remove_doubling inner product for every candidate
+//                           period (the final 3-lag xcorr speculatively for all 15)
 //   k_select  lane/stream   remove_doubling's sequential candidate selection
 //                           (needs last_period / last_gain) -> pitch index
 //   k_pspec   wg/frame      pitch window + FFT A -> P, Ep, Exp, DCT(Exp)
@@ -72,10 +73,6 @@ namespace fvad {
 
 namespace {
 constexpr int kHist = kPitchBuf - kFrame;  // 1248
-#ifndef FVAD_PITCH_FRAMES
-#define FVAD_PITCH_FRAMES 4
-#endif
-constexpr int kPitchFrames = FVAD_PITCH_FRAMES;  // frames per k_pitch workgroup
 constexpr float kScale960 = 1.f / 960;
 
 __device__ __forceinline__ int ticks_of(const StagedArgs &a, int s) {
@@ -378,21 +375,20 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_pitch: everything of pitch_search / remove_doubling that does not depend
-// on the previous frame, for F frames per workgroup.  Every C-order sum stays
-// on one lane; lanes are assigned (frame, task) pairs so the serial chains of
-// F different frames (autocorr lags, Syy / yy recurrences, find_best_pitch
-// scans) share wave instructions instead of running on 1-5 lanes each.
-//   P0 x_lp (pitch_downsample)        all lanes
-//   P1 _celt_autocorr, 5 lags x F     wave 0
-//   P2 LPC + lag window + FIR coeffs  F lanes
-//   P3 5-tap FIR in place             all lanes (via registers)
-//   P4 wave 0: coarse / fine Syy sequences; wave 1: xx + yy_lookup chain;
-//      waves 2-3: coarse xcorr, R consecutive lags per lane
-//   P5 coarse find_best_pitch scan    F lanes
-//   P6 fine xcorr at the <= 10 candidate lags
-//   P7 fine scan -> T0, candidate periods and energies
-//   P8 remove_doubling inner products + speculative final xcorr (T-1, T+1)
+// Pitch analysis (pitch.c: pitch_downsample, pitch_search, remove_doubling up
+// to its sequential selection), split by how each part parallelises:
+//
+//   k_plpc   lane per frame.  Every serial chain that depends only on the
+//            frame itself: x_lp, the 5 autocorr sums (860 terms each), LPC,
+//            the 5-tap FIR, the Syy recurrences of both find_best_pitch calls,
+//            xx and the yy_lookup recurrence.  A wave owns a tile of 64
+//            streams at one frame position (lane = stream), so all 64 lanes
+//            walk a chain.  Writes xf and the sequences to the tile buffer.
+//   k_pcorr  16 frames per workgroup, xf resident in LDS.  The inner products
+//            (coarse xcorr: 147 lags x 240, fine xcorr at <= 10 lags, the 59
+//            remove_doubling products), both find_best_pitch scans (lane per
+//            frame) and the pitch record for k_select.
+// Every C-order sum stays on one lane in its original order.
 // ---------------------------------------------------------------------------
 namespace rec {
 constexpr int kT0 = 0, kXx = 1, kXy = 2, kYyT0 = 3, kNValid = 4;
@@ -402,201 +398,462 @@ constexpr int kSize = 144;  // (the xcorr at T itself is kXy / s1)
 }  // namespace rec
 static_assert(rec::kSize == kPitchRecord, "pitch record size");
 
-template <int F>
-struct PitchGeom {
-  static constexpr int kXS = 868;                    // padded x row (floats)
-  static constexpr int kR = 2 * ((F * 147 + 255) / 256);  // coarse lags per lane (pairs)
-  static constexpr int kTPF = (147 + kR - 1) / kR;   // coarse lanes per frame
-  static constexpr int kG3 = 59;                     // remove_doubling dots per frame
-  static_assert(F * kTPF <= 128, "coarse xcorr lanes exceed waves 2-3");
-  static_assert(5 * F <= 64 && 2 * F <= 64, "serial lanes exceed one wave");
-};
-
 __device__ __forceinline__ int rd_T1(int T0, int k) { return (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k)); }
 __device__ __forceinline__ int rd_T1b(int T0, int T1, int k) {
   if (k == 2) return (T1 + T0 > 384) ? T0 : T0 + T1;
   return (int)((unsigned)(2 * second_check(k) * T0 + k) / (unsigned)(2 * k));
 }
 
-template <int F>
-__global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
-  using G = PitchGeom<F>;
-  constexpr int NT = 256, XS = G::kXS, R = G::kR, TPF = G::kTPF;
-  __shared__ __attribute__((aligned(16))) float xf[F][XS];  // FIR output (x_lp filtered)
-  // per-frame scratch: x_lp during P0-P3, then xcorr / Syy / yy sequences
-  __shared__ __attribute__((aligned(16))) float scr[F][980];
-  constexpr int oXc = 0, oSyc = 148, oSyf = 296, oYy = 592;
-  __shared__ float ac[F][5], lpc2[F][5], xxs[F], fine[F][10];
-  __shared__ int best[F][2], T0s[F], nvs[F], fval[F];
-  __shared__ long long pbo[F];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int V = a.V;
-  const long long total = (long long)a.n_streams * V;
-  const long long ngroups = (total + F - 1) / F;
+// LDS written and read back by lanes of the same wave only: LDS operations of
+// a wave execute in order, so a compiler-level fence is all that is needed.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// pitch_downsample's LPC part (celt_lpc.c _celt_lpc, order 4) and the FIR
+// coefficients lpc2 of celt_fir5, from the 5 autocorrelation values.
+__device__ __forceinline__ void lpc_fir5_coeffs(float (&acv)[5], float (&lpc2)[5]) {
+  acv[0] *= 1.0001f;
+  for (int i = 1; i <= 4; i++) acv[i] -= acv[i] * (.008f * i) * (.008f * i);
+  float lpc[4] = {0, 0, 0, 0};
+  float error = acv[0];
+  if (acv[0] != 0) {
+    for (int i = 0; i < 4; i++) {
+      float r_acc = 0;
+      for (int j = 0; j < i; j++) r_acc += lpc[j] * acv[i - j];
+      r_acc += acv[i + 1];
+      const float r = -r_acc / error;
+      lpc[i] = r;
+      for (int j = 0; j < (i + 1) >> 1; j++) {
+        const float tmp1 = lpc[j], tmp2 = lpc[i - 1 - j];
+        lpc[j] = tmp1 + r * tmp2;
+        lpc[i - 1 - j] = tmp2 + r * tmp1;
+      }
+      error = error - (r * r) * error;
+      if (error < .001f * acv[0]) break;
+    }
+  }
+  float tmp = 1.0f;
+  for (int i = 0; i < 4; i++) {
+    tmp = .9f * tmp;
+    lpc[i] = lpc[i] * tmp;
+  }
+  const float c1 = .8f;
+  lpc2[0] = lpc[0] + .8f;
+  lpc2[1] = lpc[1] + c1 * lpc[0];
+  lpc2[2] = lpc[2] + c1 * lpc[1];
+  lpc2[3] = lpc[3] + c1 * lpc[2];
+  lpc2[4] = c1 * lpc[3];
+}
+
+// ---------------------------------------------------------------------------
+// k_plpc.  The pitch buffers of a tile's 64 streams are staged through LDS in
+// chunks of 16 samples (8 x_lp steps): 16-byte coalesced loads of each
+// stream's row, transposed to [sample][stream] (row pitch 68: conflict-free
+// for both the transposing writes and the column reads), prefetched one chunk
+// ahead.  Tile t = sb * Vr + v (Vr = frame positions of this push); the four
+// waves of a workgroup take consecutive v of the same streams, which share
+// 1248 of their 1728 pitch-buffer samples in L2.
+// ---------------------------------------------------------------------------
+constexpr int kLpStep = 8;                // x_lp steps per chunk
+constexpr int kLpRows = 2 * kLpStep;      // 16 samples; sample 2*n0-1 is carried in a register
+constexpr int kLpPR = kLpRows / 4;        // float4 per stream row of a chunk (= loads per lane)
+constexpr int kLpSPI = 64 / kLpPR;        // streams per load instruction
+constexpr int kLpCols = 64 + kLpSPI / 4;  // 4 * pitch = kLpSPI (mod 64): writes hit distinct banks
+constexpr int kLpChunks = kXlp / kLpStep;  // 54
+static_assert(kXlp % kLpStep == 0, "x_lp chunking");
+
+struct LpSrc {
+  const float *p[kLpPR];  // per load slot: stream row + 4 * (lane % kLpPR)
+};
+
+__device__ __forceinline__ void lp_fetch(const LpSrc &s, int c, float4 (&r)[kLpPR]) {
+#pragma unroll
+  for (int i = 0; i < kLpPR; i++) r[i] = *reinterpret_cast<const float4 *>(s.p[i] + kLpRows * c);
+}
+
+// chunk registers -> LDS [sample][stream]
+__device__ __forceinline__ void lp_stage(float *stg, int lane, const float4 (&r)[kLpPR]) {
+  wave_sync();
+  const int p = lane % kLpPR, s0 = lane / kLpPR;
+#pragma unroll
+  for (int i = 0; i < kLpPR; i++) {
+    float *d = stg + (4 * p) * kLpCols + s0 + kLpSPI * i;
+    d[0] = r[i].x;
+    d[kLpCols] = r[i].y;
+    d[2 * kLpCols] = r[i].z;
+    d[3 * kLpCols] = r[i].w;
+  }
+  wave_sync();
+}
+
+// x_lp[n] for n = kLpStep * c + u from the staged column (pitch_downsample, C = 1)
+template <bool First>
+__device__ __forceinline__ float lp_value(const float *col, int u, float &s_prev) {
+  const float a = col[(2 * u) * kLpCols], b = col[(2 * u + 1) * kLpCols];
+  float x;
+  if (First && u == 0)
+    x = .5f * (.5f * (b) + a);
+  else
+    x = .5f * (.5f * (s_prev + b) + a);
+  s_prev = b;
+  return x;
+}
+
+// xf rows r = n0 - 480 + u of chunk n0 that the Syy recurrences read back
+__device__ __forceinline__ void plpc_back(const float *out, int n0, float (&bk)[kLpStep]) {
+#pragma unroll
+  for (int u = 0; u < kLpStep; u++) {
+    const int r = n0 + u - 480;
+    bk[u] = (r >= 0 && r < 294) ? out[r * ptile::kQuarter] : 0.0f;
+  }
+}
+
+// pass-2 state of one lane (k_plpc)
+struct Fir5State {
+  float l[5];
+  float m1 = 0, m2 = 0, m3 = 0, m4 = 0, m5 = 0;  // x_lp[n-1..n-5]
+  float sp = 0;                                  // pitch-buffer sample 2n-1
+  float Sc = 1.0f, Sf = 1.0f, xx = 0.0f;
+};
+
+// One chunk of pass 2.  Region R of n = n0 .. n0+7:
+//   1 [0, 384)    Syy initial sums      2 [384, 480)  + xx
+//   3 [480, 774)  xx + Syy recurrences  4 the chunk holding n = 773 (guarded)
+//   5 [774, 864)  xx only
+template <bool First, int R>
+__device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, float *out, int n0,
+                                           const float (&bk)[kLpStep]) {
+  float *xo = out + (ptile::kXf + n0) * ptile::kQuarter;
+#pragma unroll
+  for (int u = 0; u < kLpStep; u++) {
+    const float x = lp_value<First>(col, u, f.sp);
+    float y = x;
+    y = y + f.l[0] * f.m1;
+    y = y + f.l[1] * f.m2;
+    y = y + f.l[2] * f.m3;
+    y = y + f.l[3] * f.m4;
+    y = y + f.l[4] * f.m5;
+    f.m5 = f.m4, f.m4 = f.m3, f.m3 = f.m2, f.m2 = f.m1, f.m1 = x;
+    xo[u * ptile::kQuarter] = y;
+    if (R <= 2) {
+      if ((u & 1) == 0) f.Sc = f.Sc + y * y;  // n0 is a multiple of 8: n even <=> u even
+      f.Sf = f.Sf + y * y;
+    }
+    if (R == 3 || (R == 4 && u < (480 + 294) % kLpStep)) {  // region 4 starts at a chunk boundary
+      const int i = n0 + u - 480;
+      const float yb = bk[u];
+      out[(ptile::kSf + i) * ptile::kQuarter] = f.Sf;
+      f.Sf += y * y - yb * yb;
+      f.Sf = (1 > f.Sf) ? 1 : f.Sf;
+      if ((u & 1) == 0) {
+        out[(ptile::kSc + (i >> 1)) * ptile::kQuarter] = f.Sc;
+        f.Sc += y * y - yb * yb;
+        f.Sc = (1 > f.Sc) ? 1 : f.Sc;
+      }
+    }
+    if (R >= 2) f.xx = f.xx + y * y;
+  }
+}
+static_assert(384 % kLpStep == 0 && 480 % kLpStep == 0 && kLpStep % 2 == 0, "pass-2 regions");
+
+__global__ void __launch_bounds__(256, 2) k_plpc(StagedArgs a) {
+  __shared__ float stg_all[4][kLpRows * kLpCols];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  float *stg = stg_all[w];
+  const float *col = stg + lane;
+  const int Vr = a.n_ticks * a.n_channels;
+  const int n_sb = (a.n_streams + 63) >> 6;
+  const long long n_tiles = (long long)n_sb * Vr;
+  for (long long t = (long long)blockIdx.x * 4 + w; t < n_tiles; t += (long long)gridDim.x * 4) {
+    const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
+    LpSrc src;
+#pragma unroll
+    for (int i = 0; i < kLpPR; i++) {
+      const int s = min(sb * 64 + lane / kLpPR + kLpSPI * i, a.n_streams - 1);
+      src.p[i] = a.xs + (size_t)s * a.L + (size_t)v * kFrame + 4 * (lane % kLpPR);
+    }
+    // lane's output column: quarter (lane >> 4) of tile t, [row][16]
+    float *out = a.ptile + ((size_t)(t * 4 + (lane >> 4)) * ptile::kRows) * ptile::kQuarter + (lane & 15);
+    float4 cur[kLpPR];
+
+    // pass 1: x_lp -> _celt_autocorr (lag k: sum_{i<860} x[i] x[i+k], then the tail)
+    float acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, acc4 = 0;
+    float d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+    float h1 = 0, h2 = 0, h3 = 0, h4 = 0, sp = 0;
+    lp_fetch(src, 0, cur);
+    for (int c = 0; c < kLpChunks; c++) {
+      lp_stage(stg, lane, cur);
+      if (c + 1 < kLpChunks) lp_fetch(src, c + 1, cur);
+      if (c == 0) {
+#pragma unroll
+        for (int u = 0; u < kLpStep; u++) {
+          const float x = lp_value<true>(col, u, sp);
+          acc0 = acc0 + x * x;
+          if (u >= 1) acc1 = acc1 + h1 * x;
+          if (u >= 2) acc2 = acc2 + h2 * x;
+          if (u >= 3) acc3 = acc3 + h3 * x;
+          if (u >= 4) acc4 = acc4 + h4 * x;
+          h4 = h3, h3 = h2, h2 = h1, h1 = x;
+        }
+      } else if (c + 1 < kLpChunks) {
+#pragma unroll
+        for (int u = 0; u < kLpStep; u++) {
+          const float x = lp_value<false>(col, u, sp);
+          acc0 = acc0 + x * x;
+          acc1 = acc1 + h1 * x;
+          acc2 = acc2 + h2 * x;
+          acc3 = acc3 + h3 * x;
+          acc4 = acc4 + h4 * x;
+          h4 = h3, h3 = h2, h2 = h1, h1 = x;
+        }
+      } else {
+        // n = 856..863: term i = n - k belongs to the 860-term sum while
+        // i < 860, else (n >= 860 + k) to the tail sum of x[n] x[n-k]
+#pragma unroll
+        for (int u = 0; u < kLpStep; u++) {
+          const int n = c * kLpStep + u;
+          const float x = lp_value<false>(col, u, sp);
+          if (n < 860) acc0 = acc0 + x * x; else d0 = d0 + x * x;
+          if (n - 1 < 860) acc1 = acc1 + h1 * x; else d1 = d1 + x * h1;
+          if (n - 2 < 860) acc2 = acc2 + h2 * x; else d2 = d2 + x * h2;
+          if (n - 3 < 860) acc3 = acc3 + h3 * x; else d3 = d3 + x * h3;
+          acc4 = acc4 + h4 * x;  // n - 4 <= 859
+          (void)n;
+          h4 = h3, h3 = h2, h2 = h1, h1 = x;
+        }
+      }
+    }
+    float acv[5] = {acc0 + d0, acc1 + d1, acc2 + d2, acc3 + d3, acc4 + 0.0f};
+    float l[5];
+    lpc_fir5_coeffs(acv, l);
+
+    // pass 2: x_lp again -> celt_fir5 -> xf; Syy initial sums, xx; from
+    // n = 480 on, the Syy recurrences with xf[n - 480] read back from the tile
+    // buffer (written by this lane 480 steps earlier, fetched a chunk ahead).
+    // The chunk body is specialised per region of n, so it has no branches.
+    Fir5State fs;
+#pragma unroll
+    for (int i = 0; i < 5; i++) fs.l[i] = l[i];
+    float bk[kLpStep], bkn[kLpStep];
+#pragma unroll
+    for (int u = 0; u < kLpStep; u++) bk[u] = bkn[u] = 0.0f;
+    lp_fetch(src, 0, cur);
+    for (int c = 0; c < kLpChunks; c++) {
+      const int n0 = c * kLpStep;
+      lp_stage(stg, lane, cur);
+      if (c + 1 < kLpChunks) lp_fetch(src, c + 1, cur);
+      const int n1 = n0 + kLpStep;  // next chunk
+      if (n1 + kLpStep > 480 && n1 < 480 + 294) plpc_back(out, n1, bkn);
+      if (c == 0)
+        fir5_chunk<true, 1>(fs, col, out, n0, bk);
+      else if (n0 < 384)
+        fir5_chunk<false, 1>(fs, col, out, n0, bk);
+      else if (n0 < 480)
+        fir5_chunk<false, 2>(fs, col, out, n0, bk);
+      else if (n0 + kLpStep <= 480 + 294)
+        fir5_chunk<false, 3>(fs, col, out, n0, bk);
+      else if (n0 < 480 + 294)
+        fir5_chunk<false, 4>(fs, col, out, n0, bk);
+      else
+        fir5_chunk<false, 5>(fs, col, out, n0, bk);
+#pragma unroll
+      for (int u = 0; u < kLpStep; u++) bk[u] = bkn[u];
+    }
+    const float xx = fs.xx;
+    out[ptile::kXx * ptile::kQuarter] = xx;
+
+    // pass 3: yy_lookup[i] = max(0, yy), yy += x[-i]^2 - x[480-i]^2 (x = xf + 384);
+    // the 2 x kLpStep rows of the next chunk are fetched while this one is summed
+    float yy = xx;
+    out[ptile::kYy * ptile::kQuarter] = xx;
+    float ya[kLpStep], yb[kLpStep];
+#pragma unroll
+    for (int u = 0; u < kLpStep; u++) {
+      ya[u] = out[(383 - u) * ptile::kQuarter];
+      yb[u] = out[(863 - u) * ptile::kQuarter];
+    }
+    for (int i0 = 1; i0 <= 384; i0 += kLpStep) {
+      float na[kLpStep], nb[kLpStep];
+      const int i1 = i0 + kLpStep;
+#pragma unroll
+      for (int u = 0; u < kLpStep; u++) {
+        na[u] = i1 <= 384 ? out[(384 - i1 - u) * ptile::kQuarter] : 0.0f;
+        nb[u] = i1 <= 384 ? out[(864 - i1 - u) * ptile::kQuarter] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kLpStep; u++) {
+        yy = yy + ya[u] * ya[u] - yb[u] * yb[u];
+        out[(ptile::kYy + i0 + u) * ptile::kQuarter] = (0 > yy) ? 0 : yy;
+      }
+#pragma unroll
+      for (int u = 0; u < kLpStep; u++) {
+        ya[u] = na[u];
+        yb[u] = nb[u];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_pcorr: one workgroup per quarter tile (16 streams at one frame position;
+// its tile rows are one contiguous block).
+//   Q0 xf (rows 0..863) and the coarse Syy sequence -> LDS
+//   Q1 coarse xcorr: lane = (frame, 10 consecutive lags), a register window of
+//      10 y values slides one sample per step (2 LDS reads per 10 MACs)
+//   Q2 coarse find_best_pitch, lane per frame; the fine Syy values at the
+//      <= 10 candidate lags are fetched here, used in Q4
+//   Q3 fine xcorr at the <= 10 lags within +-2 of 2*best (others are 0)
+//   Q4 fine find_best_pitch + pseudo-interpolation -> T0, candidate count
+//   Q5 remove_doubling products: lane = (frame, candidate c); candidate c's
+//      xcorr at T-1, T, T+1 share a sliding window of 3, plus xcorr(T1b)
+// ---------------------------------------------------------------------------
+constexpr int kPcF = ptile::kQuarter;
+constexpr int kPcXS = 869;  // xf row pitch (odd: frames fall in distinct bank classes)
+constexpr int kPcSP = 153;  // coarse xcorr / Syy row pitch (odd; >= 147 rounded up to the scan block)
+
+__global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
+  constexpr int NT = 256;
+  __shared__ float xf[kPcF][kPcXS];
+  __shared__ float scl[kPcF][kPcSP], xc[kPcF][kPcSP];
+  __shared__ float sfl[kPcF][10], fine[kPcF][10];
+  __shared__ int best[kPcF][2], T0s[kPcF], nvs[kPcF], fval[kPcF];
+  __shared__ long long fidx[kPcF];
+  const int tid = threadIdx.x;
+  const int Vr = a.n_ticks * a.n_channels;
+  const int n_sb = (a.n_streams + 63) >> 6;
+  const long long ngroups = (long long)n_sb * Vr * 4;
+  STAMP_INIT();
   for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    if (tid < F) {
-      const long long f = g * F + tid;
-      int ok = 0;
-      long long off = 0;
-      if (f < total) {
-        const int s = (int)(f / V), v = (int)(f - (long long)s * V);
-        ok = v < ticks_of(a, s) * a.n_channels;
-        off = (long long)s * a.L + (long long)v * kFrame;
-      }
-      fval[tid] = ok;
-      pbo[tid] = off;
+    const long long t = g >> 2;
+    const int q = (int)(g & 3);
+    const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
+    const float *T = a.ptile + (size_t)g * ptile::kRows * ptile::kQuarter;
+    if (tid < kPcF) {
+      const int s = sb * 64 + q * 16 + tid;
+      fval[tid] = s < a.n_streams && v < ticks_of(a, s) * a.n_channels;
+      fidx[tid] = (long long)s * a.V + v;
+    }
+    // Q0
+    for (int idx = tid; idx < kXlp * 4; idx += NT) {
+      const int r = idx >> 2, p = idx & 3;
+      const float4 w4 = reinterpret_cast<const float4 *>(T)[idx];
+      xf[4 * p][r] = w4.x;
+      xf[4 * p + 1][r] = w4.y;
+      xf[4 * p + 2][r] = w4.z;
+      xf[4 * p + 3][r] = w4.w;
+    }
+    for (int idx = tid; idx < 147 * 4; idx += NT) {
+      const int r = idx >> 2, p = idx & 3;
+      const float4 w4 = reinterpret_cast<const float4 *>(T + ptile::kSc * ptile::kQuarter)[idx];
+      scl[4 * p][r] = w4.x;
+      scl[4 * p + 1][r] = w4.y;
+      scl[4 * p + 2][r] = w4.z;
+      scl[4 * p + 3][r] = w4.w;
     }
     __syncthreads();
-    // P0: x_lp[i] = .5*(.5*(pb[2i-1] + pb[2i+1]) + pb[2i])
-    for (int idx = tid; idx < F * kXlp; idx += NT) {
-      const int fr = idx / kXlp, i = idx - fr * kXlp;
-      const float *pb = a.xs + pbo[fr];
-      scr[fr][i] = (i == 0) ? .5f * (.5f * (pb[1]) + pb[0]) : .5f * (.5f * (pb[2 * i - 1] + pb[2 * i + 1]) + pb[2 * i]);
-    }
-    __syncthreads();
-    // P1: _celt_autocorr, lag k of frame fr
-    if (tid < 5 * F) {
-      const int fr = tid / 5, k = tid - 5 * fr;
-      const float *x = scr[fr];
-      const int fastN = kXlp - 4;
-      const float acc = dot_seq(0.0f, x, 1, x + k, 1, fastN);
-      float d = 0;
-      for (int i = k + fastN; i < kXlp; i++) d = d + x[i] * x[i - k];
-      ac[fr][k] = acc + d;
-    }
-    __syncthreads();
-    // P2: lag window, _celt_lpc (order 4), bandwidth expansion, FIR coefficients
-    if (tid < F) {
-      float acv[5];
-      for (int i = 0; i < 5; i++) acv[i] = ac[tid][i];
-      acv[0] *= 1.0001f;
-      for (int i = 1; i <= 4; i++) acv[i] -= acv[i] * (.008f * i) * (.008f * i);
-      float lpc[4] = {0, 0, 0, 0};
-      float error = acv[0];
-      if (acv[0] != 0) {
-        for (int i = 0; i < 4; i++) {
-          float r_acc = 0;
-          for (int j = 0; j < i; j++) r_acc += lpc[j] * acv[i - j];
-          r_acc += acv[i + 1];
-          const float r = -r_acc / error;
-          lpc[i] = r;
-          for (int j = 0; j < (i + 1) >> 1; j++) {
-            const float tmp1 = lpc[j], tmp2 = lpc[i - 1 - j];
-            lpc[j] = tmp1 + r * tmp2;
-            lpc[i - 1 - j] = tmp2 + r * tmp1;
+    RSTAMP(0);
+    // Q1: xcorr[k] = sum_j x_lp4[j] y_lp4[j+k], x_lp4[j] = xf[384+2j], y_lp4[m] = xf[2m]
+    {
+      constexpr int R = 10;
+      const int fr = tid >> 4, k0 = R * (tid & 15);
+      if (k0 < 147) {
+        const float *X = xf[fr] + (kPitchMax >> 1);
+        const float *Y = xf[fr] + 2 * k0;
+        float acc[R], win[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          acc[r] = 0.0f;
+          win[r] = Y[2 * r];
+        }
+        for (int jb = 0; jb < 240; jb += R) {
+#pragma unroll
+          for (int u = 0; u < R; u++) {
+            const float xv = X[2 * (jb + u)];
+#pragma unroll
+            for (int r = 0; r < R; r++) acc[r] = acc[r] + xv * win[(r + u) % R];
+            win[u] = Y[2 * (jb + u + R)];  // lag k0+R-1 at step jb+u+1
           }
-          error = error - (r * r) * error;
-          if (error < .001f * acv[0]) break;
-        }
-      }
-      float tmp = 1.0f;
-      for (int i = 0; i < 4; i++) {
-        tmp = .9f * tmp;
-        lpc[i] = lpc[i] * tmp;
-      }
-      const float c1 = .8f;
-      lpc2[tid][0] = lpc[0] + .8f;
-      lpc2[tid][1] = lpc[1] + c1 * lpc[0];
-      lpc2[tid][2] = lpc[2] + c1 * lpc[1];
-      lpc2[tid][3] = lpc[3] + c1 * lpc[2];
-      lpc2[tid][4] = c1 * lpc[3];
-    }
-    __syncthreads();
-    // P3: celt_fir5, x_lp (scratch) -> xf
-    for (int idx = tid; idx < F * kXlp; idx += NT) {
-      const int fr = idx / kXlp, i = idx - fr * kXlp;
-      const float *x = scr[fr];
-      const float m0 = i >= 1 ? x[i - 1] : 0.0f, m1 = i >= 2 ? x[i - 2] : 0.0f, m2 = i >= 3 ? x[i - 3] : 0.0f,
-                  m3 = i >= 4 ? x[i - 4] : 0.0f, m4 = i >= 5 ? x[i - 5] : 0.0f;
-      float sum = x[i];
-      sum = sum + lpc2[fr][0] * m0;
-      sum = sum + lpc2[fr][1] * m1;
-      sum = sum + lpc2[fr][2] * m2;
-      sum = sum + lpc2[fr][3] * m3;
-      sum = sum + lpc2[fr][4] * m4;
-      xf[fr][i] = sum;
-    }
-    __syncthreads();
-    // P4: energy sequences (waves 0-1) concurrently with the coarse xcorr (waves 2-3)
-    if (wave == 0) {
-      if (lane < 2 * F) {
-        const int fr = lane % F;
-        const bool fs = lane >= F;
-        syy_sequence(xf[fr], fs ? 1 : 2, fs ? 480 : 240, fs ? 294 : 147, scr[fr] + (fs ? oSyf : oSyc));
-      }
-    } else if (wave == 1) {
-      if (lane < F) {
-        const float *x = xf[lane] + (kPitchMax >> 1);
-        const float xx = dot_seq(0.0f, x, 1, x, 1, 480);
-        xxs[lane] = xx;
-        float yy = xx;
-        float *yo = scr[lane] + oYy;
-        yo[0] = xx;
-#pragma unroll 4
-        for (int i = 1; i <= 384; i++) {
-          yy = yy + x[-i] * x[-i] - x[480 - i] * x[480 - i];
-          yo[i] = (0 > yy) ? 0 : yy;
-        }
-      }
-    } else {
-      const int l = tid - 128;
-      const int fr = l / TPF, blk = l - fr * TPF;
-      if (fr < F) {
-        const int k0 = blk * R;
-        const float *xr = xf[fr] + (kPitchMax >> 1);
-        const float *yr = xf[fr] + 2 * k0;
-        // two lags per packed f32 multiply / add (v_pk_mul_f32, v_pk_add_f32)
-        typedef float f2v __attribute__((ext_vector_type(2)));
-        f2v acc[R / 2];
-#pragma unroll
-        for (int p = 0; p < R / 2; p++) acc[p] = f2v{0.0f, 0.0f};
-#pragma unroll 4
-        for (int j = 0; j < 240; j++) {
-          const float xv = xr[2 * j];
-          const f2v xb = f2v{xv, xv};
-#pragma unroll
-          for (int p = 0; p < R / 2; p++) acc[p] = acc[p] + xb * f2v{yr[2 * (j + 2 * p)], yr[2 * (j + 2 * p + 1)]};
         }
 #pragma unroll
-        for (int p = 0; p < R / 2; p++) {
-          if (k0 + 2 * p < 147) scr[fr][oXc + k0 + 2 * p] = acc[p].x;
-          if (k0 + 2 * p + 1 < 147) scr[fr][oXc + k0 + 2 * p + 1] = acc[p].y;
-        }
+        for (int r = 0; r < R; r++)
+          if (k0 + r < 147) xc[fr][k0 + r] = acc[r];
+      } else if (k0 < kPcSP) {
+        // lags 147.. pad the scan blocks: xcorr <= 0 never updates the best pair
+        for (int k = 147; k < kPcSP; k++) xc[fr][k] = -1.0f;
       }
     }
     __syncthreads();
-    // P5: coarse find_best_pitch
-    if (tid < F) {
+    RSTAMP(1);
+    // Q2
+    float sfv[10];
+    if (tid < kPcF) {
+      const int fr = tid;
       int bst[2] = {0, 1};
       float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
-#pragma unroll 4
-      for (int i = 0; i < 147; i++) best_pitch_visit(scr[tid][oXc + i], scr[tid][oSyc + i], i, bn0, bn1, bd0, bd1, bst);
-      best[tid][0] = bst[0];
-      best[tid][1] = bst[1];
+      // operands of the next 8 lags load while these 8 are visited
+      constexpr int B = 8;
+      float xb[B], yb[B];
+#pragma unroll
+      for (int u = 0; u < B; u++) {
+        xb[u] = xc[fr][u];
+        yb[u] = scl[fr][u];
+      }
+      for (int i0 = 0; i0 < 147; i0 += B) {
+        float xn[B], yn[B];
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+          const int i = min(i0 + B + u, kPcSP - 1);
+          xn[u] = xc[fr][i];
+          yn[u] = scl[fr][i];
+        }
+#pragma unroll
+        for (int u = 0; u < B; u++) best_pitch_visit(xb[u], yb[u], i0 + u, bn0, bn1, bd0, bd1, bst);
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+          xb[u] = xn[u];
+          yb[u] = yn[u];
+        }
+      }
+      best[fr][0] = bst[0];
+      best[fr][1] = bst[1];
+#pragma unroll
+      for (int u = 0; u < 10; u++) {
+        const int i = 2 * bst[u / 5] - 2 + (u % 5);
+        sfv[u] = (i >= 0 && i < 294) ? T[(ptile::kSf + i) * ptile::kQuarter + fr] : 0.0f;
+      }
     }
     __syncthreads();
-    // P6: fine xcorr, only the lags within +-2 of 2*best0 / 2*best1 are non-zero
-    if (tid < 10 * F) {
-      const int fr = tid / 10, t = tid - 10 * fr;
+    RSTAMP(2);
+    // Q3
+    if (tid < 10 * kPcF) {
+      const int fr = tid / 10, u = tid - 10 * fr;
       const int bp0 = best[fr][0], bp1 = best[fr][1];
-      const int i = (t < 5 ? 2 * bp0 : 2 * bp1) - 2 + (t % 5);
-      const bool dup = t >= 5 && abs(i - 2 * bp0) <= 2;
+      const int i = (u < 5 ? 2 * bp0 : 2 * bp1) - 2 + (u % 5);
+      const bool dup = u >= 5 && abs(i - 2 * bp0) <= 2;
       if (i >= 0 && i < 294 && !dup) {
         const float *xl = xf[fr] + (kPitchMax >> 1), *y = xf[fr] + i;
         const float sum = dot_seq(0.0f, xl, 1, y, 1, 480);
-        fine[fr][t] = (-1 > sum) ? -1 : sum;
+        fine[fr][u] = (-1 > sum) ? -1 : sum;
       }
     }
     __syncthreads();
-    // P7: fine find_best_pitch + pseudo-interpolation -> T0 (remove_doubling input)
-    if (tid < F) {
+    RSTAMP(3);
+    // Q4
+    if (tid < kPcF) {
       const int fr = tid;
+#pragma unroll
+      for (int u = 0; u < 10; u++) sfl[fr][u] = sfv[u];
       const int bp0 = best[fr][0], bp1 = best[fr][1];
       const int w0 = 2 * bp0 - 2, w1 = 2 * bp1 - 2;
+      // lags of the first window take its values (a duplicate lag of the
+      // second window was not computed in Q3)
+      auto slot = [&](int i) -> int { return (i >= w0 && i <= w0 + 4) ? i - w0 : ((i >= w1 && i <= w1 + 4) ? 5 + i - w1 : -1); };
       auto xcf = [&](int i) -> float {
-        if (i >= w0 && i <= w0 + 4) return fine[fr][i - w0];
-        if (i >= w1 && i <= w1 + 4) return fine[fr][5 + i - w1];
-        return 0.0f;
+        const int s = slot(i);
+        return s < 0 ? 0.0f : fine[fr][s];
       };
       int bst[2] = {0, 1};
       float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
@@ -608,9 +865,9 @@ __global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
         lo1 = t0;
         hi1 = t1;
       }
-      for (int i = max(0, lo0); i <= min(293, hi0); i++) best_pitch_visit(xcf(i), scr[fr][oSyf + i], i, bn0, bn1, bd0, bd1, bst);
+      for (int i = max(0, lo0); i <= min(293, hi0); i++) best_pitch_visit(xcf(i), sfl[fr][slot(i)], i, bn0, bn1, bd0, bd1, bst);
       for (int i = max(max(0, lo1), hi0 + 1); i <= min(293, hi1); i++)
-        best_pitch_visit(xcf(i), scr[fr][oSyf + i], i, bn0, bn1, bd0, bd1, bst);
+        best_pitch_visit(xcf(i), sfl[fr][slot(i)], i, bn0, bn1, bd0, bd1, bst);
       int offset;
       if (bst[0] > 0 && bst[0] < 294 - 1) {
         const float aa = xcf(bst[0] - 1), bb = xcf(bst[0]), cc = xcf(bst[0] + 1);
@@ -633,58 +890,58 @@ __global__ void __launch_bounds__(256) k_pitch(StagedArgs a) {
       }
       T0s[fr] = T0;
       nvs[fr] = nv;
-      if (fval[fr]) {
-        float *rg = a.rec + (g * F + fr) * rec::kSize;
-        rg[rec::kT0] = __int_as_float(T0);
-        rg[rec::kXx] = xxs[fr];
-        rg[rec::kYyT0] = scr[fr][oYy + T0];
-        rg[rec::kNValid] = __int_as_float(nv);
+    }
+    __syncthreads();
+    RSTAMP(4);
+    // Q5
+    if (tid < 15 * kPcF) {
+      const int fr = tid / 15, c = tid - 15 * fr;
+      if (fval[fr] && (c == 0 || c - 1 < nvs[fr])) {
+        const int T0 = T0s[fr];
+        const int Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
+        const int Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
+        // yy_lookup gathers, consumed after the products
+        const float yyA = T[(ptile::kYy + Tc) * ptile::kQuarter + fr];
+        const float yyB = T[(c == 0 ? ptile::kXx : ptile::kYy + Tb) * ptile::kQuarter + fr];
+        const float *X = xf[fr] + (kPitchMax >> 1);
+        float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
+        float win[3] = {X[-Tc - 1], X[-Tc], X[-Tc + 1]};
+        for (int j0 = 0; j0 < 480; j0 += 3) {
+#pragma unroll
+          for (int u = 0; u < 3; u++) {
+            const int j = j0 + u;
+            const float xv = X[j];
+            aM = aM + xv * win[u % 3];
+            a0 = a0 + xv * win[(u + 1) % 3];
+            aP = aP + xv * win[(u + 2) % 3];
+            aB = aB + xv * X[j - Tb];
+            win[u] = X[j + 2 - Tc];  // lag T-1 at step j+1
+          }
+        }
+        float *rg = a.rec + fidx[fr] * rec::kSize;
+        if (c == 0) {
+          rg[rec::kT0] = __int_as_float(T0);
+          rg[rec::kXx] = yyB;
+          rg[rec::kXy] = a0;
+          rg[rec::kYyT0] = yyA;
+          rg[rec::kNValid] = __int_as_float(nvs[fr]);
+        } else {
+          float *qk = rg + rec::kK + (c - 1) * 6;
+          qk[0] = __int_as_float(Tc);
+          qk[1] = __int_as_float(Tb);
+          qk[2] = a0;
+          qk[3] = aB;
+          qk[4] = yyA;
+          qk[5] = yyB;
+        }
+        rg[rec::kSpec + c * 3] = aP;
+        rg[rec::kSpec + c * 3 + 2] = aM;
       }
     }
     __syncthreads();
-    // P8: candidate metadata + remove_doubling dots (C order, one per lane)
-    if (tid < 14 * F) {
-      const int fr = tid / 14, kk = tid - 14 * fr, k = kk + 2;
-      if (fval[fr] && kk < nvs[fr]) {
-        const int T0 = T0s[fr], T1 = rd_T1(T0, k), T1b = rd_T1b(T0, T1, k);
-        float *q = a.rec + (g * F + fr) * rec::kSize + rec::kK + kk * 6;
-        q[0] = __int_as_float(T1);
-        q[1] = __int_as_float(T1b);
-        q[4] = scr[fr][oYy + T1];
-        q[5] = scr[fr][oYy + T1b];
-      }
-    }
-    for (int idx = tid; idx < F * G::kG3; idx += NT) {
-      const int fr = idx / G::kG3, q = idx - fr * G::kG3;
-      if (!fval[fr]) continue;
-      const int T0 = T0s[fr], nv = nvs[fr];
-      int lag = -1, slot = 0;
-      if (q == 0) {
-        lag = T0;
-        slot = rec::kXy;
-      } else if (q < 29) {
-        const int kk = (q - 1) >> 1, k = kk + 2;
-        if (kk < nv) {
-          const int T1 = rd_T1(T0, k);
-          lag = ((q - 1) & 1) ? rd_T1b(T0, T1, k) : T1;
-          slot = rec::kK + kk * 6 + 2 + ((q - 1) & 1);
-        }
-      } else {
-        const int c = (q - 29) >> 1, side = (q - 29) & 1;
-        if (c == 0 || c - 1 < nv) {
-          const int T = (c == 0) ? T0 : rd_T1(T0, c + 1);
-          lag = side ? T + 1 : T - 1;
-          slot = rec::kSpec + c * 3 + (side ? 2 : 0);
-        }
-      }
-      if (lag >= 0) {
-        const float *xl = xf[fr] + (kPitchMax >> 1);
-        const float acc = dot_seq(0.0f, xl, 1, xl - lag, 1, 480);
-        a.rec[(g * F + fr) * rec::kSize + slot] = acc;
-      }
-    }
-    __syncthreads();
+    RSTAMP(5);
   }
+  STAMP_FLUSH(32, 6);
 }
 
 // ---------------------------------------------------------------------------
@@ -1741,8 +1998,8 @@ __global__ void __launch_bounds__(64) k_vadm(StagedArgs a) {
 // launcher
 // ---------------------------------------------------------------------------
 const char *staged_kernel_name(int i) {
-  static const char *const names[kStagedKernels] = {"k_prep2", "k_fftA",  "k_pitch", "k_select", "k_pspec",
-                                                     "k_rnn",   "k_synth", "k_ola",   "k_winmeta", "k_fftb"};
+  static const char *const names[kStagedKernels] = {"k_prep2", "k_fftA", "k_plpc",  "k_pcorr",   "k_select", "k_pspec",
+                                                     "k_rnn",   "k_synth", "k_ola", "k_winmeta", "k_fftb"};
   return (i >= 0 && i < kStagedKernels) ? names[i] : nullptr;
 }
 
@@ -1763,8 +2020,8 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   static const int g_fftA = resident_blocks(k_fftA<FF>, 256, n_cu);
   static const int g_pspec = resident_blocks(k_pspec<FF>, 256, n_cu);
   static const int g_synth = resident_blocks(k_synth<FF>, 256, n_cu);
-  static const int g_pitch4 = resident_blocks(k_pitch<4>, 256, n_cu);
-  static const int g_pitch8 = resident_blocks(k_pitch<8>, 256, n_cu);
+  static const int g_plpc = resident_blocks(k_plpc, 256, n_cu);
+  static const int g_pcorr = resident_blocks(k_pcorr, 256, n_cu);
   // lane-per-stream kernels: 16 streams per workgroup spreads the serial
   // chains over more CUs (each chain is latency-bound, not lane-bound)
   const int lane_blocks = (a.n_streams + 15) / 16;
@@ -1784,34 +2041,28 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, stream, a);
   rec(2);
   {
-    // frames per k_pitch workgroup: 4 (default) or 8 (FVAD_PITCH_FRAMES=8, tuning only)
-    static const int fp = [] {
-      const char *e = getenv("FVAD_PITCH_FRAMES");
-      return (e && atoi(e) == 8) ? 8 : kPitchFrames;
-    }();
-    const long long groups = (frames + fp - 1) / fp;
-    if (fp == 8)
-      hipLaunchKernelGGL(k_pitch<8>, grid(groups, g_pitch8), dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL(k_pitch<4>, grid(groups, g_pitch4), dim3(256), 0, stream, a);
+    const long long tiles = (long long)((a.n_streams + 63) / 64) * a.n_ticks * a.n_channels;
+    hipLaunchKernelGGL(k_plpc, grid((tiles + 3) / 4, g_plpc), dim3(256), 0, stream, a);
+    rec(3);
+    hipLaunchKernelGGL(k_pcorr, grid(tiles * 4, g_pcorr), dim3(256), 0, stream, a);
   }
-  rec(3);
-  hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(4);
-  hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(5);
+  hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
+  rec(6);
   hipLaunchKernelGGL((k_rnn<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
                      stream, a);
-  rec(6);
-  hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
   rec(7);
+  hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
+  rec(8);
   const long long ola_threads = frames * kFrame;
   hipLaunchKernelGGL(k_ola, dim3((unsigned)((ola_threads + 255) / 256)), dim3(256), 0, stream, a);
-  rec(8);
-  hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(9);
-  hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(10);
+  hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
+  rec(11);
   return hipGetLastError();
 }
 

@@ -9,6 +9,7 @@ candidates).  The per-phase breakdown is reproduced in DESIGN.md §Roofline.
 """
 
 FRAME = 480
+PTILE_ROWS = 864 + 147 + 294 + 385 + 1  # k_plpc -> k_pcorr rows per frame (fvad_staged.h ptile)
 
 
 def _fft960():
@@ -100,7 +101,7 @@ def staged_kernels(n_channels=2, fft_size=2048):
     """Per channel-frame algorithmic flops and HBM bytes of each staged kernel
     (fvad_staged.hip).  Flops re-partition phases() (the sum is unchanged);
     bytes are the kernel's compulsory reads + writes of its inputs/outputs in
-    the staged layout.  k_pitch's speculative work (the
+    the staged layout.  k_pcorr's speculative work (the
     final 3-lag xcorr for every candidate instead of the selected one) is
     counted once, as the reference computes it."""
     p = phases(n_channels, fft_size)
@@ -109,13 +110,18 @@ def staged_kernels(n_channels=2, fft_size=2048):
     dct_ly = 22 * 44 + 22 * 2
     dct_exp = 6 * 44 + 6 * 2
     spec = 481 * 8  # one complex spectrum
+    pitch = (p["pitch downsample + autocorr + LPC + FIR5"] + p["coarse xcorr 147x240 + find_best_pitch"] +
+             p["fine xcorr <=10x480 + find_best_pitch"] + p["remove_doubling"] - 14 * 12)
+    # k_plpc: x_lp, autocorr, LPC, FIR and the serial energy recurrences
+    # (coarse / fine Syy init + updates, xx, yy_lookup); k_pcorr the rest
+    plpc = (p["pitch downsample + autocorr + LPC + FIR5"] + 240 * 2 + 147 * 4 + 480 * 2 + 294 * 4 +
+            480 * 2 + 384 * 4)
     k = {
         "k_prep2": (p["prep: s16 scale + HP biquad + rms"], 480 * 4 * 2 + 4.0 / C),
         "k_fftA": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly,
                    960 * 4 + spec + 22 * 4 * 2 + 4),
-        "k_pitch": (p["pitch downsample + autocorr + LPC + FIR5"] + p["coarse xcorr 147x240 + find_best_pitch"] +
-                    p["fine xcorr <=10x480 + find_best_pitch"] + p["remove_doubling"] - 14 * 12,
-                    1728 * 4 + 144 * 4),
+        "k_plpc": (plpc, 1728 * 4 + PTILE_ROWS * 4),
+        "k_pcorr": (pitch - plpc, (864 + 147 + 10 + 29 + 1) * 4 + 144 * 4),
         "k_select": (14 * 12, 144 * 4 + 4),
         "k_pspec": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
         "k_rnn": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"] + p["pitch filter + gains"],

@@ -53,10 +53,10 @@ if MODE == "staged":
         print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[16 + i] / max(1, ft), buf[16 + i] / groups))
 
 if MODE == "staged":
-    PIT = ["P0 x_lp", "P1 autocorr", "P2 LPC", "P3 FIR", "P4 Syy/yy chains + coarse xcorr", "P5 coarse scan",
-           "P6 fine xcorr", "P7 fine scan", "P8 remove_doubling dots"]
-    groups = B * 2 * T / 4.0
-    pt = sum(buf[32:41])
-    print("k_pitch: stamped cycles per 4-frame group per WG: %.0f" % (pt / max(1, groups)))
+    PIT = ["Q0 xf + coarse Syy -> LDS", "Q1 coarse xcorr", "Q2 coarse scan", "Q3 fine xcorr", "Q4 fine scan",
+           "Q5 remove_doubling products"]
+    groups = B * 2 * T / 16.0
+    pt = sum(buf[32:38])
+    print("k_pcorr: stamped cycles per 16-frame group per WG: %.0f" % (pt / max(1, groups)))
     for i, n in enumerate(PIT):
         print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[32 + i] / max(1, pt), buf[32 + i] / groups))
