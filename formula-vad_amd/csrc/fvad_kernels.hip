@@ -802,6 +802,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
         a.out_win_ratio[o] = complete ? win_ratio : 0.0f;
         a.out_win_vad[o] = complete ? vad_low : 0.0f;
       }
+      if (!complete && tid < C * a.n_bands) a.out_band[o * C * a.n_bands + tid] = 0.0f;  // defined: no window
       if (complete) {
         // FFT B per channel: window, kissfft (radix-4 DIT), kiss_fftr post-pass, |X|*norm, band sums
         const int nc = P->ncfft_b;

@@ -10,7 +10,7 @@
 namespace fvad {
 
 constexpr int kStagedKernels = 11;
-constexpr int kPitchRecord = 144;  // floats per frame of the pitch record (k_pcorr -> k_select)
+constexpr int kPitchRecord = 80;  // floats per frame of the pitch record (k_pcorr -> k_select)
 
 // Pitch tile buffer (k_plpc -> k_pcorr): a tile is 64 streams at one frame
 // position; each quarter (16 streams) is one contiguous block of kRows rows of
@@ -95,9 +95,21 @@ struct StagedArgs {
   unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn
 };
 
-// Launch the 11 kernels on `stream`; when ev != nullptr, ev[0..11] are
-// recorded around them (per-kernel timing).
-hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev);
+// Streams of one launch: k_fftA runs on `aux` concurrently with the pitch
+// branch (k_plpc -> k_pcorr -> k_select) on `main`; `fork` / `join` order
+// them (k_prep2 before both, k_pspec after both).
+struct StagedStreams {
+  hipStream_t main, aux;
+  hipEvent_t fork, join;
+};
+// Timing events: kernel i runs between ev[kStagedTime[i][0]] and
+// ev[kStagedTime[i][1]]; ev[0] and ev[kStagedLast] bracket the launch.
+constexpr int kStagedEvents = 15, kStagedLast = 13;
+constexpr int kStagedTime[kStagedKernels][2] = {{0, 1}, {2, 3},   {14, 4},  {4, 5},   {5, 6},  {7, 8},
+                                                {8, 9}, {9, 10}, {10, 11}, {11, 12}, {12, 13}};
+// Launch the 11 kernels; when ev != nullptr the kStagedEvents timing events
+// are recorded.
+hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev);
 const char *staged_kernel_name(int i);
 // Device VADMachines over the window outputs a.out_* of one push: overlap =
 // the light HBM variant meant to co-run with the next push on a side stream.

@@ -390,13 +390,27 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
 //            frame) and the pitch record for k_select.
 // Every C-order sum stays on one lane in its original order.
 // ---------------------------------------------------------------------------
+// Pitch record of a frame (k_pcorr -> k_select): everything of
+// remove_doubling's candidate loop that does not depend on the previous
+// frame, so k_select's serial part is compares only.
+//   T0, candidate count, g0 = pitch_gain(xcorr(T0), xx, yy[T0]), xcorr(T0),
+//   yy[T0], the pseudo-interpolation offset of T0; then per k = 2..15:
+//   T1, g1 = pitch_gain(xy, xx, yy), xy = (xcorr(T1) + xcorr(T1b)) / 2,
+//   yy = (yy[T1] + yy[T1b]) / 2, the offset of T1.
 namespace rec {
-constexpr int kT0 = 0, kXx = 1, kXy = 2, kYyT0 = 3, kNValid = 4;
-constexpr int kK = 8;       // per k=2..15: T1, T1b, s1 = xcorr(T1), s2 = xcorr(T1b), yyT1, yyT1b
-constexpr int kSpec = 96;   // candidate c (0 = T0, k-1 = T1_k): xcorr at T-1 [+0] and T+1 [+2]
-constexpr int kSize = 144;  // (the xcorr at T itself is kXy / s1)
+constexpr int kT0 = 0, kNValid = 1, kG0 = 2, kXy0 = 3, kYy0 = 4, kOff0 = 5;
+constexpr int kK = 8, kKStride = 5;  // T1, g1, xy, yy, offset
+constexpr int kSize = 80;
 }  // namespace rec
 static_assert(rec::kSize == kPitchRecord, "pitch record size");
+static_assert(rec::kK + 14 * rec::kKStride <= rec::kSize && rec::kSize % 4 == 0, "pitch record layout");
+
+// remove_doubling's final pseudo-interpolation from the xcorr at T-1, T, T+1
+__device__ __forceinline__ int pitch_offset(float x0, float x1, float x2) {
+  if ((x2 - x0) > .7f * (x1 - x0)) return 1;
+  if ((x0 - x2) > .7f * (x1 - x2)) return -1;
+  return 0;
+}
 
 __device__ __forceinline__ int rd_T1(int T0, int k) { return (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k)); }
 __device__ __forceinline__ int rd_T1b(int T0, int T1, int k) {
@@ -900,9 +914,10 @@ __global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
         const int T0 = T0s[fr];
         const int Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
         const int Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
-        // yy_lookup gathers, consumed after the products
+        // yy_lookup and xx gathers, consumed after the products
         const float yyA = T[(ptile::kYy + Tc) * ptile::kQuarter + fr];
-        const float yyB = T[(c == 0 ? ptile::kXx : ptile::kYy + Tb) * ptile::kQuarter + fr];
+        const float yyB = T[(ptile::kYy + Tb) * ptile::kQuarter + fr];
+        const float xx = T[ptile::kXx * ptile::kQuarter + fr];
         const float *X = xf[fr] + (kPitchMax >> 1);
         float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
         float win[3] = {X[-Tc - 1], X[-Tc], X[-Tc + 1]};
@@ -919,23 +934,23 @@ __global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
           }
         }
         float *rg = a.rec + fidx[fr] * rec::kSize;
+        const int off = pitch_offset(aP, a0, aM);
         if (c == 0) {
           rg[rec::kT0] = __int_as_float(T0);
-          rg[rec::kXx] = yyB;
-          rg[rec::kXy] = a0;
-          rg[rec::kYyT0] = yyA;
           rg[rec::kNValid] = __int_as_float(nvs[fr]);
+          rg[rec::kG0] = pitch_gain(a0, xx, yyA);
+          rg[rec::kXy0] = a0;
+          rg[rec::kYy0] = yyA;
+          rg[rec::kOff0] = __int_as_float(off);
         } else {
-          float *qk = rg + rec::kK + (c - 1) * 6;
+          float *qk = rg + rec::kK + (c - 1) * rec::kKStride;
+          const float xy = .5f * (a0 + aB), yy = .5f * (yyA + yyB);
           qk[0] = __int_as_float(Tc);
-          qk[1] = __int_as_float(Tb);
-          qk[2] = a0;
-          qk[3] = aB;
-          qk[4] = yyA;
-          qk[5] = yyB;
+          qk[1] = pitch_gain(xy, xx, yy);
+          qk[2] = xy;
+          qk[3] = yy;
+          qk[4] = __int_as_float(off);
         }
-        rg[rec::kSpec + c * 3] = aP;
-        rg[rec::kSpec + c * 3 + 2] = aM;
       }
     }
     __syncthreads();
@@ -956,28 +971,31 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
   int *istp = reinterpret_cast<int *>(stp);
   int last_period = istp[st::kLastPeriod];
   float last_gain = stp[st::kLastGain];
+  // the next frame's record loads while this frame's candidates are compared
+  constexpr int N4 = rec::kSize / 4;
+  float r[rec::kSize], rn[rec::kSize];
+  const float4 *src = reinterpret_cast<const float4 *>(a.rec + (size_t)s * a.V * rec::kSize);
+#pragma unroll
+  for (int i = 0; i < N4; i++) *reinterpret_cast<float4 *>(&r[4 * i]) = src[i];
   for (int v = 0; v < nf; v++) {
     const size_t f = (size_t)s * a.V + v;
-    const float *r = a.rec + f * rec::kSize;
+    if (v + 1 < nf) {
+#pragma unroll
+      for (int i = 0; i < N4; i++) *reinterpret_cast<float4 *>(&rn[4 * i]) = src[(size_t)(v + 1) * N4 + i];
+    }
     const int T0 = __float_as_int(r[rec::kT0]);
     const int nv = __float_as_int(r[rec::kNValid]);
     const int prev_period = last_period / 2;
     const float prev_gain = last_gain;
-    const float xx = r[rec::kXx];
-    float xy = r[rec::kXy];
-    float yy = r[rec::kYyT0];
-    float best_xy = xy, best_yy = yy;
-    const float g0 = pitch_gain(xy, xx, yy);
-    float gg = g0;
-    int T = T0, cand = 0;
+    const float g0 = r[rec::kG0];
+    float best_xy = r[rec::kXy0], best_yy = r[rec::kYy0], gg = g0;
+    int T = T0, offset = __float_as_int(r[rec::kOff0]);
+#pragma unroll
     for (int k = 2; k <= 15; k++) {
       const int kk = k - 2;
-      if (kk >= nv) break;
-      const float *q = r + rec::kK + kk * 6;
+      const float *q = r + rec::kK + kk * rec::kKStride;
       const int T1 = __float_as_int(q[0]);
-      xy = .5f * (q[2] + q[3]);
-      yy = .5f * (q[4] + q[5]);
-      const float g1 = pitch_gain(xy, xx, yy);
+      const float g1 = q[1];
       float cont;
       if (abs(T1 - prev_period) <= 1)
         cont = prev_gain;
@@ -997,12 +1015,14 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
         const float vv = .9f * g0 - cont;
         thresh = (.5f > vv) ? .5f : vv;
       }
-      if (g1 > thresh) {
-        best_xy = xy;
-        best_yy = yy;
+      // candidates are a prefix (k < 2 + nv): the reference loop stops at the
+      // first T1 < 30
+      if (kk < nv && g1 > thresh) {
+        best_xy = q[2];
+        best_yy = q[3];
         T = T1;
         gg = g1;
-        cand = k - 1;
+        offset = __float_as_int(q[4]);
       }
     }
     best_xy = (0 > best_xy) ? 0 : best_xy;
@@ -1011,21 +1031,14 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
       pg = 1.0f;
     else
       pg = best_xy / (best_yy + 1);
-    const float x0 = r[rec::kSpec + cand * 3], x2 = r[rec::kSpec + cand * 3 + 2];
-    const float x1 = cand == 0 ? r[rec::kXy] : r[rec::kK + (cand - 1) * 6 + 2];  // xcorr at T itself
-    int offset;
-    if ((x2 - x0) > .7f * (x1 - x0))
-      offset = 1;
-    else if ((x0 - x2) > .7f * (x1 - x2))
-      offset = -1;
-    else
-      offset = 0;
     if (pg > gg) pg = gg;
     int pi = 2 * T + offset;
     if (pi < kPitchMin) pi = kPitchMin;
     a.pitch[f] = pi;
     last_period = pi;
     last_gain = pg;
+#pragma unroll
+    for (int i = 0; i < rec::kSize; i++) r[i] = rn[i];
   }
   istp[st::kLastPeriod] = last_period;
   stp[st::kLastGain] = last_gain;
@@ -1683,6 +1696,8 @@ __global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
         vol += ratio * ((float)kFrame / (float)FB);
         a.out_win_ratio[o] = 0.0f;
         a.out_win_vad[o] = 0.0f;
+        // no window completes in this tick: band sums are defined as 0
+        for (int i = 0; i < a.n_channels * a.n_bands; i++) a.out_band[o * a.n_channels * a.n_bands + i] = 0.0f;
       }
       a.out_win_flag[o] = complete ? 1 : 0;
       fd++;
@@ -2014,7 +2029,8 @@ int resident_blocks(K kernel, int threads, int n_cu) {
 }
 }  // namespace
 
-hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev) {
+hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev) {
+  hipStream_t stream = st.main;
   constexpr int NT = 256;
   constexpr int FF = kFftFrames;
   static const int g_fftA = resident_blocks(k_fftA<FF>, 256, n_cu);
@@ -2031,38 +2047,50 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   auto rec = [&](int k) {
     if (ev) (void)hipEventRecord(ev[k], stream);
   };
+  auto rec_aux = [&](int k) {
+    if (ev) (void)hipEventRecord(ev[k], st.aux);
+  };
   rec(0);
   {
     const int S = kPrepSlots / a.n_channels;
     hipLaunchKernelGGL(k_prep2, dim3((a.n_streams + S - 1) / S), dim3(256), 0, stream, a);
   }
   rec(1);
+  // fork: k_fftA (aux) || pitch branch (main); both only read xs and write
+  // disjoint buffers (X, Ex, Lyf, silence | ptile, rec, pitch, pitch state)
   const long long fgroups = (frames + FF - 1) / FF;
-  hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, stream, a);
-  rec(2);
+  (void)hipEventRecord(st.fork, stream);
+  (void)hipStreamWaitEvent(st.aux, st.fork, 0);
+  rec_aux(2);
+  hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, st.aux, a);
+  rec_aux(3);
+  (void)hipEventRecord(st.join, st.aux);
   {
     const long long tiles = (long long)((a.n_streams + 63) / 64) * a.n_ticks * a.n_channels;
+    rec(14);
     hipLaunchKernelGGL(k_plpc, grid((tiles + 3) / 4, g_plpc), dim3(256), 0, stream, a);
-    rec(3);
+    rec(4);
     hipLaunchKernelGGL(k_pcorr, grid(tiles * 4, g_pcorr), dim3(256), 0, stream, a);
   }
-  rec(4);
-  hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(5);
-  hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(6);
+  (void)hipStreamWaitEvent(stream, st.join, 0);  // join
+  rec(7);
+  hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
+  rec(8);
   hipLaunchKernelGGL((k_rnn<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
                      stream, a);
-  rec(7);
+  rec(9);
   hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
-  rec(8);
+  rec(10);
   const long long ola_threads = frames * kFrame;
   hipLaunchKernelGGL(k_ola, dim3((unsigned)((ola_threads + 255) / 256)), dim3(256), 0, stream, a);
-  rec(9);
-  hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(16), 0, stream, a);
-  rec(10);
-  hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
   rec(11);
+  hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(16), 0, stream, a);
+  rec(12);
+  hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
+  rec(13);
   return hipGetLastError();
 }
 

@@ -121,8 +121,8 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_fftA": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly,
                    960 * 4 + spec + 22 * 4 * 2 + 4),
         "k_plpc": (plpc, 1728 * 4 + PTILE_ROWS * 4),
-        "k_pcorr": (pitch - plpc, (864 + 147 + 10 + 29 + 1) * 4 + 144 * 4),
-        "k_select": (14 * 12, 144 * 4 + 4),
+        "k_pcorr": (pitch - plpc - 14 * 4, (864 + 147 + 10 + 29 + 1) * 4 + 80 * 4),
+        "k_select": (14 * 4 + 14 * 12, 80 * 4 + 4),
         "k_pspec": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
         "k_rnn": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"] + p["pitch filter + gains"],
                   22 * 4 * 4 + 8 * 4 + 3 * spec + 4),

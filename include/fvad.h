@@ -133,7 +133,7 @@ typedef struct {
   int32_t *win_flag;   /* [ticks][streams]  1 if an FFT-B window completed in this tick */
   float *win_ratio;    /* [ticks][streams]  share-weighted window volume ratio (VAD.zig:319-325) */
   float *win_vad;      /* [ticks][streams]  window vad = last frame's vad (VAD.zig:330) */
-  float *band;         /* [ticks][streams][channels][n_bands] band sums (PipelineFFT.zig:99-112) */
+  float *band;         /* [ticks][streams][channels][n_bands] band sums (PipelineFFT.zig:99-112); 0 where win_flag is 0 */
   float *denoised;     /* [ticks][streams][channels][480] normalised denoised PCM (want_denoised) */
 } fvad_outputs;
 
@@ -151,7 +151,8 @@ int fvad_engine_run_resident(fvad_engine *e, int n_ticks);
 int fvad_engine_sync(fvad_engine *e);
 /* average per-launch kernel durations (ms) of the timed resident runs,
  * measured with HIP events on the engine's stream.  ms_avg holds
- * FVAD_MAX_TIMES doubles: [0] whole push, [1 + i] kernel i (names below). */
+ * FVAD_MAX_TIMES doubles: [0] whole push (GPU time from its first to its last
+ * kernel; staged kernels may overlap), [1 + i] kernel i (names below). */
 int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_runs);
 /* name of kernel i of this engine's mode, NULL past the last one */
 const char *fvad_engine_kernel_name(const fvad_engine *e, int i);
