@@ -1293,18 +1293,44 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 
 template <int S, int G, int NT>
 __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) int8_t W[rnnimg::kBytes];
-  __shared__ float tt[204];
-  __shared__ __attribute__((aligned(16))) float featT[44 * S];
-  __shared__ float ceps[S][kCeps * kBands];
-  __shared__ float dist[S][kCeps * kCeps];
-  __shared__ __attribute__((aligned(16))) float doutT[24 * S], gvT[2][24 * S], gnT[2][48 * S], gdT[2][96 * S];
-  __shared__ __attribute__((aligned(16))) float zrT[192 * S];
-  __shared__ float lastg[S][kBands];
-  __shared__ float pf[S][kRnnPf];  // features of the current frame (prefetched)
-  __shared__ int memid[S], act[S], nfs[S];
-  __shared__ long long fbase[S];
-  __shared__ float vad_s[S];
+  // One LDS block with a fixed member order: the activation vectors come
+  // first (all below 64 KB, so every read of them uses an immediate offset),
+  // the 90 KB GRU image last.
+  struct Lds {
+    alignas(16) float featT[44 * S];
+    alignas(16) float doutT[24 * S];
+    alignas(16) float gvT[2][24 * S];
+    alignas(16) float gnT[2][48 * S];
+    alignas(16) float gdT[2][96 * S];
+    alignas(16) float zrT[192 * S];
+    float tt[204];
+    float ceps[S][kCeps * kBands];
+    float dist[S][kCeps * kCeps];
+    float lastg[S][kBands];
+    float pf[S][kRnnPf];  // features of the current frame (prefetched)
+    int memid[S], act[S], nfs[S];
+    long long fbase[S];
+    float vad_s[S];
+    alignas(16) int8_t W[rnnimg::kBytes];
+  };
+  __shared__ Lds L;
+  auto &featT = L.featT;
+  auto &doutT = L.doutT;
+  auto &gvT = L.gvT;
+  auto &gnT = L.gnT;
+  auto &gdT = L.gdT;
+  auto &zrT = L.zrT;
+  auto &tt = L.tt;
+  auto &ceps = L.ceps;
+  auto &dist = L.dist;
+  auto &lastg = L.lastg;
+  auto &pf = L.pf;
+  auto &memid = L.memid;
+  auto &act = L.act;
+  auto &nfs = L.nfs;
+  auto &fbase = L.fbase;
+  auto &vad_s = L.vad_s;
+  auto &W = L.W;
   const int tid = threadIdx.x;
   const int sb = blockIdx.x * S;
   {
