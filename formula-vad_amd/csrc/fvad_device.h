@@ -175,8 +175,8 @@ __device__ __forceinline__ void fft960_load(Fft960Tw &t, const float2 *__restric
 // F independent 960-point transforms W[fr][960], fr < F, by one 256-thread
 // workgroup: a thread owns the same butterfly index in every frame, so its
 // twiddles stay in registers and each stage costs one barrier for F frames.
-template <int F>
-__device__ __forceinline__ void fft960_run(const Fft960Tw &t, float2 (*W)[kWin], int tid) {
+template <int F, int P>
+__device__ __forceinline__ void fft960_run(const Fft960Tw &t, float2 (*W)[P], int tid) {
   if (tid < 240) {  // radix 4, m = 1
 #pragma unroll
     for (int fr = 0; fr < F; fr++) {
@@ -253,6 +253,44 @@ __device__ __forceinline__ float band_sum_t(const float2 *A, const float2 *B, co
   if (b == 0 || b == kBands - 1) acc *= 2;
   return acc;
 }
+// compute_band_energy / compute_band_corr split in two: the per-bin terms of
+// bin k < 400 (band i = of[k]) are computed by any lane,
+//   lo[k] = (1 - frac[k]) * tmp  (summed into band i)
+//   hi[k] = frac[k] * tmp        (summed into band i + 1),  tmp = A.x*B.x + A.y*B.y,
+// with exactly band_sum_t's roundings; band_chain() then adds them in band_sum_t's
+// order.  Band edges are multiples of 4, so the chain reads 4 terms per load.
+__device__ __forceinline__ void band_terms(float2 A, float2 B, const BandTab &T, int k, float &lo, float &hi) {
+  float tmp = A.x * B.x;
+  tmp += A.y * B.y;
+  hi = T.frac[k] * tmp;
+  lo = (1 - T.frac[k]) * tmp;
+}
+__device__ __forceinline__ float band_chain(const float *lo, const float *hi, const BandTab &T, int b) {
+  float acc = 0;
+  if (b >= 1) {
+    const float4 *h4 = reinterpret_cast<const float4 *>(hi);
+    for (int q = T.e4[b - 1] >> 2; q < T.e4[b] >> 2; q++) {
+      const float4 v = h4[q];
+      acc += v.x;
+      acc += v.y;
+      acc += v.z;
+      acc += v.w;
+    }
+  }
+  if (b <= kBands - 2) {
+    const float4 *l4 = reinterpret_cast<const float4 *>(lo);
+    for (int q = T.e4[b] >> 2; q < T.e4[b + 1] >> 2; q++) {
+      const float4 v = l4[q];
+      acc += v.x;
+      acc += v.y;
+      acc += v.z;
+      acc += v.w;
+    }
+  }
+  if (b == 0 || b == kBands - 1) acc *= 2;
+  return acc;
+}
+
 __device__ __forceinline__ float interp_gain_t(const float *bandE, const BandTab &T, int k) {
   if (k >= 400) return 0.0f;
   const int b = T.of[k];

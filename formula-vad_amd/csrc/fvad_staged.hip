@@ -74,6 +74,12 @@ namespace fvad {
 namespace {
 constexpr int kHist = kPitchBuf - kFrame;  // 1248
 constexpr float kScale960 = 1.f / 960;
+// LDS row pitch of the 960-point transforms (float2): frames 16 banks apart,
+// so band-sum lanes of different frames reading the same bin do not conflict
+constexpr int kWinP = kWin + 8;
+// after a forward transform, bins >= 481 of a row are dead: band terms go there
+constexpr int kTermOff = 964;  // float offset in a W row (16-byte aligned; + 800 <= 2 * kWinP)
+static_assert(kTermOff >= 2 * kFreq && kTermOff % 4 == 0 && kTermOff + 800 <= 2 * kWinP, "band term area");
 
 __device__ __forceinline__ int ticks_of(const StagedArgs &a, int s) {
   return a.ticks_valid ? a.ticks_valid[s] : a.n_ticks;
@@ -286,7 +292,7 @@ __device__ __forceinline__ void load_window(const StagedArgs &a, long long g, in
 // ---------------------------------------------------------------------------
 template <int F>
 __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[F][kWin];
+  __shared__ __attribute__((aligned(16))) float2 W[F][kWinP];
   __shared__ BandTab T;
   __shared__ float Ly[F][kBands + 2], Exl[F][kBands + 2];
   __shared__ int sil[F], fidx[F];
@@ -323,15 +329,23 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
       for (int r = 0; r < 4; r++) win_cur[fr][r] = win_nxt[fr][r];
     __syncthreads();
     RSTAMP(1);
-    fft960_run<F>(cx.tw, W, tid);
+    fft960_run<F, kWinP>(cx.tw, W, tid);
     RSTAMP(2);
+    // X out; band-energy terms into the dead upper half of each row
     for (int idx = tid; idx < F * kFreq; idx += 256) {
       const int fr = idx / kFreq, k = idx - fr * kFreq;
-      if (fidx[fr] >= 0) a.X[(size_t)fidx[fr] * kFreq + k] = W[fr][k];
+      const float2 x = W[fr][k];
+      if (fidx[fr] >= 0) a.X[(size_t)fidx[fr] * kFreq + k] = x;
+      if (k < 400) {
+        float *tr = reinterpret_cast<float *>(W[fr]) + kTermOff;
+        band_terms(x, x, T, k, tr[k], tr[400 + k]);
+      }
     }
+    __syncthreads();
     if (tid < F * kBands) {
       const int fr = tid / kBands, b = tid - fr * kBands;
-      const float ex = band_sum_t(W[fr], W[fr], T, b);
+      const float *tr = reinterpret_cast<const float *>(W[fr]) + kTermOff;
+      const float ex = band_chain(tr, tr + 400, T, b);
       Exl[fr][b] = ex;
       if (fidx[fr] >= 0) a.Ex[(size_t)fidx[fr] * kBands + b] = ex;
       Ly[fr][b] = (float)log10(1e-2 + (double)ex);
@@ -1048,8 +1062,8 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
 // k_pspec: pitch spectrum P, Ep, normalised Exp, DCT(Exp)[0..5], feature 40
 // ---------------------------------------------------------------------------
 template <int F>
-__global__ void __launch_bounds__(256) k_pspec(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[F][kWin];
+__global__ void __launch_bounds__(256, 3) k_pspec(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 W[F][kWinP];
   __shared__ __attribute__((aligned(16))) float2 Xl[F][kFreq + 1];
   __shared__ BandTab T;
   __shared__ float Ep[F][kBands + 2], Exp[F][kBands + 2];
@@ -1084,17 +1098,49 @@ __global__ void __launch_bounds__(256) k_pspec(StagedArgs a) {
       if (fidx[fr] >= 0) Xl[fr][k] = a.X[(size_t)fidx[fr] * kFreq + k];
     }
     __syncthreads();
-    fft960_run<F>(cx.tw, W, tid);
-    for (int idx = tid; idx < F * kFreq; idx += 256) {
-      const int fr = idx / kFreq, k = idx - fr * kFreq;
-      if (fidx[fr] >= 0) a.P[(size_t)fidx[fr] * kFreq + k] = W[fr][k];
+    fft960_run<F, kWinP>(cx.tw, W, tid);
+    // P out; Ep (P.P) band terms into the dead upper half of each row, Exp
+    // (X.P) terms over the lower half once every P value has been read
+    {
+      constexpr int NI = (F * kFreq + 255) / 256;
+      float clo[NI], chi[NI];
+#pragma unroll
+      for (int u = 0; u < NI; u++) {
+        const int idx = tid + 256 * u;
+        if (idx < F * kFreq) {
+          const int fr = idx / kFreq, k = idx - fr * kFreq;
+          const float2 pv = W[fr][k];
+          if (fidx[fr] >= 0) a.P[(size_t)fidx[fr] * kFreq + k] = pv;
+          if (k < 400) {
+            float *tr = reinterpret_cast<float *>(W[fr]) + kTermOff;
+            band_terms(pv, pv, T, k, tr[k], tr[400 + k]);
+            band_terms(Xl[fr][k], pv, T, k, clo[u], chi[u]);
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < NI; u++) {
+        const int idx = tid + 256 * u;
+        if (idx < F * kFreq) {
+          const int fr = idx / kFreq, k = idx - fr * kFreq;
+          float *tr = reinterpret_cast<float *>(W[fr]);
+          if (k < 400) {
+            tr[k] = clo[u];
+            tr[400 + k] = chi[u];
+          }
+        }
+      }
     }
+    __syncthreads();
     if (tid < 2 * F * kBands) {
       const int h = tid / (F * kBands), r = tid - h * (F * kBands), fr = r / kBands, b = r - fr * kBands;
+      const float *tr = reinterpret_cast<const float *>(W[fr]) + (h == 0 ? kTermOff : 0);
+      const float v = band_chain(tr, tr + 400, T, b);
       if (h == 0)
-        Ep[fr][b] = band_sum_t(W[fr], W[fr], T, b);
+        Ep[fr][b] = v;
       else
-        Exp[fr][b] = band_sum_t(Xl[fr], W[fr], T, b);
+        Exp[fr][b] = v;
     }
     __syncthreads();
     if (tid < F * kBands) {
@@ -1544,7 +1590,7 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
 // ---------------------------------------------------------------------------
 template <int F>
 __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[F][kWin];
+  __shared__ __attribute__((aligned(16))) float2 W[F][kWinP];
   __shared__ __attribute__((aligned(16))) float2 Xl[F][kFreq + 1];
   __shared__ BandTab T;
   __shared__ float rr[F][kBands + 2], nrm[F][kBands + 2], gs[F][kBands + 2], newE[F][kBands + 2];
@@ -1582,20 +1628,29 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
       }
     }
     __syncthreads();
+    // pitch filter X += r P, and the band terms of the filtered X (into W's
+    // rows: W is free until the synthesis input is staged)
     for (int idx = tid; idx < F * kFreq; idx += 256) {
       const int fr = idx / kFreq, k = idx - fr * kFreq;
       if (fil[fr]) {
         const float rf = interp_gain_t(rr[fr], T, k);
         const float2 pk = a.P[(size_t)fidx[fr] * kFreq + k];
-        Xl[fr][k].x += rf * pk.x;
-        Xl[fr][k].y += rf * pk.y;
+        float2 xv = Xl[fr][k];
+        xv.x += rf * pk.x;
+        xv.y += rf * pk.y;
+        Xl[fr][k] = xv;
+        if (k < 400) {
+          float *tr = reinterpret_cast<float *>(W[fr]);
+          band_terms(xv, xv, T, k, tr[k], tr[400 + k]);
+        }
       }
     }
     __syncthreads();
     if (tid < F * kBands) {
       const int fr = tid / kBands, i = tid - fr * kBands;
       if (fil[fr]) {
-        newE[fr][i] = band_sum_t(Xl[fr], Xl[fr], T, i);
+        const float *tr = reinterpret_cast<const float *>(W[fr]);
+        newE[fr][i] = band_chain(tr, tr + 400, T, i);
         nrm[fr][i] = (float)sqrt((double)a.Ex[(size_t)fidx[fr] * kBands + i] / (1e-8 + (double)newE[fr][i]));
       }
     }
@@ -1632,7 +1687,7 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
       }
     }
     __syncthreads();
-    fft960_run<F>(cx.tw, W, tid);
+    fft960_run<F, kWinP>(cx.tw, W, tid);
 #pragma unroll
     for (int fr = 0; fr < F; fr++) {
       const int f = fidx[fr];
