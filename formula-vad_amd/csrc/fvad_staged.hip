@@ -32,6 +32,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "fvad_device.h"
 #include "fvad_internal.h"
@@ -149,23 +150,30 @@ __global__ void __launch_bounds__(256) k_prep2(StagedArgs a) {
     if (t < T) {
       if (wave == 0) {
         if (lane < ns && t < nts[lane]) {
-          for (int c = 0; c < C; c++) {
-            const float *x = inb[cur] + (lane * C + c) * kFrame;
-            float *y = outb[cur] + (lane * C + c) * kFrame;
+          // b*x and a*y are exact in double (24-bit x 24-bit significands), so
+          // one fma rounds b*x - a*y exactly once, as the C expression does;
+          // it shortens the serial chain by one dependent f64 operation.  The
+          // loop is specialised on raw_s16 (uniform) so no per-sample select
+          // sits in the chain wave's in-order instruction stream.
+          auto run = [&](auto scaled) {
+            for (int c = 0; c < C; c++) {
+              const float *x = inb[cur] + (lane * C + c) * kFrame;
+              float *y = outb[cur] + (lane * C + c) * kFrame;
 #pragma unroll 8
-            for (int i = 0; i < kFrame; i++) {
-              const float v0 = x[i];
-              const float xi = a.raw_s16 ? v0 : v0 * scalar;
-              const float yi = xi + mem0;
-              // b*x and a*y are exact in double (24-bit x 24-bit significands), so
-              // one fma rounds b*x - a*y exactly once, as the C expression does;
-              // it shortens the serial chain by one dependent f64 operation
-              const double yd = (double)yi;
-              mem0 = (float)((double)mem1 + __builtin_fma(-(double)a0, yd, b0 * (double)xi));
-              mem1 = (float)__builtin_fma(-(double)a1, yd, b1 * (double)xi);
-              y[i] = yi;
+              for (int i = 0; i < kFrame; i++) {
+                const float xi = decltype(scaled)::value ? x[i] * scalar : x[i];
+                const float yi = xi + mem0;
+                const double yd = (double)yi;
+                mem0 = (float)((double)mem1 + __builtin_fma(-(double)a0, yd, b0 * (double)xi));
+                mem1 = (float)__builtin_fma(-(double)a1, yd, b1 * (double)xi);
+                y[i] = yi;
+              }
             }
-          }
+          };
+          if (a.raw_s16)
+            run(std::false_type{});
+          else
+            run(std::true_type{});
         }
       } else if (wave == 1) {
         if (lane < slots) {
@@ -1600,6 +1608,7 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
   frame_ctx_load(cx, a.plan, tid);
   bandtab_load(T, a.plan, tid, 256);
   const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
+  STAMP_INIT();
   for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
     group_frames<F>(a, g, tid, fidx);
     __syncthreads();
@@ -1628,6 +1637,7 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
       }
     }
     __syncthreads();
+    RSTAMP(0);
     // pitch filter X += r P, and the band terms of the filtered X (into W's
     // rows: W is free until the synthesis input is staged)
     for (int idx = tid; idx < F * kFreq; idx += 256) {
@@ -1646,6 +1656,7 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
       }
     }
     __syncthreads();
+    RSTAMP(1);
     if (tid < F * kBands) {
       const int fr = tid / kBands, i = tid - fr * kBands;
       if (fil[fr]) {
@@ -1669,6 +1680,7 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
       }
     }
     __syncthreads();
+    RSTAMP(2);
 #pragma unroll
     for (int fr = 0; fr < F; fr++) {
 #pragma unroll
@@ -1687,6 +1699,7 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
       }
     }
     __syncthreads();
+    RSTAMP(3);
     fft960_run<F, kWinP>(cx.tw, W, tid);
 #pragma unroll
     for (int fr = 0; fr < F; fr++) {
@@ -1703,7 +1716,9 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
       }
     }
     __syncthreads();
+    RSTAMP(4);
   }
+  STAMP_FLUSH(40, 5);
 }
 
 // ---------------------------------------------------------------------------

@@ -60,3 +60,12 @@ if MODE == "staged":
     print("k_pcorr: stamped cycles per 16-frame group per WG: %.0f" % (pt / max(1, groups)))
     for i, n in enumerate(PIT):
         print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[32 + i] / max(1, pt), buf[32 + i] / groups))
+
+if MODE == "staged":
+    SYN = ["setup + X load + pitch gain r", "pitch filter + band terms", "band chains, norm, gains",
+           "Hermitian staging", "FFT + synthesis window out"]
+    groups = B * 2 * T / 4.0
+    tt = sum(buf[40:45])
+    print("k_synth: stamped cycles per 4-frame group per WG: %.0f" % (tt / max(1, groups)))
+    for i, n in enumerate(SYN):
+        print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[40 + i] / max(1, tt), buf[40 + i] / groups))
