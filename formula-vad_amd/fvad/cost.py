@@ -124,9 +124,14 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_pcorr": (pitch - plpc - 14 * 4, (864 + 147 + 10 + 29 + 1) * 4 + 80 * 4),
         "k_select": (14 * 4 + 14 * 12, 80 * 4 + 4),
         "k_pspec": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
-        "k_rnn": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"] + p["pitch filter + gains"],
-                  22 * 4 * 4 + 8 * 4 + 3 * spec + 4),
-        "k_synth": (p["synthesis (scale, FFT A, window, OLA, 1/32767)"] - 960, spec + 960 * 4),
+        # k_rnn: cepstral memory, spectral variability, GRU stack, gain
+        # smoothing; reads DCT(Ly), features 34..40, silence; writes g, smoothed g, vad
+        "k_rnn": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"],
+                  (22 + 8 + 1) * 4 + (22 + 22 + 1) * 4),
+        # k_synth: pitch filter (X + r P, band energies, norm), gains, synthesis;
+        # reads X, P, Exp, g, Ex, Ep, smoothed g, silence; writes the windowed frame
+        "k_synth": (p["pitch filter + gains"] + p["synthesis (scale, FFT A, window, OLA, 1/32767)"] - 960,
+                    2 * spec + 5 * 22 * 4 + 4 + 960 * 4),
         "k_ola": (960, 960 * 4 + 480 * 4 + 4.0 / C),
         "k_winmeta": (0.0, 4 * 4.0 / C),
         "k_fftb": (p["re-block + FFT B share"], 480 * 4 + 4),
