@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-ticks", type=int, default=200)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="measure the CPU sample for about this long")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--host-rate", action="store_true",
+                    help="also time pushes from host buffers (PCIe-inclusive; reported as host_buffers, never value)")
     return ap.parse_args()
 
 
@@ -168,6 +170,25 @@ def main():
     value = aggregate_rate(B * Ch * T, world, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
+    host = None
+    if args.host_rate:
+        # fvad_engine_push: [t][s][c][480] f32 copied from pageable host memory,
+        # outputs copied back; white-noise input (no silent frames)
+        import numpy as np
+        pcm = (np.random.default_rng(rank).standard_normal((T, B, Ch, 480), dtype=np.float32) * 0.05)
+        eng.push(pcm)
+        eng.sync()
+        barrier(dist, torch)
+        h0 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.push(pcm)
+        eng.sync()
+        barrier(dist, torch)
+        hsec = max_over_ranks(time.perf_counter() - h0, dist, torch)
+        host = {"value": aggregate_rate(B * Ch * T, world, args.steps, hsec), "unit": "frames/s",
+                "ms_per_step": round(1000.0 * hsec / args.steps, 3),
+                "input_bytes_per_step": int(pcm.nbytes), "note": "pageable host buffers, PCIe-inclusive"}
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -246,6 +267,8 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if host is not None:
+        line["host_buffers"] = host
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
