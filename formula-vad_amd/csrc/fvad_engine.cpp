@@ -813,6 +813,27 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
 }
 
 extern "C" size_t fvad_engine_segments(fvad_engine *e, int stream, int machine, fvad_segment *out, size_t cap) {
+  return fvad_engine_segments_range(e, stream, machine, 0, out, cap);
+}
+
+extern "C" int fvad_engine_vadm_state(fvad_engine *e, int stream, int machine, int *speech_state,
+                                      uint64_t *speech_start, uint64_t *speech_end) {
+  if (!e || e->vadm.n == 0 || stream < 0 || stream >= e->cfg.n_streams || machine < 0 || machine >= e->vadm.n)
+    return fail(FVAD_EINVAL, "no such attached machine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipStreamSynchronize(e->side));
+  fvad::VadmState st;
+  HIP_TRY(hipMemcpy(&st, e->vadm.st + (size_t)machine * e->cfg.n_streams + stream, sizeof(st),
+                    hipMemcpyDeviceToHost));
+  if (speech_state) *speech_state = st.state;
+  if (speech_start) *speech_start = st.speech_start;
+  if (speech_end) *speech_end = st.speech_end;
+  return FVAD_OK;
+}
+
+extern "C" size_t fvad_engine_segments_range(fvad_engine *e, int stream, int machine, size_t first,
+                                             fvad_segment *out, size_t cap) {
   if (!e || e->vadm.n == 0 || stream < 0 || stream >= e->cfg.n_streams || machine < 0 || machine >= e->vadm.n)
     return 0;
   if (hipSetDevice(e->cfg.device) != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess ||
@@ -822,10 +843,10 @@ extern "C" size_t fvad_engine_segments(fvad_engine *e, int stream, int machine, 
   fvad::VadmState st;
   if (hipMemcpy(&st, e->vadm.st + idx, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return 0;
   const size_t n = std::min<size_t>(st.n_segs, (size_t)e->vadm.seg_cap);
-  const size_t k = std::min(n, cap);
+  const size_t k = first < n ? std::min(n - first, cap) : 0;
   if (out && k) {
     std::vector<fvad::VadmSeg> tmp(k);
-    if (hipMemcpy(tmp.data(), e->vadm.seg + idx * e->vadm.seg_cap, k * sizeof(fvad::VadmSeg),
+    if (hipMemcpy(tmp.data(), e->vadm.seg + idx * e->vadm.seg_cap + first, k * sizeof(fvad::VadmSeg),
                   hipMemcpyDeviceToHost) != hipSuccess)
       return 0;
     for (size_t i = 0; i < k; i++) {

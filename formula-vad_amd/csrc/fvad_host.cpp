@@ -311,7 +311,39 @@ struct fvad_pipeline {
   uint64_t total_write_count = 0;
   TickBuffers tb;
   std::vector<float> pcm;
+  // Recorder: raw input history [hist0, total_write_count) per channel, kept
+  // from the earliest sample a capture that may still complete can start at
+  std::vector<std::vector<float>> hist;
+  uint64_t hist0 = 0;
+  fvad_recording_fn rec_fn = nullptr;
+  void *rec_ctx = nullptr;
+  size_t rec_done = 0;  // main-machine segments already handed to rec_fn
 };
+
+namespace {
+// AudioPipeline's ring holds 10 s (AudioPipeline.zig:45); a capture starts
+// 2 s before its speech start (VADMachine.getOffsetRecordingStart), and a
+// closed machine's next speech start lies within the last window's latency
+constexpr uint64_t kRecKeep = 48000 * 10;
+constexpr uint64_t kRecMargin = 48000 * 2;
+}  // namespace
+
+extern "C" int fvad_recording_channel(const float *const *pcm, int n_channels, size_t n) {
+  if (!pcm || n_channels < 1) return FVAD_EINVAL;
+  int best = 0;
+  float best_vol = 9999;
+  for (int c = 0; c < n_channels; c++) {
+    float sum = 0.0f;
+    for (size_t i = 0; i < n; i++) sum += pcm[c][i] * pcm[c][i];
+    const float mean = sum / (float)n;
+    const float vol = std::sqrt(mean);
+    if (vol < best_vol) {
+      best = c;
+      best_vol = vol;
+    }
+  }
+  return best;
+}
 
 extern "C" int fvad_pipeline_create(int sample_rate, int n_channels, const fvad_model *model, int device,
                                     const fvad_vadm_config *main_cfg, const fvad_vadm_config *alt_cfgs, int n_alt,
@@ -353,11 +385,59 @@ extern "C" void fvad_pipeline_destroy(fvad_pipeline *p) {
   delete p;
 }
 
+namespace {
+// Recordings of the main machine's newly completed segments, then trim the
+// history (AudioPipeline.maybeRecordBuffer / Recorder.finalize, keep = true)
+int record_segments(fvad_pipeline *p) {
+  const int C = p->n_channels;
+  const size_t total = fvad_engine_segments_range(p->engine, 0, 0, p->rec_done, nullptr, 0);
+  if (total > p->rec_done) {
+    std::vector<fvad_segment> segs(total - p->rec_done);
+    const size_t k = std::min(segs.size(), (size_t)kPipelineSegCap > p->rec_done ? (size_t)kPipelineSegCap - p->rec_done : 0);
+    fvad_engine_segments_range(p->engine, 0, 0, p->rec_done, segs.data(), k);
+    std::vector<const float *> ch(C);
+    for (size_t i = 0; i < k; i++) {
+      const uint64_t from = segs[i].sample_from, to = segs[i].sample_to;
+      if (from < p->hist0 || to > p->hist0 + p->hist[0].size() || to <= from) continue;  // not retained
+      for (int c = 0; c < C; c++) ch[c] = p->hist[c].data() + (from - p->hist0);
+      const size_t len = (size_t)(to - from);
+      const int best = fvad_recording_channel(ch.data(), C, len);
+      p->rec_fn(p->rec_ctx, ch[best], len, from, best);
+    }
+    p->rec_done = total;
+  }
+  int state = 0;
+  uint64_t speech_start = 0;
+  int rc = fvad_engine_vadm_state(p->engine, 0, 0, &state, &speech_start, nullptr);
+  if (rc) return rc;
+  uint64_t keep_from = p->total_write_count > kRecKeep ? p->total_write_count - kRecKeep : 0;
+  if (state != 0) keep_from = std::min(keep_from, speech_start > kRecMargin ? speech_start - kRecMargin : 0);
+  if (keep_from > p->hist0) {
+    const size_t drop = (size_t)std::min<uint64_t>(keep_from - p->hist0, p->hist[0].size());
+    for (int c = 0; c < C; c++) p->hist[c].erase(p->hist[c].begin(), p->hist[c].begin() + drop);
+    p->hist0 += drop;
+  }
+  return FVAD_OK;
+}
+}  // namespace
+
+extern "C" int fvad_pipeline_set_recorder(fvad_pipeline *p, fvad_recording_fn fn, void *ctx) {
+  if (!p) return FVAD_EINVAL;
+  p->rec_fn = fn;
+  p->rec_ctx = ctx;
+  p->hist.assign(p->n_channels, {});
+  p->hist0 = p->total_write_count;
+  p->rec_done = fn ? fvad_engine_segments_range(p->engine, 0, 0, 0, nullptr, 0) : 0;
+  return FVAD_OK;
+}
+
 extern "C" int fvad_pipeline_push(fvad_pipeline *p, const float *const *pcm, size_t n, uint64_t *first_index) {
   if (!p || (!pcm && n)) return FVAD_EINVAL;
   if (first_index) *first_index = p->total_write_count;
   const int C = p->n_channels;
   for (int c = 0; c < C; c++) p->pending[c].insert(p->pending[c].end(), pcm[c], pcm[c] + n);
+  if (p->rec_fn)
+    for (int c = 0; c < C; c++) p->hist[c].insert(p->hist[c].end(), pcm[c], pcm[c] + n);
   p->total_write_count += n;
   size_t avail = p->pending[0].size() / fvad::kFrame;
   size_t consumed = 0;
@@ -374,7 +454,7 @@ extern "C" int fvad_pipeline_push(fvad_pipeline *p, const float *const *pcm, siz
     avail -= nt;
   }
   for (int c = 0; c < C; c++) p->pending[c].erase(p->pending[c].begin(), p->pending[c].begin() + consumed);
-  return FVAD_OK;
+  return p->rec_fn ? record_segments(p) : FVAD_OK;
 }
 
 extern "C" size_t fvad_pipeline_segments(const fvad_pipeline *p, int alt, fvad_segment *out, size_t cap) {

@@ -190,6 +190,33 @@ void make_path(const std::string &p) {
   }
 }
 
+// Mono 32-bit float WAV (AudioBuffer.Format.wav = SF_FORMAT_WAV | SF_FORMAT_FLOAT,
+// AudioBuffer.zig:11-13): the recordings' container here (the reference saves
+// them as ogg/vorbis, which is out of scope)
+bool write_wav_f32(const std::string &path, const float *x, size_t n, int sample_rate) {
+  std::string h;
+  auto u32 = [&](uint32_t v) { h.append(reinterpret_cast<const char *>(&v), 4); };
+  auto u16 = [&](uint16_t v) { h.append(reinterpret_cast<const char *>(&v), 2); };
+  const uint32_t data_bytes = (uint32_t)(n * 4);
+  h += "RIFF";
+  u32(4 + (8 + 16) + (8 + 4) + (8 + data_bytes));
+  h += "WAVEfmt ";
+  u32(16);
+  u16(3);  // WAVE_FORMAT_IEEE_FLOAT
+  u16(1);
+  u32((uint32_t)sample_rate);
+  u32((uint32_t)sample_rate * 4);
+  u16(4);
+  u16(32);
+  h += "fact";
+  u32(4);
+  u32((uint32_t)n);
+  h += "data";
+  u32(data_bytes);
+  h.append(reinterpret_cast<const char *>(x), n * 4);
+  return write_file(path, h);
+}
+
 // ---------------- WAV ingest (AudioFileStream replacement) ----------------
 struct Audio {
   int channels = 0, sample_rate = 0;
@@ -458,6 +485,25 @@ extern "C" int fvad_simulator_main(int argc, char **argv) {
       fvad_multi_segments(multi, (int)k, inst[k].segs.data(), n);
     }
     fvad_multi_destroy(multi);
+    // on_recording (SimulationInstance.zig:28-58): the Recorder's capture of
+    // every completed segment -- raw input of [sample_from, sample_to) on the
+    // lowest-RMS channel (Recorder.zig:95-146) -- saved as NNN-<name>.wav
+    if (!out_dir.empty()) {
+      for (auto &I : inst) {
+        size_t count = 0;
+        std::vector<const float *> ch(channels);
+        for (auto &sg : I.segs) {
+          if (sg.sample_to > I.audio.n || sg.sample_to <= sg.sample_from) continue;
+          const size_t len = (size_t)(sg.sample_to - sg.sample_from);
+          for (int c = 0; c < channels; c++) ch[c] = I.audio.planar.data() + (size_t)c * I.audio.n + sg.sample_from;
+          const int best = fvad_recording_channel(ch.data(), channels, len);
+          char nm[32];
+          std::snprintf(nm, sizeof nm, "%03zu-", count++);
+          if (!write_wav_f32(join(out_dir, std::string(nm) + I.name + ".wav"), ch[best], len, 48000))
+            std::fprintf(stderr, "error(sim_instance): Failed to save recording %s%s.wav\n", nm, I.name.c_str());
+        }
+      }
+    }
   }
   fvad_model_free(model);
 

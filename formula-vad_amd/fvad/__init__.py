@@ -124,6 +124,9 @@ SYMBOLS = [
     ("fvad_engine_kernel_name", C.c_char_p, [C.c_void_p, C.c_int]),
     ("fvad_engine_attach_vadm", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     ("fvad_engine_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
+    ("fvad_engine_segments_range", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_size_t]),
+    ("fvad_engine_vadm_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint64)]),
     ("fvad_engine_clear_times", C.c_int, [C.c_void_p]),
     ("fvad_engine_fetch", C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     ("fvad_vadm_config_default", None, [C.c_void_p]),
@@ -137,6 +140,8 @@ SYMBOLS = [
     ("fvad_pipeline_destroy", None, [C.c_void_p]),
     ("fvad_pipeline_push", C.c_int, [C.c_void_p, C.POINTER(F32P), C.c_size_t, C.POINTER(C.c_uint64)]),
     ("fvad_pipeline_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    ("fvad_recording_channel", C.c_int, [C.POINTER(F32P), C.c_int, C.c_size_t]),
+    ("fvad_pipeline_set_recorder", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fvad_multi_create", C.c_int, [C.c_int, C.c_int, C.c_void_p, I32P, C.c_int, C.c_void_p, C.c_int,
                                     C.POINTER(C.c_void_p)]),
     ("fvad_multi_destroy", None, [C.c_void_p]),
@@ -398,6 +403,17 @@ class VADMachine:
             pass
 
 
+# on_recording callback (fvad_recording_fn)
+RECORDING_FN = C.CFUNCTYPE(None, C.c_void_p, F32P, C.c_size_t, C.c_uint64, C.c_int)
+
+
+def recording_channel(channel_pcm):
+    """Recorder.findBestChannel: index of the lowest-rmsVolume channel."""
+    chans = [np.ascontiguousarray(c, np.float32) for c in channel_pcm]
+    arr = (F32P * len(chans))(*[fptr(c) for c in chans])
+    return lib().fvad_recording_channel(arr, len(chans), len(chans[0]))
+
+
 class AudioPipeline:
     """src/AudioPipeline.zig for one stream (pushSamples -> VAD -> VADMachine)."""
 
@@ -418,6 +434,18 @@ class AudioPipeline:
         first = C.c_uint64()
         _check(lib().fvad_pipeline_push(self.h, arr, len(chans[0]), C.byref(first)), "fvad_pipeline_push")
         return first.value
+
+    def record(self):
+        """Attach the Recorder: completed main-machine segments are captured
+        into self.recordings as (start_sample, channel, pcm) (on_recording)."""
+        self.recordings = []
+
+        def on_rec(ctx, pcm, n, start, channel):
+            self.recordings.append((int(start), int(channel), np.ctypeslib.as_array(pcm, shape=(n,)).copy()))
+
+        self._rec_cb = RECORDING_FN(on_rec)
+        _check(lib().fvad_pipeline_set_recorder(self.h, C.cast(self._rec_cb, C.c_void_p), None),
+               "fvad_pipeline_set_recorder")
 
     def segments(self, alt=-1):
         n = lib().fvad_pipeline_segments(self.h, alt, None, 0)

@@ -204,6 +204,13 @@ size_t fvad_vadm_segments(const fvad_vadm *v, fvad_segment *out, size_t cap);
 int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *cfgs, int n, int seg_capacity);
 /* total segments of (stream, machine) so far; copies min(total, capacity, cap) */
 size_t fvad_engine_segments(fvad_engine *e, int stream, int machine, fvad_segment *out, size_t cap);
+/* the same from segment index `first` on (returns the total count) */
+size_t fvad_engine_segments_range(fvad_engine *e, int stream, int machine, size_t first, fvad_segment *out,
+                                  size_t cap);
+/* speech state of an attached machine (VADMachine.zig:11-16: 0 closed, 1 opening,
+ * 2 open, 3 closing) and its current speech start / end sample indices */
+int fvad_engine_vadm_state(fvad_engine *e, int stream, int machine, int *speech_state, uint64_t *speech_start,
+                           uint64_t *speech_end);
 
 /* AudioPipeline (AudioPipeline.zig:20-26,39-120) for one stream, backed by a
  * 1-stream engine.  n_alt alternative VADMachine configs (VAD.zig:20-23). */
@@ -217,6 +224,17 @@ void fvad_pipeline_destroy(fvad_pipeline *p);
 int fvad_pipeline_push(fvad_pipeline *p, const float *const *channel_pcm, size_t n, uint64_t *first_index);
 /* vad_segments of the main (alt < 0) or an alternative machine */
 size_t fvad_pipeline_segments(const fvad_pipeline *p, int alt, fvad_segment *out, size_t cap);
+
+/* Recorder (Recorder.zig:95-110 findBestChannel): the channel with the lowest
+ * rmsVolume (audio_utils.zig:14-24) over n samples; the first one on ties. */
+int fvad_recording_channel(const float *const *channel_pcm, int n_channels, size_t n);
+/* on_recording (AudioPipeline.zig:15-18, :134-195, Recorder.zig:52-146): called
+ * from fvad_pipeline_push once per completed main-machine segment with the raw
+ * pushed input of [sample_from, sample_to) on its lowest-RMS channel
+ * (AudioBuffer: one channel, global_start_frame_number = start_sample).
+ * fn = NULL detaches; only segments completed after attaching are recorded. */
+typedef void (*fvad_recording_fn)(void *ctx, const float *pcm, size_t n, uint64_t start_sample, int channel);
+int fvad_pipeline_set_recorder(fvad_pipeline *p, fvad_recording_fn fn, void *ctx);
 
 /* Multi-stream simulator core: n streams processed in lockstep on the given
  * devices (one engine per device, streams partitioned contiguously).

@@ -395,3 +395,18 @@ float ora_rms_volume(const float *x, int n) {
   for (i = 0; i < n; i++) sum += x[i] * x[i];
   return sqrtf(sum / (float)n);
 }
+
+/* Recorder.findBestChannel (Recorder.zig:95-110): the lowest rmsVolume, first
+ * on ties (strict <, starting from 9999) */
+int ora_recording_channel(const float *const *ch, int n_channels, int n) {
+  int best = 0, c;
+  float best_vol = 9999;
+  for (c = 0; c < n_channels; c++) {
+    const float vol = ora_rms_volume(ch[c], n);
+    if (vol < best_vol) {
+      best = c;
+      best_vol = vol;
+    }
+  }
+  return best;
+}

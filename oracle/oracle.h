@@ -97,6 +97,7 @@ float ora_window_norm_factor(const float *w, int n);
 /* FFT.fft: magnitude spectrum (n/2+1 bins) of samples*window, normalised */
 int ora_fftzig(int nfft, const float *samples, const float *window, float *mag);
 float ora_rms_volume(const float *x, int n);
+int ora_recording_channel(const float *const *ch, int n_channels, int n); /* Recorder.zig:95-110 */
 
 /* ---------------- reference unit-test restatements ---------------- */
 /* SegmentWriter.write on a 1-channel segment with (first, second) split source */

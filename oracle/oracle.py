@@ -54,6 +54,8 @@ def lib():
         L.ora_fftzig.argtypes = [C.c_int, F32P, F32P, F32P]
         L.ora_rms_volume.restype = C.c_float
         L.ora_rms_volume.argtypes = [F32P, C.c_int]
+        L.ora_recording_channel.restype = C.c_int
+        L.ora_recording_channel.argtypes = [C.POINTER(F32P), C.c_int, C.c_int]
         L.ora_segwriter_write.restype = C.c_size_t
         L.ora_segwriter_write.argtypes = [C.c_void_p, F32P, C.c_size_t, F32P, C.c_size_t, C.c_size_t, C.c_long]
         L.ora_ring_write.restype = C.c_size_t
@@ -243,6 +245,29 @@ def fftzig(samples, window):
 def rms_volume(x):
     x = np.ascontiguousarray(x, np.float32)
     return lib().ora_rms_volume(fptr(x), len(x))
+
+
+def recording_channel(channel_pcm):
+    """Recorder.findBestChannel (Recorder.zig:95-110)."""
+    chans = [np.ascontiguousarray(c, np.float32) for c in channel_pcm]
+    arr = (F32P * len(chans))(*[fptr(c) for c in chans])
+    return lib().ora_recording_channel(arr, len(chans), len(chans[0]))
+
+
+def recordings(channel_pcm, segments):
+    """What AudioPipeline's Recorder hands to on_recording (AudioPipeline.zig:
+    134-195, Recorder.zig:52-146): for each completed main-machine segment
+    (sample_from, sample_to, ...) -- whose bounds are VADMachine's
+    getOffsetRecordingStart/End, the capture's start and finalize sample -- the
+    pushed input of [sample_from, sample_to) on its lowest-RMS channel, as
+    (start_sample, channel, pcm)."""
+    out = []
+    for seg in segments:
+        a, b = int(seg[0]), int(seg[1])
+        sl = [np.ascontiguousarray(c[a:b], np.float32) for c in channel_pcm]
+        ch = recording_channel(sl)
+        out.append((a, ch, sl[ch].copy()))
+    return out
 
 
 class Pipeline:

@@ -75,6 +75,33 @@ def test_simulator_plan(fvad_mod, oracle_mod, tmp_path):
     assert len(outdirs) == 1
     files = sorted(f.name for f in outdirs[0].iterdir())
     assert "report.txt" in files and "plan.json" in files and "drv0-audacity.txt" in files
+    # Recorder: one mono float WAV per completed segment, NNN-<name>.wav, equal
+    # to the oracle's capture (raw input of the segment on its lowest-RMS channel)
+    n_rec = 0
+    for inst in out["instances"]:
+        x, _ = truth[inst["name"]]
+        exp = oracle_mod.recordings([x[0], x[1]], [tuple(sg) for sg in inst["segments"]])
+        for k, (start, ch, pcm) in enumerate(exp):
+            got = read_wav_f32(outdirs[0] / ("%03d-%s.wav" % (k, inst["name"])))
+            assert np.array_equal(got, pcm), (inst["name"], k)
+            n_rec += 1
+        assert not (outdirs[0] / ("%03d-%s.wav" % (len(exp), inst["name"]))).exists()
+    assert n_rec > 0
+
+
+def read_wav_f32(path):
+    b = open(path, "rb").read()
+    assert b[:4] == b"RIFF" and b[8:12] == b"WAVE"
+    pos, fmt, data = 12, None, None
+    while pos + 8 <= len(b):
+        cid, sz = b[pos:pos + 4], struct.unpack("<I", b[pos + 4:pos + 8])[0]
+        if cid == b"fmt ":
+            fmt = struct.unpack("<HHIIHH", b[pos + 8:pos + 24])
+        elif cid == b"data":
+            data = b[pos + 8:pos + 8 + sz]
+        pos += 8 + sz
+    assert fmt[0] == 3 and fmt[1] == 1 and fmt[2] == 48000 and fmt[5] == 32
+    return np.frombuffer(data, "<f4")
 
 
 def test_simulator_bad_plan(tmp_path):
