@@ -102,7 +102,8 @@ struct fvad_engine {
   int n_timed = 0;
   bool timing_pending = false;  // unused (kept for layout clarity)
   int raw_s16 = 0;  // rnnoise compat mode (s16-scaled I/O)
-  unsigned long long *d_stamps = nullptr;  // diagnostic stamp buffer (FVAD_STAMPS builds)
+  unsigned long long *d_stamps = nullptr;
+  unsigned *d_work = nullptr;  // staged: persistent-kernel group counters  // diagnostic stamp buffer (FVAD_STAMPS builds)
 };
 
 // Diagnostic builds: per-phase cycle totals of k_frame (thread 0 of every workgroup).
@@ -240,7 +241,7 @@ void free_all(fvad_engine *e) {
   void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm,   e->d_xbuf, e->d_ratio,
                   e->d_vad,  e->d_wratio,  e->d_wvad,  e->d_band, e->d_den,   e->d_wflag, e->d_ticks,
                   e->d_model, e->d_stamps, e->d_xs,    e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
-                  e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_vadf,  e->d_ys,    e->d_sil,
+                  e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->vadm.st, e->vadm.buf,
                   e->vadm.seg, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband};
   for (void *p : ptrs)
@@ -352,7 +353,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
         (rc = dalloc(&e->d_P, F * fvad::kFreq * 2)) || (rc = dalloc(&e->d_Ex, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Ep, F * fvad::kBands)) || (rc = dalloc(&e->d_Exp, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Lyf, F * fvad::kBands)) || (rc = dalloc(&e->d_f34, F * 8)) ||
-        (rc = dalloc(&e->d_rec, F * fvad::kPitchRecord)) ||
+        (rc = dalloc(&e->d_rec, F * fvad::kPitchRecord)) || (rc = dalloc(&e->d_work, (size_t)fvad::kWorkCounters)) ||
         (rc = dalloc(&e->d_ptile, (B + fvad::ptile::kTile - 1) / fvad::ptile::kTile * e->V * fvad::ptile::kTile *
                                       fvad::ptile::kRows)) || (rc = dalloc(&e->d_vadf, F)) ||
         (rc = dalloc(&e->d_ys, F * fvad::kWin)) || (rc = dalloc(&e->d_sil, F)) || (rc = dalloc(&e->d_pitch, F)) ||
@@ -458,6 +459,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.silence = e->d_sil;
   a.rec = e->d_rec;
   a.ptile = e->d_ptile;
+  a.work = e->d_work;
   a.pitch = e->d_pitch;
   a.vadf = e->d_vadf;
   a.gr = e->d_gr;

@@ -10,6 +10,7 @@
 namespace fvad {
 
 constexpr int kStagedKernels = 11;
+constexpr int kWorkCounters = 64;  // persistent-kernel queues (fvad_staged.hip: take_group)
 constexpr int kPitchRecord = 80;  // floats per frame of the pitch record (k_pcorr -> k_select)
 
 // Pitch tile buffer (k_plpc -> k_pcorr): a tile is 64 streams at one frame
@@ -92,6 +93,7 @@ struct StagedArgs {
   int *out_win_flag;
   int raw_s16;
   VadmArgs vadm;
+  unsigned *work;          // [kWorkCounters] dynamic group counters of the persistent kernels
   unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn
 };
 

@@ -86,6 +86,20 @@ __device__ __forceinline__ int ticks_of(const StagedArgs &a, int s) {
   return a.ticks_valid ? a.ticks_valid[s] : a.n_ticks;
 }
 
+// Dynamic group scheduling of the persistent kernels: a workgroup takes the
+// index of its next group from one of 8 queues (queue x serves groups x,
+// x + 8, x + 16, ... and the workgroups with blockIdx % 8 == x, i.e. one XCD's
+// under round-robin dispatch, which keeps each counter's atomics local and
+// few).  A workgroup that starts late -- beside another kernel's waves --
+// just takes fewer groups instead of stretching the launch with a tail.
+// The counters a.work[slot][8] are zeroed on the stream before every launch.
+constexpr int kQueues = 8;
+enum WorkSlot { kWorkFftA = 0, kWorkPlpc, kWorkPcorr, kWorkPspec, kWorkSynth, kWorkSlots };
+__device__ __forceinline__ long long take_group(const StagedArgs &a, int slot) {
+  const int x = blockIdx.x % kQueues;
+  return x + (long long)kQueues * atomicAdd(&a.work[slot * kQueues + x], 1u);
+}
+
 // analysis / synthesis window value for index i of the 960-sample window
 __device__ __forceinline__ float win960(const float *__restrict__ hw, int i) {
   return (i < kFrame) ? hw[i] : hw[kWin - 1 - i];
@@ -310,12 +324,20 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
   bandtab_load(T, a.plan, tid, 256);
   const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
   STAMP_INIT();
+  __shared__ long long gq;
+  if (tid == 0) gq = take_group(a, kWorkFftA);
+  __syncthreads();
+  long long g = gq;
+  __syncthreads();
+  if (tid == 0) gq = take_group(a, kWorkFftA);
   float win_cur[F][4];
-  if (blockIdx.x < ngroups) load_window<F>(a, blockIdx.x, tid, cx, win_cur);
-  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  if (g < ngroups) load_window<F>(a, g, tid, cx, win_cur);
+  __syncthreads();
+  long long gn = gq;  // the group after g (its window is prefetched)
+  while (g < ngroups) {
     group_frames<F>(a, g, tid, fidx);
     float win_nxt[F][4];
-    if (g + gridDim.x < ngroups) load_window<F>(a, g + gridDim.x, tid, cx, win_nxt);
+    if (gn < ngroups) load_window<F>(a, gn, tid, cx, win_nxt);
     __syncthreads();
     RSTAMP(0);
 #pragma unroll
@@ -390,8 +412,11 @@ __global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
         a.Lyf[(size_t)fidx[fr] * kBands + b] = val;
       }
     }
+    if (tid == 0 && gn < ngroups) gq = take_group(a, kWorkFftA);
     __syncthreads();
     RSTAMP(5);
+    g = gn;
+    gn = (g < ngroups) ? gq : ngroups;
   }
   STAMP_FLUSH(16, 6);
 }
@@ -603,7 +628,22 @@ __global__ void __launch_bounds__(256, 2) k_plpc(StagedArgs a) {
   const int Vr = a.n_ticks * a.n_channels;
   const int n_sb = (a.n_streams + 63) >> 6;
   const long long n_tiles = (long long)n_sb * Vr;
-  for (long long t = (long long)blockIdx.x * 4 + w; t < n_tiles; t += (long long)gridDim.x * 4) {
+  // a workgroup takes 4 consecutive tiles (one per wave: neighbouring frame
+  // positions of the same streams share pitch-buffer samples in L2)
+  const long long n_quads = (n_tiles + 3) / 4;
+  __shared__ long long gq;
+  if (tid == 0) gq = take_group(a, kWorkPlpc);
+  __syncthreads();
+  long long q = gq;
+  while (q < n_quads) {
+    const long long t = q * 4 + w;
+    if (t >= n_tiles) {
+      __syncthreads();
+      if (tid == 0) gq = take_group(a, kWorkPlpc);
+      __syncthreads();
+      q = gq;
+      continue;
+    }
     const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
     LpSrc src;
 #pragma unroll
@@ -730,6 +770,10 @@ __global__ void __launch_bounds__(256, 2) k_plpc(StagedArgs a) {
         yb[u] = nb[u];
       }
     }
+    __syncthreads();
+    if (tid == 0) gq = take_group(a, kWorkPlpc);
+    __syncthreads();
+    q = gq;
   }
 }
 
@@ -762,7 +806,11 @@ __global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
   const int n_sb = (a.n_streams + 63) >> 6;
   const long long ngroups = (long long)n_sb * Vr * 4;
   STAMP_INIT();
-  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  __shared__ long long gq;
+  if (threadIdx.x == 0) gq = take_group(a, kWorkPcorr);
+  __syncthreads();
+  long long g = gq;
+  while (g < ngroups) {
     const long long t = g >> 2;
     const int q = (int)(g & 3);
     const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
@@ -975,8 +1023,10 @@ __global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
         }
       }
     }
+    if (tid == 0) gq = take_group(a, kWorkPcorr);
     __syncthreads();
     RSTAMP(5);
+    g = gq;
   }
   STAMP_FLUSH(32, 6);
 }
@@ -1081,7 +1131,11 @@ __global__ void __launch_bounds__(256, 3) k_pspec(StagedArgs a) {
   frame_ctx_load(cx, a.plan, tid);
   bandtab_load(T, a.plan, tid, 256);
   const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
-  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  __shared__ long long gq;
+  if (threadIdx.x == 0) gq = take_group(a, kWorkPspec);
+  __syncthreads();
+  long long g = gq;
+  while (g < ngroups) {
     group_frames<F>(a, g, tid, fidx);
     __syncthreads();
     if (tid < F) pit[tid] = fidx[tid] >= 0 ? a.pitch[fidx[tid]] : 0;
@@ -1178,7 +1232,9 @@ __global__ void __launch_bounds__(256, 3) k_pspec(StagedArgs a) {
         a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pit[fr] - 300));
       }
     }
+    if (tid == 0) gq = take_group(a, kWorkPspec);
     __syncthreads();
+    g = gq;
   }
 }
 
@@ -1609,7 +1665,11 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
   bandtab_load(T, a.plan, tid, 256);
   const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
   STAMP_INIT();
-  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  __shared__ long long gq;
+  if (threadIdx.x == 0) gq = take_group(a, kWorkSynth);
+  __syncthreads();
+  long long g = gq;
+  while (g < ngroups) {
     group_frames<F>(a, g, tid, fidx);
     __syncthreads();
     if (tid < F) fil[tid] = fidx[tid] >= 0 && !a.silence[fidx[tid]];  // silent frames: X passes through
@@ -1715,8 +1775,10 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
         }
       }
     }
+    if (tid == 0) gq = take_group(a, kWorkSynth);
     __syncthreads();
     RSTAMP(4);
+    g = gq;
   }
   STAMP_FLUSH(40, 5);
 }
@@ -2140,6 +2202,8 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   const long long frames = (long long)a.n_streams * a.V;
   auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
   (void)hipGetLastError();
+  static_assert(kWorkSlots * kQueues <= kWorkCounters, "work counters");
+  (void)hipMemsetAsync(a.work, 0, kWorkSlots * kQueues * sizeof(unsigned), stream);
   auto rec = [&](int k) {
     if (ev) (void)hipEventRecord(ev[k], stream);
   };
