@@ -73,7 +73,17 @@ struct fvad_engine {
   // k_vadm runs on a side stream over copies of one push's window outputs,
   // overlapped with the next push (it only depends on its own state)
   hipStream_t side = nullptr;
-  hipStream_t aux = nullptr;  // staged mode: k_fftA concurrent with the pitch branch
+  hipStream_t aux = nullptr;  // staged mode: k_fftA concurrent with the pitch branch (FVAD_FORK)
+  // staged mode: k_prep3 runs on pstream, so push k's prep overlaps push k-1's
+  // kernels; xs / ratio / ticks are double-buffered (d_xs, d_ratio, d_ticks
+  // alias the buffer of the latest push), buffer b is reused once the push that
+  // used it last has finished (ev_buf_free[b])
+  hipStream_t pstream = nullptr;
+  float *d_xs_b[2] = {}, *d_ratio_b[2] = {};
+  int *d_ticks_b[2] = {};
+  hipEvent_t ev_prep_done[2] = {}, ev_buf_free[2] = {};
+  bool buf_busy[2] = {false, false};
+  int next_buf = 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int n_events = 0;           // timing events per launch
   int last_event = 0;         // the one recorded last (the launch's end)
@@ -238,9 +248,10 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
 }
 
 void free_all(fvad_engine *e) {
-  void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm,   e->d_xbuf, e->d_ratio,
-                  e->d_vad,  e->d_wratio,  e->d_wvad,  e->d_band, e->d_den,   e->d_wflag, e->d_ticks,
-                  e->d_model, e->d_stamps, e->d_xs,    e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
+  void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm,   e->d_xbuf, e->d_ratio_b[0],
+                  e->d_ratio_b[1], e->d_ticks_b[0], e->d_ticks_b[1], e->d_xs_b[0], e->d_xs_b[1],
+                  e->d_vad,  e->d_wratio,  e->d_wvad,  e->d_band, e->d_den,   e->d_wflag,
+                  e->d_model, e->d_stamps, e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->vadm.st, e->vadm.buf,
                   e->vadm.seg, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband};
@@ -254,6 +265,11 @@ void free_all(fvad_engine *e) {
     if (ev) (void)hipEventDestroy(ev);
   if (e->side) (void)hipStreamDestroy(e->side);
   if (e->aux) (void)hipStreamDestroy(e->aux);
+  if (e->pstream) (void)hipStreamDestroy(e->pstream);
+  for (auto &ev : e->ev_prep_done)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto &ev : e->ev_buf_free)
+    if (ev) (void)hipEventDestroy(ev);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -266,6 +282,7 @@ int vadm_reset(fvad_engine *e);
 extern "C" int fvad_engine_reset(fvad_engine *e) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (e->pstream) HIP_TRY(hipStreamSynchronize(e->pstream));
   if (e->vadm.n > 0) {
     HIP_TRY(hipStreamSynchronize(e->side));
     const int rc = vadm_reset(e);
@@ -321,7 +338,12 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   if (c.mode == FVAD_MODE_STAGED &&
       (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
-       hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess))
+       hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess ||
+       hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_prep_done[0], hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_prep_done[1], hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_buf_free[0], hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_buf_free[1], hipEventDisableTiming) != hipSuccess))
     return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
   for (int i = 0; i < e->n_events; i++)
     if (hipEventCreate(&e->evs[0][i]) != hipSuccess || hipEventCreate(&e->evs[1][i]) != hipSuccess)
@@ -337,11 +359,13 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t frames = T * B * C * fvad::kFrame;
   if ((rc = dalloc(&e->d_state, B * fvad::st::kWords)) || (rc = dalloc(&e->d_ring, B * C * e->ring_len)) ||
-      (rc = dalloc(&e->d_pcm, frames)) || (rc = dalloc(&e->d_ratio, T * B)) ||
+      (rc = dalloc(&e->d_pcm, frames)) || (rc = dalloc(&e->d_ratio_b[0], T * B)) ||
       (rc = dalloc(&e->d_vad, T * B)) || (rc = dalloc(&e->d_wratio, T * B)) || (rc = dalloc(&e->d_wvad, T * B)) ||
       (rc = dalloc(&e->d_wflag, T * B)) || (rc = dalloc(&e->d_band, T * B * C * c.n_bands)) ||
-      (rc = dalloc(&e->d_ticks, B)) || (c.want_denoised && (rc = dalloc(&e->d_den, frames))))
+      (rc = dalloc(&e->d_ticks_b[0], B)) || (c.want_denoised && (rc = dalloc(&e->d_den, frames))))
     return bail(rc);
+  e->d_ratio = e->d_ratio_b[0];
+  e->d_ticks = e->d_ticks_b[0];
   if (c.mode == FVAD_MODE_FUSED) {
     if ((rc = dalloc(&e->d_xbuf, frames))) return bail(rc);
   } else {
@@ -349,7 +373,8 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     e->L = (fvad::kPitchBuf - fvad::kFrame) + e->V * fvad::kFrame;
     e->wmax = (int)(T * fvad::kFrame / c.fft_size) + 2;
     const size_t F = B * e->V;
-    if ((rc = dalloc(&e->d_xs, B * e->L)) || (rc = dalloc(&e->d_X, F * fvad::kFreq * 2)) ||
+    if ((rc = dalloc(&e->d_xs_b[0], B * e->L)) || (rc = dalloc(&e->d_xs_b[1], B * e->L)) ||
+        (rc = dalloc(&e->d_ratio_b[1], T * B)) || (rc = dalloc(&e->d_ticks_b[1], B)) || (rc = dalloc(&e->d_X, F * fvad::kFreq * 2)) ||
         (rc = dalloc(&e->d_P, F * fvad::kFreq * 2)) || (rc = dalloc(&e->d_Ex, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Ep, F * fvad::kBands)) || (rc = dalloc(&e->d_Exp, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Lyf, F * fvad::kBands)) || (rc = dalloc(&e->d_f34, F * 8)) ||
@@ -360,6 +385,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
         (rc = dalloc(&e->d_wtick, B * e->wmax)) || (rc = dalloc(&e->d_wstart, B * e->wmax)) ||
         (rc = dalloc(&e->d_gr, F * fvad::kBands)) || (rc = dalloc(&e->d_gs, F * fvad::kBands)))
       return bail(rc);
+    e->d_xs = e->d_xs_b[0];
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "device query failed"));
     e->grid_frames = prop.multiProcessorCount;  // CUs; persistent grids are sized per kernel
@@ -372,6 +398,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
 extern "C" void fvad_engine_destroy(fvad_engine *e) {
   if (!e) return;
   (void)hipSetDevice(e->cfg.device);
+  if (e->pstream) (void)hipStreamSynchronize(e->pstream);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->side) (void)hipStreamSynchronize(e->side);
   free_all(e);
@@ -444,6 +471,13 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.n_ticks = n_ticks;
   a.V = e->V;
   a.L = e->L;
+  // push k uses buffer b = k & 1 of xs / ratio / ticks; its k_prep3 waits
+  // (on pstream) until push k-2 released b, then runs beside push k-1
+  const int b = e->next_buf;
+  if (e->buf_busy[b]) HIP_TRY(hipStreamWaitEvent(e->pstream, e->ev_buf_free[b], 0));
+  e->d_xs = e->d_xs_b[b];
+  e->d_ratio = e->d_ratio_b[b];
+  e->d_ticks = e->d_ticks_b[b];
   a.ticks_valid = use_ticks ? e->d_ticks : nullptr;
   a.pcm = e->d_pcm;
   a.xs = e->d_xs;
@@ -493,6 +527,9 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
     return v && atoi(v) == 1;
   }();
   const fvad::StagedStreams st{e->stream, fork ? e->aux : e->stream, e->ev_fork, e->ev_join};
+  HIP_TRY(fvad::launch_prep(a, e->pstream, timed ? e->ev : nullptr));
+  HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
+  HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
   HIP_TRY(fvad::launch_staged(a, e->grid_frames, st, timed ? e->ev : nullptr));
   if (e->vadm.n > 0) {
     const fvad_engine_config &c = e->cfg;
@@ -528,6 +565,10 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
     }
     HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
   }
+  // every reader of buffer b (incl. the copy of ticks for k_vadm) is queued
+  HIP_TRY(hipEventRecord(e->ev_buf_free[b], e->stream));
+  e->buf_busy[b] = true;
+  e->next_buf = b ^ 1;
   return FVAD_OK;
 }
 
@@ -608,12 +649,23 @@ extern "C" int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, c
   if (n_ticks == 0) return FVAD_OK;
   HIP_TRY(hipSetDevice(c.device));
   const size_t bytes = (size_t)n_ticks * c.n_streams * c.n_channels * fvad::kFrame * sizeof(float);
-  HIP_TRY(hipMemcpyAsync(e->d_pcm, pcm, bytes, hipMemcpyHostToDevice, e->stream));
-  if (ticks_valid) {
+  if (ticks_valid)
     for (int s = 0; s < c.n_streams; s++)
       if (ticks_valid[s] < 0 || ticks_valid[s] > n_ticks) return fail(FVAD_EINVAL, "ticks_valid out of range");
-    HIP_TRY(hipMemcpyAsync(e->d_ticks, ticks_valid, sizeof(int32_t) * c.n_streams, hipMemcpyHostToDevice, e->stream));
+  // staged: the inputs go through the prep stream (the input of push k-1 is
+  // read only by its k_prep3, earlier on that stream; ticks buffer b is free
+  // once push k-2 finished)
+  hipStream_t cs = e->stream;
+  int *dticks = e->d_ticks;
+  if (e->cfg.mode == FVAD_MODE_STAGED) {
+    const int b = e->next_buf;
+    if (e->buf_busy[b]) HIP_TRY(hipStreamWaitEvent(e->pstream, e->ev_buf_free[b], 0));
+    cs = e->pstream;
+    dticks = e->d_ticks_b[b];
   }
+  HIP_TRY(hipMemcpyAsync(e->d_pcm, pcm, bytes, hipMemcpyHostToDevice, cs));
+  if (ticks_valid)
+    HIP_TRY(hipMemcpyAsync(dticks, ticks_valid, sizeof(int32_t) * c.n_streams, hipMemcpyHostToDevice, cs));
   e->resident_ticks = 0;
   int rc = launch(e, n_ticks, ticks_valid != nullptr, false);
   if (rc) return rc;
@@ -666,6 +718,7 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
 extern "C" int fvad_engine_sync(fvad_engine *e) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (e->pstream) HIP_TRY(hipStreamSynchronize(e->pstream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (e->side) {
     HIP_TRY(hipStreamSynchronize(e->side));

@@ -109,8 +109,11 @@ struct StagedStreams {
 constexpr int kStagedEvents = 15, kStagedLast = 13;
 constexpr int kStagedTime[kStagedKernels][2] = {{0, 1}, {2, 3},   {14, 4},  {4, 5},   {5, 6},  {7, 8},
                                                 {8, 9}, {9, 10}, {10, 11}, {11, 12}, {12, 13}};
-// Launch the 11 kernels; when ev != nullptr the kStagedEvents timing events
-// are recorded.
+// k_prep3 on `stream` (ev[0], ev[1] around it); the engine runs it one push
+// ahead on its own stream (double-buffered xs / ratio / ticks).
+hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev);
+// Launch the other 10 kernels; when ev != nullptr their timing events are
+// recorded.
 hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev);
 const char *staged_kernel_name(int i);
 // Device VADMachines over the window outputs a.out_* of one push: overlap =

@@ -3,7 +3,7 @@
 // rnnoise_process_frame splits into work that depends only on the input
 // samples of the (virtual, channel-interleaved) stream and a thin recurrence:
 //
-//   k_prep2   lane/stream   HP biquad (serial IIR), s16 scaling, RMS volume
+//   k_prep3   lane/stream   HP biquad (serial IIR), s16 scaling, RMS volume
 //                           ratio; x written stream-contiguous with 1248 samples
 //                           of pitch history in front of the launch's frames
 //   k_fftA    wg/frame      analysis window + FFT A, band energies Ex, the
@@ -107,133 +107,148 @@ __device__ __forceinline__ float win960(const float *__restrict__ hw, int i) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// k_prep2: high-pass biquad (a serial IIR with f64 intermediates: no exact
-// parallel form exists, so one lane walks one stream), s16 scaling, RMS
-// volume ratio.  A 256-thread workgroup owns S = 16 / C streams: wave 0 runs
-// the S serial biquad chains out of LDS while waves 2-3 stream the next
-// tick's input in and the previous tick's output out with coalesced 16-byte
-// accesses (the input of S consecutive streams of one tick is contiguous),
-// and wave 1 computes the per-channel RMS sums.
+// k_prep3: high-pass biquad (a serial IIR with f64 intermediates: no exact
+// parallel form exists, so one lane walks one stream), s16 scaling, RMS volume
+// ratio, pitch history.  It uses no LDS and 2 waves per 8 streams: the engine
+// runs it on its own stream beside the previous push's kernels (xs, ratio and
+// ticks are double-buffered), where it must not take the LDS or the wave
+// slots those kernels are sized for.  Wave 0: lane = stream, the biquad chain
+// straight from the input rows (16-byte loads through an 8-deep prefetch
+// ring, 16-byte stores into the stream's xs row); wave 1: lane = channel-slot,
+// the per-tick RMS sums and the volume ratio (channels of a stream are
+// neighbouring lanes).
 // ---------------------------------------------------------------------------
-constexpr int kPrepSlots = 16;  // channel-frames per tick per workgroup
+constexpr int kPrepSlots = 16;  // channel-slots per workgroup (8 stereo streams)
+constexpr int kPrepRing = 8;    // float4 loads in flight per lane
+static_assert((kFrame / 4) % kPrepRing == 0, "prep ring must divide a frame");
 
-__global__ void __launch_bounds__(256) k_prep2(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float inb[2][kPrepSlots * kFrame];
-  __shared__ __attribute__((aligned(16))) float outb[2][kPrepSlots * kFrame];
-  __shared__ float vol[2][kPrepSlots];
-  __shared__ int nts[kPrepSlots];
+// One lane's input sequence of float4 chunks: per tick the C * 480 samples of
+// stream s (contiguous), ticks B * C * 480 floats apart.
+struct PrepSrc {
+  const float *p;  // next chunk to load
+  int r, per_tick;  // chunk index within the tick, chunks per tick
+  size_t tick_jump;  // floats from a tick's end to the next tick's start
+  __device__ __forceinline__ float4 next() {
+    const float4 v = *reinterpret_cast<const float4 *>(p);
+    p += 4;
+    if (++r == per_tick) {
+      r = 0;
+      p += tick_jump;
+    }
+    return v;
+  }
+};
+
+template <bool Scaled>
+__device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, float &mem0, float &mem1) {
+  const int C = a.n_channels;
+  const int per_tick = C * (kFrame / 4);
+  PrepSrc src{a.pcm + (size_t)s * C * kFrame, 0, per_tick, (size_t)(a.n_streams - 1) * C * kFrame};
+  float4 *dst = reinterpret_cast<float4 *>(a.xs + (size_t)s * a.L + kHist);
+  const int nch = nt * per_tick;  // a multiple of kPrepRing
+  float4 ring[kPrepRing];
+#pragma unroll
+  for (int u = 0; u < kPrepRing; u++) ring[u] = u < nch ? src.next() : make_float4(0, 0, 0, 0);
+  const float b0 = -2.0f, b1 = 1.0f, a0 = -1.99599f, a1 = 0.99600f;
+  const float scalar = (float)32767;
+  // b*x and a*y are exact in double (24-bit x 24-bit significands), so one
+  // fma rounds b*x - a*y exactly once, as the C expression does
+  auto step = [&](float v) -> float {
+    const float xi = Scaled ? v * scalar : v;
+    const float yi = xi + mem0;
+    const double yd = (double)yi;
+    mem0 = (float)((double)mem1 + __builtin_fma(-(double)a0, yd, b0 * (double)xi));
+    mem1 = (float)__builtin_fma(-(double)a1, yd, b1 * (double)xi);
+    return yi;
+  };
+  for (int j0 = 0; j0 < nch; j0 += kPrepRing) {
+#pragma unroll
+    for (int u = 0; u < kPrepRing; u++) {
+      const float4 x = ring[u];
+      if (j0 + u + kPrepRing < nch) ring[u] = src.next();
+      float4 y;
+      y.x = step(x.x);
+      y.y = step(x.y);
+      y.z = step(x.z);
+      y.w = step(x.w);
+      dst[j0 + u] = y;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(128) k_prep3(StagedArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int C = a.n_channels, S = kPrepSlots / C, sb = blockIdx.x * S;
   const int ns = min(S, a.n_streams - sb);  // streams in this workgroup
   if (ns <= 0) return;
-  const int slots = ns * C;
-  if (tid < S) nts[tid] = (tid < ns) ? ticks_of(a, sb + tid) : 0;
-  __syncthreads();
-  int T = 0;
-  for (int s = 0; s < ns; s++) T = max(T, nts[s]);
   // pitch history of every stream -> xs[s][0..1248)
-  for (int idx = tid; idx < ns * kHist; idx += 256) {
+  for (int idx = tid; idx < ns * kHist; idx += 128) {
     const int s = idx / kHist, i = idx - s * kHist;
-    if (nts[s] > 0)
+    if (ticks_of(a, sb + s) > 0)
       a.xs[(size_t)(sb + s) * a.L + i] = a.state[(size_t)(sb + s) * st::kWords + st::kPitch + kFrame + i];
   }
-  auto load_tick = [&](int t, int buf) {  // waves 2-3
-    const float4 *src = reinterpret_cast<const float4 *>(a.pcm + ((size_t)t * a.n_streams + sb) * C * kFrame);
-    float4 *dst = reinterpret_cast<float4 *>(inb[buf]);
-    for (int i = tid - 128; i < slots * kFrame / 4; i += 128) dst[i] = src[i];
-  };
-  auto store_tick = [&](int t, int buf) {  // waves 2-3
-    for (int i = tid - 128; i < slots * kFrame / 4; i += 128) {
-      const int slot = i / (kFrame / 4), s = slot / C, c = slot - s * C, k = i - slot * (kFrame / 4);
-      if (t < nts[s])
-        reinterpret_cast<float4 *>(a.xs + (size_t)(sb + s) * a.L + kHist + (size_t)(t * C + c) * kFrame)[k] =
-            reinterpret_cast<const float4 *>(outb[buf] + slot * kFrame)[k];
+  if (wave == 0) {
+    // the chain wave shares its SIMD with the previous push's kernels: its
+    // latency-bound instruction stream goes first
+    __builtin_amdgcn_s_setprio(3);
+    if (lane < ns) {
+      const int s = sb + lane, nt = ticks_of(a, s);
+      if (nt > 0) {
+        float *hp = a.state + (size_t)s * st::kWords + st::kHp;
+        float mem0 = hp[0], mem1 = hp[1];
+        if (a.raw_s16)
+          prep_chain<false>(a, s, nt, mem0, mem1);
+        else
+          prep_chain<true>(a, s, nt, mem0, mem1);
+        hp[0] = mem0;
+        hp[1] = mem1;
+      }
     }
-  };
-  float mem0 = 0, mem1 = 0;
-  if (wave == 0 && lane < ns) {
-    mem0 = a.state[(size_t)(sb + lane) * st::kWords + st::kHp];
-    mem1 = a.state[(size_t)(sb + lane) * st::kWords + st::kHp + 1];
-  }
-  if (wave >= 2 && T > 0) load_tick(0, 0);
-  __syncthreads();
-  const float b0 = -2.0f, b1 = 1.0f, a0 = -1.99599f, a1 = 0.99600f;
-  const float scalar = (float)32767;
-  for (int t = 0; t <= T; t++) {
-    const int cur = t & 1;
-    if (t < T) {
-      if (wave == 0) {
-        if (lane < ns && t < nts[lane]) {
-          // b*x and a*y are exact in double (24-bit x 24-bit significands), so
-          // one fma rounds b*x - a*y exactly once, as the C expression does;
-          // it shortens the serial chain by one dependent f64 operation.  The
-          // loop is specialised on raw_s16 (uniform) so no per-sample select
-          // sits in the chain wave's in-order instruction stream.
-          auto run = [&](auto scaled) {
-            for (int c = 0; c < C; c++) {
-              const float *x = inb[cur] + (lane * C + c) * kFrame;
-              float *y = outb[cur] + (lane * C + c) * kFrame;
-#pragma unroll 8
-              for (int i = 0; i < kFrame; i++) {
-                const float xi = decltype(scaled)::value ? x[i] * scalar : x[i];
-                const float yi = xi + mem0;
-                const double yd = (double)yi;
-                mem0 = (float)((double)mem1 + __builtin_fma(-(double)a0, yd, b0 * (double)xi));
-                mem1 = (float)__builtin_fma(-(double)a1, yd, b1 * (double)xi);
-                y[i] = yi;
-              }
-            }
-          };
-          if (a.raw_s16)
-            run(std::false_type{});
-          else
-            run(std::true_type{});
-        }
-      } else if (wave == 1) {
-        if (lane < slots) {
-          const float *x = inb[cur] + lane * kFrame;
-          float sum = 0;
-#pragma unroll 8
-          for (int i = 0; i < kFrame; i++) sum += x[i] * x[i];
-          vol[cur][lane] = sqrtf(sum / (float)kFrame);
-        }
-        if (t > 0 && lane < ns && t - 1 < nts[lane]) {
-          float vmin = 1, vmax = 0;
-          for (int c = 0; c < C; c++) {
-            const float vl = vol[cur ^ 1][lane * C + c];
-            if (vl < vmin) vmin = vl;
-            if (vl > vmax) vmax = vl;
+  } else {
+    // lane = channel-slot (s, c); every lane runs the tick loop (shuffles)
+    const int ls = min(lane, ns * C - 1);
+    const int sl = ls / C, c = ls - sl * C, s = sb + sl;
+    const int nt = lane < ns * C ? ticks_of(a, s) : 0;
+    const float *x = a.pcm + ((size_t)s * C + c) * kFrame;
+    const size_t tick_stride = (size_t)a.n_streams * C * kFrame;
+    for (int t = 0; t < a.n_ticks; t++) {
+      float sum = 0;
+      if (t < nt) {
+        const float4 *x4 = reinterpret_cast<const float4 *>(x + (size_t)t * tick_stride);
+        float4 ring[kPrepRing];
+#pragma unroll
+        for (int u = 0; u < kPrepRing; u++) ring[u] = x4[u];
+        for (int j0 = 0; j0 < kFrame / 4; j0 += kPrepRing) {
+#pragma unroll
+          for (int u = 0; u < kPrepRing; u++) {
+            const float4 v = ring[u];
+            if (j0 + u + kPrepRing < kFrame / 4) ring[u] = x4[j0 + u + kPrepRing];
+            sum += v.x * v.x;
+            sum += v.y * v.y;
+            sum += v.z * v.z;
+            sum += v.w * v.w;
           }
-          a.ratio[(size_t)(t - 1) * a.n_streams + sb + lane] = (vmax == 0) ? 0 : vmin / vmax;
         }
-      } else {
-        if (t + 1 < T) load_tick(t + 1, cur ^ 1);
-        if (t > 0) store_tick(t - 1, cur ^ 1);
       }
-    } else {
-      if (wave >= 2 && t > 0) store_tick(t - 1, cur ^ 1);
-      if (wave == 1 && t > 0 && lane < ns && t - 1 < nts[lane]) {
-        float vmin = 1, vmax = 0;
-        for (int c = 0; c < C; c++) {
-          const float vl = vol[cur ^ 1][lane * C + c];
-          if (vl < vmin) vmin = vl;
-          if (vl > vmax) vmax = vl;
-        }
-        a.ratio[(size_t)(t - 1) * a.n_streams + sb + lane] = (vmax == 0) ? 0 : vmin / vmax;
+      const float vol = sqrtf(sum / (float)kFrame);
+      // volume ratio of the stream (VAD.zig:253-272): min / max over its channels
+      float vmin = 1, vmax = 0;
+      for (int c2 = 0; c2 < C; c2++) {
+        const float vl = __shfl(vol, sl * C + c2);
+        if (vl < vmin) vmin = vl;
+        if (vl > vmax) vmax = vl;
       }
+      if (lane < ns * C && c == 0 && t < nt) a.ratio[(size_t)t * a.n_streams + s] = (vmax == 0) ? 0 : vmin / vmax;
     }
-    __syncthreads();
   }
-  if (wave == 0 && lane < ns && nts[lane] > 0) {
-    a.state[(size_t)(sb + lane) * st::kWords + st::kHp] = mem0;
-    a.state[(size_t)(sb + lane) * st::kWords + st::kHp + 1] = mem1;
-  }
+  __syncthreads();
   // pitch_buf after the last frame = the last 1728 samples of the row
-  for (int idx = tid; idx < ns * kPitchBuf; idx += 256) {
+  for (int idx = tid; idx < ns * kPitchBuf; idx += 128) {
     const int s = idx / kPitchBuf, i = idx - s * kPitchBuf;
-    if (nts[s] > 0)
+    const int nt = ticks_of(a, sb + s);
+    if (nt > 0)
       a.state[(size_t)(sb + s) * st::kWords + st::kPitch + i] =
-          a.xs[(size_t)(sb + s) * a.L + (size_t)(nts[s] * C - 1) * kFrame + i];
+          a.xs[(size_t)(sb + s) * a.L + (size_t)(nt * C - 1) * kFrame + i];
   }
 }
 
@@ -2171,7 +2186,7 @@ __global__ void __launch_bounds__(64) k_vadm(StagedArgs a) {
 // launcher
 // ---------------------------------------------------------------------------
 const char *staged_kernel_name(int i) {
-  static const char *const names[kStagedKernels] = {"k_prep2", "k_fftA", "k_plpc",  "k_pcorr",   "k_select", "k_pspec",
+  static const char *const names[kStagedKernels] = {"k_prep3", "k_fftA", "k_plpc",  "k_pcorr",   "k_select", "k_pspec",
                                                      "k_rnn",   "k_synth", "k_ola", "k_winmeta", "k_fftb"};
   return (i >= 0 && i < kStagedKernels) ? names[i] : nullptr;
 }
@@ -2186,6 +2201,14 @@ int resident_blocks(K kernel, int threads, int n_cu) {
   return per_cu * n_cu;
 }
 }  // namespace
+
+hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) {
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  const int S = kPrepSlots / a.n_channels;
+  hipLaunchKernelGGL(k_prep3, dim3((a.n_streams + S - 1) / S), dim3(128), 0, stream, a);
+  if (ev) (void)hipEventRecord(ev[1], stream);
+  return hipGetLastError();
+}
 
 hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev) {
   hipStream_t stream = st.main;
@@ -2210,12 +2233,6 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   auto rec_aux = [&](int k) {
     if (ev) (void)hipEventRecord(ev[k], st.aux);
   };
-  rec(0);
-  {
-    const int S = kPrepSlots / a.n_channels;
-    hipLaunchKernelGGL(k_prep2, dim3((a.n_streams + S - 1) / S), dim3(256), 0, stream, a);
-  }
-  rec(1);
   // fork: k_fftA (aux) || pitch branch (main); both only read xs and write
   // disjoint buffers (X, Ex, Lyf, silence | ptile, rec, pitch, pitch state)
   const long long fgroups = (frames + FF - 1) / FF;

@@ -117,7 +117,7 @@ def staged_kernels(n_channels=2, fft_size=2048):
     plpc = (p["pitch downsample + autocorr + LPC + FIR5"] + 240 * 2 + 147 * 4 + 480 * 2 + 294 * 4 +
             480 * 2 + 384 * 4)
     k = {
-        "k_prep2": (p["prep: s16 scale + HP biquad + rms"], 480 * 4 * 2 + 4.0 / C),
+        "k_prep3": (p["prep: s16 scale + HP biquad + rms"], 480 * 4 * 2 + 4.0 / C),
         "k_fftA": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly,
                    960 * 4 + spec + 22 * 4 * 2 + 4),
         "k_plpc": (plpc, 1728 * 4 + PTILE_ROWS * 4),
