@@ -1369,13 +1369,14 @@ __device__ __forceinline__ void rnn_inputs(const int8_t *wc, const RnnIn &in, in
 
 // dense layer / GRU z|r gates of image matrix m:
 //   out[c][s] = act(kWs * (b[c] + sum_j w[c][j] * [in ; state][j][s]))
+// (tasks t = tid, tid + NT, ...; NT = 0: the single task tid)
 template <int m, int S, int G, int NT>
 __device__ __forceinline__ void rnn_gates(const int8_t *W, const RnnIn &in, const float *stT, float *outT, int act,
                                           const float *tt, int tid) {
   constexpr int SL = S / G, cols = rnnimg::kCols[m];
   constexpr int ob = rnnimg::off_b(m), ow = rnnimg::off_w(m), ws = rnnimg::stride(m);
   constexpr int gst = (m == 1) ? 1 : (m == 3 || m == 5) ? 3 : -1;  // state segment of z|r matrices
-  for (int t = tid; t < cols * G; t += NT) {
+  for (int t = tid; t < cols * G; t += (NT ? NT : cols * G)) {
     const int c = t / G, s0 = (t - c * G) * SL;
     const int8_t *wc = W + ow + c * ws;
     float acc[SL];
@@ -1397,7 +1398,7 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
   constexpr int SL = S / G, cols = rnnimg::kCols[m], N = cols;
   constexpr int ob = rnnimg::off_b(m), ow = rnnimg::off_w(m), ws = rnnimg::stride(m);
   constexpr int gst = (m == 2) ? 1 : 3;
-  for (int t = tid; t < cols * G; t += NT) {
+  for (int t = tid; t < cols * G; t += (NT ? NT : cols * G)) {
     const int c = t / G, s0 = (t - c * G) * SL;
     const int8_t *wc = W + ow + c * ws;
     float acc[SL];
@@ -1660,6 +1661,263 @@ __global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
   }
   if (tid < S && sb + tid < a.n_streams && nfs[tid] > 0)
     reinterpret_cast<int *>(a.state)[(size_t)(sb + tid) * st::kWords + st::kMemId] = memid[tid];
+}
+
+// ---------------------------------------------------------------------------
+// k_rnn2: k_rnn's recurrence as a three-stage software pipeline over frames.
+// compute_rnn's GRUs depend on each other only within a frame (vad -> noise ->
+// denoise) and on their own previous state, so step t runs the vad GRU of
+// frame t, the noise GRU of frame t-1 and the denoise GRU of frame t-2 side by
+// side, with the frame features of t+1 and the gain smoothing of t-3:
+//   P1  z|r gates of vad(t), noise(t-1), denoise(t-2); features of t+1
+//       (cepstral memory, deltas, distance row); gains of t-3
+//   P2  candidate gates of the three GRUs; spectral variability of t+1
+//   P3  denoise_output(t-2), dense(t+1), vad_output(t), next features -> LDS
+// Three barriers per step instead of twelve, and every phase has enough
+// independent chains to fill the CU.  Buffers are rings indexed by frame.
+// ---------------------------------------------------------------------------
+template <int S, int G, int NT>
+__global__ void __launch_bounds__(NT) k_rnn2(StagedArgs a) {
+  static_assert(NT == 1024 && S == 8 && G == 4, "k_rnn2 thread plan is for 8 streams x 4 groups x 1024 threads");
+  struct Lds {
+    alignas(16) float featT[4][44 * S];  // frame f in slot f & 3
+    alignas(16) float doutT[4][24 * S];
+    alignas(16) float gvT[4][24 * S];
+    alignas(16) float gnT[2][48 * S];
+    alignas(16) float gdT[2][96 * S];
+    alignas(16) float zrv[48 * S], zrn[96 * S], zrd[192 * S];
+    alignas(16) float gout[22 * S];
+    float tt[204];
+    float ceps[S][kCeps * kBands];
+    float dist[S][kCeps * kCeps];
+    float lastg[S][kBands];
+    float pf[S][kRnnPf];  // features of the frame the next F-C stage reads
+    int act[8][S];        // frame f in slot f & 7: valid and not silent
+    int memid[S], nfs[S];
+    long long fbase[S];
+    alignas(16) int8_t W[rnnimg::kBytes];
+  };
+  __shared__ Lds L;
+  const int tid = threadIdx.x;
+  const int sb = blockIdx.x * S;
+  const int *ra = a.rnn_act;
+  {
+    const int4 *src = reinterpret_cast<const int4 *>(a.rnn_img);
+    int4 *dst = reinterpret_cast<int4 *>(L.W);
+    for (int i = tid; i < rnnimg::kBytes / 16; i += NT) dst[i] = src[i];
+    for (int i = tid; i < 201; i += NT) L.tt[i] = a.plan->tansig[i];
+  }
+  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
+    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
+    L.ceps[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] : 0.0f;
+  }
+  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
+    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
+    L.dist[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] : 0.0f;
+  }
+  for (int idx = tid; idx < S * kBands; idx += NT) {
+    const int s = idx / kBands, i = idx - s * kBands;
+    L.lastg[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] : 0.0f;
+  }
+  // states before frame 0 = "frame -1": gv slot 3, gn / gd slot 1
+  for (int idx = tid; idx < S * 96; idx += NT) {
+    const int s = idx / 96, i = idx - s * 96;
+    const bool ok = sb + s < a.n_streams;
+    const float *stp = a.state + (size_t)(sb + s) * st::kWords;
+    if (i < 24) L.gvT[3][i * S + s] = ok ? stp[st::kVadGru + i] : 0.0f;
+    if (i < 48) L.gnT[1][i * S + s] = ok ? stp[st::kNoiseGru + i] : 0.0f;
+    L.gdT[1][i * S + s] = ok ? stp[st::kDenGru + i] : 0.0f;
+  }
+  if (tid < 8 * S) L.act[tid / S][tid % S] = 0;
+  if (tid < S) {
+    const int s = sb + tid;
+    const bool ok = s < a.n_streams;
+    L.memid[tid] = ok ? reinterpret_cast<const int *>(a.state)[(size_t)s * st::kWords + st::kMemId] : 0;
+    L.nfs[tid] = ok ? ticks_of(a, s) * a.n_channels : 0;
+    L.fbase[tid] = (long long)s * a.V;
+  }
+  __syncthreads();
+  int maxnf = 0;
+#pragma unroll
+  for (int s = 0; s < S; s++) maxnf = max(maxnf, L.nfs[s]);
+  // prefetch lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (as 1.0 / 0.0)
+  const int pfs = tid / kRnnPf, pfi = tid - pfs * kRnnPf;
+  const bool pf_lane = tid < S * kRnnPf;
+  auto fetch = [&](int v) -> float {
+    if (!pf_lane || v >= L.nfs[pfs]) return 1.0f;  // past the end: treated as silent (inactive)
+    const long long f = L.fbase[pfs] + v;
+    if (pfi < kBands) return a.Lyf[f * kBands + pfi];
+    if (pfi < kBands + 7) return a.f34[f * 8 + (pfi - kBands)];
+    return a.silence[f] ? 1.0f : 0.0f;
+  };
+  // F-C: frame f's features from L.pf (cepstral memory, deltas, 34..40, the
+  // new distance row); item (s, i), i < 37; item i == 0 records act(f)
+  auto feat_c = [&](int f, int idx) {
+    const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
+    const bool valid = f < L.nfs[s];
+    const bool on = valid && L.pf[s][kRnnPf - 1] == 0.0f;
+    if (i == 0) {
+      L.act[f & 7][s] = on;
+      if (valid && !on) a.vadf[L.fbase[s] + f] = 0;  // silent: X passes through, state untouched
+    }
+    if (!on) return;
+    float *featT = L.featT[f & 3];
+    const int mi = L.memid[s];
+    const float *c0 = L.pf[s];  // ceps_0 (the row being written at memid)
+    if (i < kBands) {
+      L.ceps[s][mi * kBands + i] = c0[i];
+      if (i < 6) {
+        const float *c1 = L.ceps[s] + ((mi < 1) ? kCeps + mi - 1 : mi - 1) * kBands;
+        const float *c2 = L.ceps[s] + ((mi < 2) ? kCeps + mi - 2 : mi - 2) * kBands;
+        featT[i * S + s] = c0[i] + c1[i] + c2[i];
+        featT[(kBands + i) * S + s] = c0[i] - c2[i];
+        featT[(kBands + 6 + i) * S + s] = c0[i] - 2 * c1[i] + c2[i];
+      } else {
+        featT[i * S + s] = c0[i];
+      }
+    } else if (i < kBands + 7) {
+      featT[(34 + i - kBands) * S + s] = c0[i];
+    } else {
+      const int j = i - kBands - 7;
+      if (j != mi) {
+        const float *cj = L.ceps[s] + j * kBands;
+        float d = 0;
+#pragma unroll
+        for (int k = 0; k < kBands; k++) {
+          const float tmp = c0[k] - cj[k];
+          d += tmp * tmp;
+        }
+        L.dist[s][mi * kCeps + j] = d;
+        L.dist[s][j * kCeps + mi] = d;
+      }
+    }
+  };
+  // F-D: spectral variability of frame f, stream s
+  auto feat_d = [&](int f, int s) {
+    if (!L.act[f & 7][s]) return;
+    float sv = 0;
+    for (int i = 0; i < kCeps; i++) {
+      float mindist = 1e15f;
+      for (int j = 0; j < kCeps; j++)
+        if (j != i) mindist = (mindist < L.dist[s][i * kCeps + j]) ? mindist : L.dist[s][i * kCeps + j];
+      sv += mindist;
+    }
+    L.featT[f & 3][41 * S + s] = (float)(sv / kCeps - 2.1);
+    int mid = L.memid[s] + 1;
+    if (mid == kCeps) mid = 0;
+    L.memid[s] = mid;
+  };
+  // prologue: features and dense layer of frame 0, features of frame 1 staged
+  if (pf_lane) L.pf[pfs][pfi] = fetch(0);
+  __syncthreads();
+  for (int idx = tid; idx < S * (kBands + 7 + kCeps); idx += NT) feat_c(0, idx);
+  __syncthreads();
+  if (tid < S) feat_d(0, tid);
+  __syncthreads();
+  rnn_gates<0, S, G, NT>(L.W, RnnIn{L.featT[0], nullptr, nullptr}, nullptr, L.doutT[0], ra[0], L.tt, tid);
+  if (pf_lane) L.pf[pfs][pfi] = fetch(1);
+  float pf_next = fetch(2);
+  __syncthreads();
+  STAMP_INIT();
+  for (int t = 0; t <= maxnf + 2; t++) {
+    const int fv = t, fn = t - 1, fd = t - 2;
+    // ---- P1: z|r gates; features of t+1; gains of t-3
+    if (fn >= 0 && fn < maxnf) {
+      if (tid < 256)  // noise z|r tasks 0..255
+        rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 3]}, L.gnT[(fn + 1) & 1], L.zrn,
+                              kActSigmoid, L.tt, tid);
+    }
+    if (fd >= 0 && fd < maxnf && tid >= 256)  // denoise z|r tasks 0..767
+      rnn_gates<5, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 3]}, L.gdT[(fd + 1) & 1], L.zrd,
+                            kActSigmoid, L.tt, tid - 256);
+    if (fn >= 0 && fn < maxnf && tid < 128)  // noise z|r tasks 256..383
+      rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 3]}, L.gnT[(fn + 1) & 1], L.zrn,
+                            kActSigmoid, L.tt, 256 + tid);
+    if (fv < maxnf && tid >= 128 && tid < 320)  // vad z|r tasks 0..191
+      rnn_gates<1, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, kActSigmoid,
+                            L.tt, tid - 128);
+    if (t + 1 < maxnf && tid >= 768)
+      for (int idx = tid - 768; idx < S * (kBands + 7 + kCeps); idx += 256) feat_c(t + 1, idx);
+    if (t >= 3 && tid >= 576 && tid < 768) {  // gain smoothing g = max(g, .6*lastg) (denoise.c), frame t-3
+      const int f3 = t - 3;
+      for (int idx = tid - 576; idx < S * kBands; idx += 192) {
+        const int s = idx / kBands, i = idx - s * kBands;
+        if (!L.act[f3 & 7][s]) continue;
+        const long long f = L.fbase[s] + f3;
+        const float gi = L.gout[i * S + s];
+        const float al = .6f * L.lastg[s][i];
+        const float gsm = (gi > al) ? gi : al;
+        L.lastg[s][i] = gsm;
+        a.gr[f * kBands + i] = gi;
+        a.gs[f * kBands + i] = gsm;
+      }
+    }
+    __syncthreads();
+    RSTAMP(0);
+    // ---- P2: candidate gates; spectral variability of t+1
+    if (tid < 384) {
+      if (fd >= 0 && fd < maxnf)
+        rnn_cand<6, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 3]}, L.gdT[(fd + 1) & 1], L.zrd,
+                             L.gdT[fd & 1], L.act[fd & 7], ra[6], L.tt, tid);
+    } else if (tid < 576) {
+      if (fn >= 0 && fn < maxnf)
+        rnn_cand<4, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 3]}, L.gnT[(fn + 1) & 1], L.zrn,
+                             L.gnT[fn & 1], L.act[fn & 7], ra[4], L.tt, tid - 384);
+    } else if (tid < 672) {
+      if (fv < maxnf)
+        rnn_cand<2, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, L.gvT[fv & 3],
+                             L.act[fv & 7], ra[2], L.tt, tid - 576);
+    } else if (tid < 672 + S) {
+      if (t + 1 < maxnf) feat_d(t + 1, tid - 672);
+    }
+    __syncthreads();
+    RSTAMP(1);
+    // ---- P3: denoise_output(t-2), dense(t+1), vad_output(t); features of t+2 -> LDS
+    if (tid < 88) {
+      if (fd >= 0 && fd < maxnf)
+        rnn_gates<7, S, G, 0>(L.W, RnnIn{L.gdT[fd & 1], nullptr, nullptr}, nullptr, L.gout, ra[7], L.tt, tid);
+    } else if (tid < 88 + 96) {
+      if (t + 1 < maxnf)
+        rnn_gates<0, S, G, 0>(L.W, RnnIn{L.featT[(t + 1) & 3], nullptr, nullptr}, nullptr, L.doutT[(t + 1) & 3], ra[0],
+                              L.tt, tid - 88);
+    } else if (tid < 88 + 96 + S) {
+      const int s = tid - 184;
+      if (fv < maxnf && L.act[fv & 7][s]) {
+        constexpr int ob = rnnimg::off_b(8), ow = rnnimg::off_w(8);
+        float sum = (float)L.W[ob];
+        for (int j = 0; j < 24; j++) sum += (float)L.W[ow + j] * L.gvT[fv & 3][j * S + s];
+        a.vadf[L.fbase[s] + fv] = activate(L.tt, ra[8], kWs * sum);
+      }
+    }
+    if (pf_lane) L.pf[pfs][pfi] = pf_next;
+    pf_next = fetch(t + 3);
+    __syncthreads();
+    RSTAMP(2);
+  }
+  STAMP_FLUSH(0, 3);
+  const int fin = maxnf - 1;  // the slots of the latest states ("frame -1" if there were none)
+  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
+    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
+    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] = L.ceps[s][i];
+  }
+  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
+    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
+    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] = L.dist[s][i];
+  }
+  for (int idx = tid; idx < S * kBands; idx += NT) {
+    const int s = idx / kBands, i = idx - s * kBands;
+    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] = L.lastg[s][i];
+  }
+  for (int idx = tid; idx < S * 96; idx += NT) {
+    const int s = idx / 96, i = idx - s * 96;
+    if (sb + s >= a.n_streams || L.nfs[s] <= 0) continue;
+    float *stp = a.state + (size_t)(sb + s) * st::kWords;
+    if (i < 24) stp[st::kVadGru + i] = L.gvT[fin & 3][i * S + s];
+    if (i < 48) stp[st::kNoiseGru + i] = L.gnT[fin & 1][i * S + s];
+    stp[st::kDenGru + i] = L.gdT[fin & 1][i * S + s];
+  }
+  if (tid < S && sb + tid < a.n_streams && L.nfs[tid] > 0)
+    reinterpret_cast<int *>(a.state)[(size_t)(sb + tid) * st::kWords + st::kMemId] = L.memid[tid];
 }
 
 // ---------------------------------------------------------------------------
@@ -2187,7 +2445,7 @@ __global__ void __launch_bounds__(64) k_vadm(StagedArgs a) {
 // ---------------------------------------------------------------------------
 const char *staged_kernel_name(int i) {
   static const char *const names[kStagedKernels] = {"k_prep3", "k_fftA", "k_plpc",  "k_pcorr",   "k_select", "k_pspec",
-                                                     "k_rnn",   "k_synth", "k_ola", "k_winmeta", "k_fftb"};
+                                                     "k_rnn2",   "k_synth", "k_ola", "k_winmeta", "k_fftb"};
   return (i >= 0 && i < kStagedKernels) ? names[i] : nullptr;
 }
 
@@ -2256,7 +2514,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   rec(7);
   hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
   rec(8);
-  hipLaunchKernelGGL((k_rnn<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
+  hipLaunchKernelGGL((k_rnn2<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
                      stream, a);
   rec(9);
   hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);

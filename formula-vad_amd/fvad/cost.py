@@ -126,7 +126,7 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_pspec": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
         # k_rnn: cepstral memory, spectral variability, GRU stack, gain
         # smoothing; reads DCT(Ly), features 34..40, silence; writes g, smoothed g, vad
-        "k_rnn": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"],
+        "k_rnn2": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"],
                   (22 + 8 + 1) * 4 + (22 + 22 + 1) * 4),
         # k_synth: pitch filter (X + r P, band energies, norm), gains, synthesis;
         # reads X, P, Exp, g, Ex, Ep, smoothed g, silence; writes the windowed frame

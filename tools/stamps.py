@@ -17,7 +17,10 @@ NAMES = ["load state", "pitch shift", "analysis window+scatter", "FFT A (X) + co
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 MODE = sys.argv[3] if len(sys.argv) > 3 else "fused"
-if MODE == "staged":
+if MODE == "staged" and os.environ.get("FVAD_RNN2", "1") == "1":
+    NAMES = ["P1 z|r gates + features(t+1) + gains(t-3)", "P2 candidates + spectral variability",
+             "P3 outputs, dense(t+1), vad_out"] + [""] * 9
+elif MODE == "staged":
     NAMES = ["features+deltas+dist row", "spectral variability", "dense", "vad z|r", "vad h", "noise z|r + vad_out",
              "noise h", "denoise z|r", "denoise h", "denoise_output", "gains + outputs + prefetch", "next act"]
     FFTA = ["group setup", "window scatter (global loads)", "FFT 960 x F", "X store + band sums + log10",
