@@ -37,6 +37,7 @@
 #include "fvad_device.h"
 #include "fvad_internal.h"
 #include "fvad_staged.h"
+#include "fvad_wfft.h"
 
 namespace fvad {
 
@@ -2443,6 +2444,318 @@ __global__ void __launch_bounds__(64) k_vadm(StagedArgs a) {
 // ---------------------------------------------------------------------------
 // launcher
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Wave-per-frame frame kernels (k_fftAw, k_pspecw, k_synthw): one wave owns a
+// frame at a time and runs its 960-point transform in registers (fvad_wfft.h)
+// with its own LDS region, so a workgroup never waits at a barrier between
+// FFT stages; band terms go to the same region once the transform is done and
+// the 22 band chains run on lanes 0..21 (k_pspecw: Ep on 0..21 beside Exp on
+// 32..53).  Same arithmetic as k_fftA / k_pspec / k_synth.  Frames are taken
+// in batches of kWB consecutive frames per wave (dynamic, per-XCD queues as
+// take_group); k_fftAw runs each batch's serial Ly chains lane per frame.
+// ---------------------------------------------------------------------------
+constexpr int kWB = 8;   // frames per wave batch
+constexpr int kWNW = 4;  // waves per workgroup
+constexpr int kWOcc = 3;  // workgroups per CU (<= 168 VGPRs, <= 53 KB LDS)
+
+__device__ __forceinline__ long long wave_take(const StagedArgs &a, int slot, int lane) {
+  const int x = blockIdx.x % kQueues;
+  unsigned v = 0;
+  if (lane == 0) v = atomicAdd(&a.work[slot * kQueues + x], 1u);
+  v = __shfl(v, 0);
+  return x + (long long)kQueues * v;
+}
+
+// A per-iteration zero the compiler cannot see through: table reads indexed
+// with it stay inside the frame loop instead of being hoisted into registers
+// for the whole kernel (which would cost occupancy).
+__device__ __forceinline__ int opaque0() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+
+struct WaveTabs {
+  BandTab T;
+  wfft::TwTab tw;
+  float hw[kFrame];
+};
+__device__ __forceinline__ void wave_tabs_load(WaveTabs &w, const Plan *__restrict__ P, int tid) {
+  bandtab_load(w.T, P, tid, 64 * kWNW);
+  wfft::load_twtab(w.tw, reinterpret_cast<const float2 *>(P->tw960), tid, 64 * kWNW);
+  for (int i = tid; i < kFrame; i += 64 * kWNW) w.hw[i] = P->half_window[i];
+}
+
+// layout-A input of a 960-sample analysis window at pb (x * w / 960, imag 0)
+__device__ __forceinline__ void wave_window(const float *__restrict__ pb, const float *hw, int lane,
+                                            float2 (&v)[16]) {
+  hw += opaque0();
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int i = wfft::in_index(lane, k);
+    float val = lane < 60 ? pb[i] : 0.0f;
+    val *= lane < 60 ? win960(hw, i) : 0.0f;
+    v[k] = make_float2(kScale960 * val, kScale960 * 0.0f);
+  }
+}
+
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
+  __shared__ WaveTabs tb;
+  __shared__ float exb[kWNW][kWB][kBands + 2], lyb[kWNW][kWB][kBands + 2];
+  __shared__ int silb[kWNW][kWB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  wave_tabs_load(tb, a.plan, tid);
+  wfft::Tw tw;
+  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
+  __syncthreads();
+  const BandTab &T = tb.T;
+  float2 *R = Rg[wv];
+  float *tr = reinterpret_cast<float *>(R);
+  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
+  for (long long g = wave_take(a, kWorkFftA, lane); g < nb; g = wave_take(a, kWorkFftA, lane)) {
+    for (int fr = 0; fr < kWB; fr++) {
+      const int f = frame_of(a, g, kWB, fr);
+      if (f < 0) continue;
+      float2 v[16];
+      wave_window(frame_pb(a, f) + (kPitchBuf - kWin), tb.hw, lane, v);
+      wfft::run(v, tw, tb.tw, R, lane);
+      float2 *X = a.X + (size_t)f * kFreq;
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        if (64 * r + lane < kFreq) X[64 * r + lane] = v[r];
+#pragma unroll
+      for (int r = 0; r < 7; r++) {
+        const int n = 64 * r + lane;
+        if (n < 400) band_terms(v[r], v[r], T, n, tr[n], tr[400 + n]);
+      }
+      wfft::wsync();
+      if (lane < kBands) {
+        const float ex = band_chain(tr, tr + 400, T, lane);
+        a.Ex[(size_t)f * kBands + lane] = ex;
+        exb[wv][fr][lane] = ex;
+        lyb[wv][fr][lane] = (float)log10(1e-2 + (double)ex);
+      }
+      wfft::wsync();
+    }
+    // the Ly floor chain and the silence gate, lane per frame
+    if (lane < kWB) {
+      const int f = frame_of(a, g, kWB, lane);
+      if (f >= 0) {
+        float *Ly = lyb[wv][lane];
+        const float *Exl = exb[wv][lane];
+        float logMax = -2, follow = -2, E = 0;
+        for (int i = 0; i < kBands; i++) {
+          const float ly0 = Ly[i];
+          const double bb = (follow - 1.5 > (double)ly0) ? follow - 1.5 : (double)ly0;
+          const double aa = ((double)(logMax - 7) > bb) ? (double)(logMax - 7) : bb;
+          const float ly = (float)aa;
+          Ly[i] = ly;
+          logMax = (logMax > ly) ? logMax : ly;
+          follow = (float)((follow - 1.5 > (double)ly) ? follow - 1.5 : (double)ly);
+          E += Exl[i];
+        }
+        const int sil = ((double)E < 0.04) ? 1 : 0;
+        silb[wv][lane] = sil;
+        a.silence[f] = sil;
+      }
+    }
+    wfft::wsync();
+    for (int idx = lane; idx < kWB * kBands; idx += 64) {
+      const int fr = idx / kBands, b = idx - fr * kBands;
+      const int f = frame_of(a, g, kWB, fr);
+      if (f >= 0 && !silb[wv][fr]) {
+        const float *Ly = lyb[wv][fr];
+        float sum = 0;
+#pragma unroll
+        for (int j = 0; j < kBands; j++) sum += Ly[j] * T.dct[j * kBands + b];
+        float val = (float)(sum * sqrt(2. / 22));
+        if (b == 0) val -= 12;
+        if (b == 1) val -= 4;
+        a.Lyf[(size_t)f * kBands + b] = val;
+      }
+    }
+    wfft::wsync();
+  }
+}
+
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
+  __shared__ WaveTabs tb;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  wave_tabs_load(tb, a.plan, tid);
+  wfft::Tw tw;
+  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
+  __syncthreads();
+  const BandTab &T = tb.T;
+  float2 *R = Rg[wv];
+  float *tr = reinterpret_cast<float *>(R);
+  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
+  for (long long g = wave_take(a, kWorkPspec, lane); g < nb; g = wave_take(a, kWorkPspec, lane)) {
+    for (int fr = 0; fr < kWB; fr++) {
+      const int f = frame_of(a, g, kWB, fr);
+      if (f < 0) continue;
+      const int pit = a.pitch[f];
+      // X of bins < 400 (Exp terms), issued before the transform
+      float2 xr[7];
+      const float2 *X = a.X + (size_t)f * kFreq;
+#pragma unroll
+      for (int r = 0; r < 7; r++) xr[r] = (64 * r + lane < 400) ? X[64 * r + lane] : make_float2(0, 0);
+      float2 v[16];
+      wave_window(frame_pb(a, f) + (kPitchBuf - kWin - pit), tb.hw, lane, v);
+      wfft::run(v, tw, tb.tw, R, lane);
+      float2 *P = a.P + (size_t)f * kFreq;
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        if (64 * r + lane < kFreq) P[64 * r + lane] = v[r];
+#pragma unroll
+      for (int r = 0; r < 7; r++) {
+        const int n = 64 * r + lane;
+        if (n < 400) {
+          band_terms(v[r], v[r], T, n, tr[n], tr[400 + n]);
+          band_terms(xr[r], v[r], T, n, tr[800 + n], tr[1200 + n]);
+        }
+      }
+      wfft::wsync();
+      // Ep chains on lanes 0..21, Exp chains on lanes 32..53
+      const int h = lane >> 5, b = lane & 31;
+      float cv = 0;
+      if (b < kBands) cv = band_chain(tr + 800 * h, tr + 800 * h + 400, T, b);
+      const float expv = __shfl(cv, lane + 32);
+      float e = 0;
+      if (lane < kBands) {
+        const size_t o = (size_t)f * kBands + lane;
+        const float ex = a.Ex[o];
+        e = (float)((double)expv / sqrt(.001 + (double)(ex * cv)));
+        a.Ep[o] = cv;
+        a.Exp[o] = e;
+      }
+      float sum = 0;
+#pragma unroll
+      for (int j = 0; j < kBands; j++)
+        sum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), j)) * T.dct[j * kBands + (lane < 6 ? lane : 0)];
+      if (lane < 6) {
+        float val = (float)(sum * sqrt(2. / 22));
+        if (lane == 0) val = (float)(val - 1.3);
+        if (lane == 1) val = (float)(val - 0.9);
+        a.f34[(size_t)f * 8 + lane] = val;
+      } else if (lane == 6) {
+        a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pit - 300));
+      }
+      wfft::wsync();
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
+  __shared__ WaveTabs tb;
+  __shared__ float bp[kWNW][3][kBands + 2];  // r, nrm, smoothed gains of the wave's frame
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  wave_tabs_load(tb, a.plan, tid);
+  wfft::Tw tw;
+  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
+  __syncthreads();
+  const BandTab &T = tb.T;
+  float2 *R = Rg[wv];
+  float *tr = reinterpret_cast<float *>(R);
+  float *rr = bp[wv][0], *nrm = bp[wv][1], *gsm = bp[wv][2];
+  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
+  for (long long g = wave_take(a, kWorkSynth, lane); g < nb; g = wave_take(a, kWorkSynth, lane)) {
+    for (int fr = 0; fr < kWB; fr++) {
+      const int f = frame_of(a, g, kWB, fr);
+      if (f < 0) continue;
+      const bool fil = !a.silence[f];  // silent frames: X passes through
+      const float2 *X = a.X + (size_t)f * kFreq;
+      const float2 *P = a.P + (size_t)f * kFreq;
+      float2 xv[8];
+#pragma unroll
+      for (int r = 0; r < 8; r++) xv[r] = (64 * r + lane < kFreq) ? X[64 * r + lane] : make_float2(0, 0);
+      if (fil) {
+        float2 pv[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) pv[r] = (64 * r + lane < kFreq) ? P[64 * r + lane] : make_float2(0, 0);
+        if (lane < kBands) {
+          const size_t o = (size_t)f * kBands + lane;
+          const float Exp = a.Exp[o], gg = a.gr[o], Ex = a.Ex[o], Ep = a.Ep[o];
+          float r;
+          if (Exp > gg)
+            r = 1;
+          else
+            r = (float)((double)((Exp * Exp) * (1 - (gg * gg))) / (.001 + (double)((gg * gg) * (1 - (Exp * Exp)))));
+          float cl = (0 > r) ? 0 : r;
+          cl = (1 < cl) ? 1 : cl;
+          r = (float)sqrt((double)cl);
+          r = (float)((double)r * sqrt((double)Ex / (1e-8 + (double)Ep)));
+          rr[lane] = r;
+          gsm[lane] = a.gs[o];
+        }
+        wfft::wsync();
+        // pitch filter X += r P; band terms of the filtered X
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const int n = 64 * r + lane;
+          if (n < kFreq) {
+            const float rf = interp_gain_t(rr, T, n);
+            xv[r].x += rf * pv[r].x;
+            xv[r].y += rf * pv[r].y;
+            if (n < 400) band_terms(xv[r], xv[r], T, n, tr[n], tr[400 + n]);
+          }
+        }
+        wfft::wsync();
+        if (lane < kBands) {
+          const float newE = band_chain(tr, tr + 400, T, lane);
+          nrm[lane] = (float)sqrt((double)a.Ex[(size_t)f * kBands + lane] / (1e-8 + (double)newE));
+        }
+        wfft::wsync();
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const int n = 64 * r + lane;
+          if (n < kFreq) {
+            const float nf = interp_gain_t(nrm, T, n);
+            xv[r].x *= nf;
+            xv[r].y *= nf;
+            const float gf = interp_gain_t(gsm, T, n);
+            xv[r].x *= gf;
+            xv[r].y *= gf;
+          }
+        }
+      }
+      // Hermitian extension, gathered into layout A through the region
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        if (64 * r + lane < kFreq) R[64 * r + lane] = xv[r];
+      wfft::wsync();
+      float2 v[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int i = wfft::in_index(lane, k);
+        float2 val = make_float2(0, 0);
+        if (lane < 60) {
+          if (i < kFreq) {
+            val = R[i];
+          } else {
+            const float2 c = R[kWin - i];
+            val = make_float2(c.x, -c.y);
+          }
+        }
+        v[k] = make_float2(kScale960 * val.x, kScale960 * val.y);
+      }
+      wfft::wsync();
+      wfft::run(v, tw, tb.tw, R, lane);
+      float *y = a.ys + (size_t)f * kWin;
+#pragma unroll
+      for (int r = 0; r < 15; r++) {
+        const int n = 64 * r + lane;
+        const int i = (n == 0) ? 0 : kWin - n;
+        const float yv = kWin * v[r].x;
+        y[i] = yv * win960(tb.hw, i);
+      }
+      wfft::wsync();
+    }
+  }
+}
+
 const char *staged_kernel_name(int i) {
   static const char *const names[kStagedKernels] = {"k_prep3", "k_fftA", "k_plpc",  "k_pcorr",   "k_select", "k_pspec",
                                                      "k_rnn2",   "k_synth", "k_ola", "k_winmeta", "k_fftb"};
@@ -2476,11 +2789,20 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   static const int g_pspec = resident_blocks(k_pspec<FF>, 256, n_cu);
   static const int g_synth = resident_blocks(k_synth<FF>, 256, n_cu);
   static const int g_plpc = resident_blocks(k_plpc, 256, n_cu);
+  static const int g_fftAw = resident_blocks(k_fftAw, 64 * kWNW, n_cu);
+  static const int g_pspecw = resident_blocks(k_pspecw, 64 * kWNW, n_cu);
+  static const int g_synthw = resident_blocks(k_synthw, 64 * kWNW, n_cu);
+  // FVAD_WFFT=0 selects the workgroup-per-4-frames FFT kernels (comparison)
+  static const bool wfft = [] {
+    const char *v = getenv("FVAD_WFFT");
+    return !(v && atoi(v) == 0);
+  }();
   static const int g_pcorr = resident_blocks(k_pcorr, 256, n_cu);
   // lane-per-stream kernels: 16 streams per workgroup spreads the serial
   // chains over more CUs (each chain is latency-bound, not lane-bound)
   const int lane_blocks = (a.n_streams + 15) / 16;
   const long long frames = (long long)a.n_streams * a.V;
+  const long long wbatches = (frames + kWB - 1) / kWB;
   auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
   (void)hipGetLastError();
   static_assert(kWorkSlots * kQueues <= kWorkCounters, "work counters");
@@ -2497,7 +2819,10 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   (void)hipEventRecord(st.fork, stream);
   (void)hipStreamWaitEvent(st.aux, st.fork, 0);
   rec_aux(2);
-  hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, st.aux, a);
+  if (wfft)
+    hipLaunchKernelGGL(k_fftAw, grid(wbatches, g_fftAw), dim3(64 * kWNW), 0, st.aux, a);
+  else
+    hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, st.aux, a);
   rec_aux(3);
   (void)hipEventRecord(st.join, st.aux);
   {
@@ -2512,12 +2837,18 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   rec(6);
   (void)hipStreamWaitEvent(stream, st.join, 0);  // join
   rec(7);
-  hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
+  if (wfft)
+    hipLaunchKernelGGL(k_pspecw, grid(wbatches, g_pspecw), dim3(64 * kWNW), 0, stream, a);
+  else
+    hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
   rec(8);
   hipLaunchKernelGGL((k_rnn2<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
                      stream, a);
   rec(9);
-  hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
+  if (wfft)
+    hipLaunchKernelGGL(k_synthw, grid(wbatches, g_synthw), dim3(64 * kWNW), 0, stream, a);
+  else
+    hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
   rec(10);
   const long long ola_threads = frames * kFrame;
   hipLaunchKernelGGL(k_ola, dim3((unsigned)((ola_threads + 255) / 256)), dim3(256), 0, stream, a);
