@@ -510,6 +510,14 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.model = e->d_model;
   a.n_bands = c.n_bands;
   fill_bands(c, a.band_lo, a.band_hi, &a.bin_lo_all, &a.bin_hi_all);
+  a.nfft_b = c.fft_size;
+  // wave kernels with static batch striding (bit 1 << fvad::WaveKernel):
+  // k_pspecw and k_synthw by default; FVAD_WSTATIC=<mask> overrides
+  static const int wstatic = [] {
+    const char *v = getenv("FVAD_WSTATIC");
+    return v ? atoi(v) : (1 << fvad::kWavePspec) | (1 << fvad::kWaveSynth);
+  }();
+  a.wave_static = wstatic;
   a.out_vad = e->d_vad;
   a.out_win_ratio = e->d_wratio;
   a.out_win_vad = e->d_wvad;

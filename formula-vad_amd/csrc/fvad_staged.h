@@ -87,6 +87,8 @@ struct StagedArgs {
   const Plan *plan;
   const DevModel *model;
   int n_bands;
+  int nfft_b;                  // FFT B size (fft_size)
+  int wave_static;             // wave kernels with static batch striding: bit 1 << WaveKernel
   int band_lo[kMaxBandCfg], band_hi[kMaxBandCfg];
   int bin_lo_all, bin_hi_all;
   float *out_vad, *out_win_ratio, *out_win_vad, *out_band, *out_den;
@@ -116,6 +118,10 @@ hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev);
 // recorded.
 hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev);
 const char *staged_kernel_name(int i);
+// The wave-per-frame FFT kernels (fvad_wave.hip), persistent grids; kWaveFftB
+// needs fft_size 2048 (a 1024-point complex transform).
+enum WaveKernel { kWaveFftA, kWavePspec, kWaveSynth, kWaveFftB };
+hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream);
 // Device VADMachines over the window outputs a.out_* of one push: overlap =
 // the light HBM variant meant to co-run with the next push on a side stream.
 hipError_t launch_vadm(const StagedArgs &a, bool overlap, hipStream_t stream);

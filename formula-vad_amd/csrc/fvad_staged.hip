@@ -37,7 +37,7 @@
 #include "fvad_device.h"
 #include "fvad_internal.h"
 #include "fvad_staged.h"
-#include "fvad_wfft.h"
+#include "fvad_staged_dev.h"
 
 namespace fvad {
 
@@ -74,8 +74,6 @@ namespace fvad {
 #endif
 
 namespace {
-constexpr int kHist = kPitchBuf - kFrame;  // 1248
-constexpr float kScale960 = 1.f / 960;
 // LDS row pitch of the 960-point transforms (float2): frames 16 banks apart,
 // so band-sum lanes of different frames reading the same bin do not conflict
 constexpr int kWinP = kWin + 8;
@@ -83,28 +81,6 @@ constexpr int kWinP = kWin + 8;
 constexpr int kTermOff = 964;  // float offset in a W row (16-byte aligned; + 800 <= 2 * kWinP)
 static_assert(kTermOff >= 2 * kFreq && kTermOff % 4 == 0 && kTermOff + 800 <= 2 * kWinP, "band term area");
 
-__device__ __forceinline__ int ticks_of(const StagedArgs &a, int s) {
-  return a.ticks_valid ? a.ticks_valid[s] : a.n_ticks;
-}
-
-// Dynamic group scheduling of the persistent kernels: a workgroup takes the
-// index of its next group from one of 8 queues (queue x serves groups x,
-// x + 8, x + 16, ... and the workgroups with blockIdx % 8 == x, i.e. one XCD's
-// under round-robin dispatch, which keeps each counter's atomics local and
-// few).  A workgroup that starts late -- beside another kernel's waves --
-// just takes fewer groups instead of stretching the launch with a tail.
-// The counters a.work[slot][8] are zeroed on the stream before every launch.
-constexpr int kQueues = 8;
-enum WorkSlot { kWorkFftA = 0, kWorkPlpc, kWorkPcorr, kWorkPspec, kWorkSynth, kWorkSlots };
-__device__ __forceinline__ long long take_group(const StagedArgs &a, int slot) {
-  const int x = blockIdx.x % kQueues;
-  return x + (long long)kQueues * atomicAdd(&a.work[slot * kQueues + x], 1u);
-}
-
-// analysis / synthesis window value for index i of the 960-sample window
-__device__ __forceinline__ float win960(const float *__restrict__ hw, int i) {
-  return (i < kFrame) ? hw[i] : hw[kWin - 1 - i];
-}
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -295,17 +271,6 @@ __device__ __forceinline__ void group_frames(const StagedArgs &a, long long g, i
     }
     fidx[tid] = ok;
   }
-}
-__device__ __forceinline__ const float *frame_pb(const StagedArgs &a, int f) {
-  const int s = f / a.V, v = f - s * a.V;
-  return a.xs + (size_t)s * a.L + (size_t)v * kFrame;
-}
-// frame index of slot fr of group g, or -1 (same rule as group_frames)
-__device__ __forceinline__ int frame_of(const StagedArgs &a, long long g, int F, int fr) {
-  const long long f = g * F + fr;
-  if (f >= (long long)a.n_streams * a.V) return -1;
-  const int s = (int)(f / a.V), v = (int)(f - (long long)s * a.V);
-  return v < ticks_of(a, s) * a.n_channels ? (int)f : -1;
 }
 // This thread's 4 samples of the 960-sample analysis window of every frame of
 // group g (issued one group ahead so the HBM latency hides behind the work)
@@ -1922,6 +1887,311 @@ __global__ void __launch_bounds__(NT) k_rnn2(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_rnn3: k_rnn2's recurrence with 4 streams per lane (G = 2: one column's
+// 8 streams on two lanes) and a two-phase layer pipeline.  A lane's inputs
+// for one term are one 16-byte LDS read (ds_read_b128, full LDS rate; the
+// float2 reads of G = 4 were paired into half-rate ds_read2_b64) and one
+// int8 -> f32 conversion serves 4 streams.  Step t:
+//   P1  z|r gates of vad(t-1), noise(t-2), denoise(t-3); features of t+1
+//       (cepstral memory, deltas, distance row); gain smoothing of t-5
+//   P2  candidates of vad(t-1), noise(t-2), denoise(t-3); dense(t);
+//       denoise_output(t-4); vad_output(t-2); spectral variability of t+1;
+//       next features -> LDS
+// Two barriers per step.  Every term keeps its C order; buffers are rings
+// indexed by frame (features 8, dense/vad state 4, noise/denoise state 2).
+// ---------------------------------------------------------------------------
+constexpr int kR3S = 8, kR3G = 2, kR3NT = 1024;
+__global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
+  constexpr int S = kR3S, G = kR3G, NT = kR3NT;
+  struct Lds {
+    alignas(16) float featT[8][44 * S];  // frame f in slot f & 7
+    alignas(16) float doutT[4][24 * S];
+    alignas(16) float gvT[4][24 * S];
+    alignas(16) float gnT[2][48 * S];
+    alignas(16) float gdT[2][96 * S];
+    alignas(16) float zrv[48 * S], zrn[96 * S], zrd[192 * S];
+    alignas(16) float gout[22 * S];
+    alignas(16) float vo[S];  // vad_output of the frame P2 computed last
+    float tt[204];
+    float ceps[S][kCeps * kBands];
+    float dist[S][kCeps * kCeps];
+    float lastg[S][kBands];
+    float pf[S][kRnnPf];  // features of the frame the next F-C stage reads
+    int act[8][S];        // frame f in slot f & 7: valid and not silent
+    int memid[S], nfs[S];
+    long long fbase[S];
+    alignas(16) int8_t W[rnnimg::kBytes];
+  };
+  __shared__ Lds L;
+  const int tid = threadIdx.x;
+  const int sb = blockIdx.x * S;
+  const int *ra = a.rnn_act;
+  {
+    const int4 *src = reinterpret_cast<const int4 *>(a.rnn_img);
+    int4 *dst = reinterpret_cast<int4 *>(L.W);
+    for (int i = tid; i < rnnimg::kBytes / 16; i += NT) dst[i] = src[i];
+    for (int i = tid; i < 201; i += NT) L.tt[i] = a.plan->tansig[i];
+  }
+  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
+    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
+    L.ceps[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] : 0.0f;
+  }
+  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
+    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
+    L.dist[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] : 0.0f;
+  }
+  for (int idx = tid; idx < S * kBands; idx += NT) {
+    const int s = idx / kBands, i = idx - s * kBands;
+    L.lastg[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] : 0.0f;
+  }
+  // states before frame 0 = "frame -1": gv slot 3, gn / gd slot 1
+  for (int idx = tid; idx < S * 96; idx += NT) {
+    const int s = idx / 96, i = idx - s * 96;
+    const bool ok = sb + s < a.n_streams;
+    const float *stp = a.state + (size_t)(sb + s) * st::kWords;
+    if (i < 24) L.gvT[3][i * S + s] = ok ? stp[st::kVadGru + i] : 0.0f;
+    if (i < 48) L.gnT[1][i * S + s] = ok ? stp[st::kNoiseGru + i] : 0.0f;
+    L.gdT[1][i * S + s] = ok ? stp[st::kDenGru + i] : 0.0f;
+  }
+  if (tid < 8 * S) L.act[tid / S][tid % S] = 0;
+  if (tid < S) {
+    const int s = sb + tid;
+    const bool ok = s < a.n_streams;
+    L.memid[tid] = ok ? reinterpret_cast<const int *>(a.state)[(size_t)s * st::kWords + st::kMemId] : 0;
+    L.nfs[tid] = ok ? ticks_of(a, s) * a.n_channels : 0;
+    L.fbase[tid] = (long long)s * a.V;
+  }
+  __syncthreads();
+  int maxnf = 0;
+#pragma unroll
+  for (int s = 0; s < S; s++) maxnf = max(maxnf, L.nfs[s]);
+  // prefetch lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (as 1.0 / 0.0)
+  const int pfs = tid / kRnnPf, pfi = tid - pfs * kRnnPf;
+  const bool pf_lane = tid < S * kRnnPf;
+  auto fetch = [&](int v) -> float {
+    if (!pf_lane || v >= L.nfs[pfs]) return 1.0f;  // past the end: treated as silent (inactive)
+    const long long f = L.fbase[pfs] + v;
+    if (pfi < kBands) return a.Lyf[f * kBands + pfi];
+    if (pfi < kBands + 7) return a.f34[f * 8 + (pfi - kBands)];
+    return a.silence[f] ? 1.0f : 0.0f;
+  };
+  // F-C: frame f's features from L.pf (cepstral memory, deltas, 34..40, the
+  // new distance row); item (s, i), i < 37; item i == 0 records act(f)
+  auto feat_c = [&](int f, int idx) {
+    const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
+    const bool valid = f < L.nfs[s];
+    const bool on = valid && L.pf[s][kRnnPf - 1] == 0.0f;
+    if (i == 0) {
+      L.act[f & 7][s] = on;
+      if (valid && !on) a.vadf[L.fbase[s] + f] = 0;  // silent: X passes through, state untouched
+    }
+    if (!on) return;
+    float *featT = L.featT[f & 7];
+    const int mi = L.memid[s];
+    const float *c0 = L.pf[s];  // ceps_0 (the row being written at memid)
+    if (i < kBands) {
+      L.ceps[s][mi * kBands + i] = c0[i];
+      if (i < 6) {
+        const float *c1 = L.ceps[s] + ((mi < 1) ? kCeps + mi - 1 : mi - 1) * kBands;
+        const float *c2 = L.ceps[s] + ((mi < 2) ? kCeps + mi - 2 : mi - 2) * kBands;
+        featT[i * S + s] = c0[i] + c1[i] + c2[i];
+        featT[(kBands + i) * S + s] = c0[i] - c2[i];
+        featT[(kBands + 6 + i) * S + s] = c0[i] - 2 * c1[i] + c2[i];
+      } else {
+        featT[i * S + s] = c0[i];
+      }
+    } else if (i < kBands + 7) {
+      featT[(34 + i - kBands) * S + s] = c0[i];
+    } else {
+      const int j = i - kBands - 7;
+      if (j != mi) {
+        const float *cj = L.ceps[s] + j * kBands;
+        float d = 0;
+#pragma unroll
+        for (int k = 0; k < kBands; k++) {
+          const float tmp = c0[k] - cj[k];
+          d += tmp * tmp;
+        }
+        L.dist[s][mi * kCeps + j] = d;
+        L.dist[s][j * kCeps + mi] = d;
+      }
+    }
+  };
+  // F-D: spectral variability of frame f, stream s
+  auto feat_d = [&](int f, int s) {
+    if (!L.act[f & 7][s]) return;
+    float sv = 0;
+    for (int i = 0; i < kCeps; i++) {
+      float mindist = 1e15f;
+      for (int j = 0; j < kCeps; j++)
+        if (j != i) mindist = (mindist < L.dist[s][i * kCeps + j]) ? mindist : L.dist[s][i * kCeps + j];
+      sv += mindist;
+    }
+    L.featT[f & 7][41 * S + s] = (float)(sv / kCeps - 2.1);
+    int mid = L.memid[s] + 1;
+    if (mid == kCeps) mid = 0;
+    L.memid[s] = mid;
+  };
+  // prologue: features of frame 0; frame 1's staged
+  if (pf_lane) L.pf[pfs][pfi] = fetch(0);
+  __syncthreads();
+  for (int idx = tid; idx < S * (kBands + 7 + kCeps); idx += NT) feat_c(0, idx);
+  __syncthreads();
+  if (tid < S) feat_d(0, tid);
+  if (pf_lane) L.pf[pfs][pfi] = fetch(1);
+  __syncthreads();
+  // P1 thread plan: denoise z|r tasks 0..383, noise z|r 0..191, vad z|r 0..95,
+  // then features (296 items) and gains (176 items)
+  constexpr int kP1Den = 0, kP1Noise = 384, kP1Vad = 576, kP1Feat = 672, kP1Gain = 968;
+  // P2: denoise h 0..191, noise h 0..95, vad h 0..47, dense 0..47,
+  // denoise_output 0..43, vad_output (one lane, 8 streams), spectral variability
+  constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 288, kP2Dense = 336, kP2Out = 384, kP2VadOut = 428,
+                kP2Var = 448;
+  STAMP_INIT();
+#ifdef FVAD_STAMPS
+  // role finish times: the first thread of each role adds (its role's end -
+  // its phase start) to stamps[2 + role]
+  unsigned long long ph0 = 0, racc = 0;
+  int rslot = -1;
+  {
+    const int l1[5] = {kP1Den, kP1Noise, kP1Vad, kP1Feat, kP1Gain};
+    const int l2[7] = {kP2Den, kP2Noise, kP2Vad, kP2Dense, kP2Out, kP2VadOut, kP2Var};
+    for (int i = 0; i < 5; i++)
+      if (tid == l1[i]) rslot = i;
+    for (int i = 0; i < 7; i++)
+      if (tid == l2[i]) rslot = (rslot < 0) ? 16 + i : rslot;  // tid 0 / 384 lead in both phases
+  }
+  unsigned long long racc2[2] = {0, 0};
+#define ROLE_BEGIN() ph0 = __builtin_amdgcn_s_memtime()
+#define ROLE_END(ph) racc2[ph] += __builtin_amdgcn_s_memtime() - ph0
+#else
+#define ROLE_BEGIN() \
+  do {               \
+  } while (0)
+#define ROLE_END(ph) \
+  do {               \
+  } while (0)
+#endif
+  for (int t = 0; t <= maxnf + 4; t++) {
+    const int fv = t - 1, fn = t - 2, fd = t - 3;
+    ROLE_BEGIN();
+    // frame t+2's features, staged at the end of this step: issued here, so
+    // no load is outstanding across a step boundary (a loop-carried register
+    // would make the step's last barrier wait for it)
+    const float pf_now = fetch(t + 2);
+    // ---- P1
+    if (tid < kP1Noise) {
+      if (fd >= 0 && fd < maxnf)
+        rnn_gates<5, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, L.gdT[(fd + 1) & 1], L.zrd,
+                              kActSigmoid, L.tt, tid - kP1Den);
+    } else if (tid < kP1Vad) {
+      if (fn >= 0 && fn < maxnf)
+        rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
+                              kActSigmoid, L.tt, tid - kP1Noise);
+    } else if (tid < kP1Feat) {
+      if (fv >= 0 && fv < maxnf)
+        rnn_gates<1, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, kActSigmoid,
+                              L.tt, tid - kP1Vad);
+    } else if (tid < kP1Gain) {
+      if (t + 1 < maxnf) feat_c(t + 1, tid - kP1Feat);
+    } else if (tid < kP1Gain + 48) {  // gain smoothing g = max(g, .6*lastg) (denoise.c), frame t-5
+      const int f5 = t - 5;
+      for (int idx = tid - kP1Gain; f5 >= 0 && idx < S * kBands; idx += 48) {
+        const int s = idx / kBands, i = idx - s * kBands;
+        if (!L.act[f5 & 7][s]) continue;
+        const long long f = L.fbase[s] + f5;
+        const float gi = L.gout[i * S + s];
+        const float al = .6f * L.lastg[s][i];
+        const float gsm = (gi > al) ? gi : al;
+        L.lastg[s][i] = gsm;
+        a.gr[f * kBands + i] = gi;
+        a.gs[f * kBands + i] = gsm;
+      }
+    } else if (tid < kP1Gain + 48 + S) {  // vad_output of frame t-3 (P2 of step t-1)
+      const int s = tid - kP1Gain - 48, fw = t - 3;
+      if (fw >= 0 && fw < maxnf && L.act[fw & 7][s]) a.vadf[L.fbase[s] + fw] = L.vo[s];
+    }
+    ROLE_END(0);
+    __syncthreads();
+    RSTAMP(0);
+    ROLE_BEGIN();
+    // ---- P2
+    const int fo = t - 4;
+    if (tid < kP2Noise) {
+      if (fd >= 0 && fd < maxnf)
+        rnn_cand<6, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, L.gdT[(fd + 1) & 1], L.zrd,
+                             L.gdT[fd & 1], L.act[fd & 7], ra[6], L.tt, tid - kP2Den);
+    } else if (tid < kP2Vad) {
+      if (fn >= 0 && fn < maxnf)
+        rnn_cand<4, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
+                             L.gnT[fn & 1], L.act[fn & 7], ra[4], L.tt, tid - kP2Noise);
+    } else if (tid < kP2Dense) {
+      if (fv >= 0 && fv < maxnf)
+        rnn_cand<2, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, L.gvT[fv & 3],
+                             L.act[fv & 7], ra[2], L.tt, tid - kP2Vad);
+    } else if (tid < kP2Out) {
+      if (t < maxnf)
+        rnn_gates<0, S, G, 0>(L.W, RnnIn{L.featT[t & 7], nullptr, nullptr}, nullptr, L.doutT[t & 3], ra[0], L.tt,
+                              tid - kP2Dense);
+    } else if (tid < kP2VadOut) {
+      if (fo >= 0 && fo < maxnf)
+        rnn_gates<7, S, G, 0>(L.W, RnnIn{L.gdT[fo & 1], nullptr, nullptr}, nullptr, L.gout, ra[7], L.tt, tid - kP2Out);
+    } else if (tid < kP2VadOut + G) {
+      // vad_output(t-2) -> L.vo, stored by the next step's P1
+      if (fn >= 0 && fn < maxnf)
+        rnn_gates<8, S, G, 0>(L.W, RnnIn{L.gvT[fn & 3], nullptr, nullptr}, nullptr, L.vo, ra[8], L.tt,
+                              tid - kP2VadOut);
+    } else if (tid >= kP2Var && tid < kP2Var + S) {
+      if (t + 1 < maxnf) feat_d(t + 1, tid - kP2Var);
+    }
+    ROLE_END(1);
+    if (pf_lane) L.pf[pfs][pfi] = pf_now;
+    __syncthreads();
+    RSTAMP(1);
+  }
+  STAMP_FLUSH(0, 2);
+#ifdef FVAD_STAMPS
+  // P1 roles -> stamps[2..6], P2 roles -> stamps[8..14] (tid 0 and 384 lead a
+  // role in both phases)
+  if (a.stamps) {
+    const int p1[5] = {kP1Den, kP1Noise, kP1Vad, kP1Feat, kP1Gain};
+    const int p2[7] = {kP2Den, kP2Noise, kP2Vad, kP2Dense, kP2Out, kP2VadOut, kP2Var};
+    for (int i = 0; i < 5; i++)
+      if (tid == p1[i]) atomicAdd(&a.stamps[2 + i], racc2[0]);
+    for (int i = 0; i < 7; i++)
+      if (tid == p2[i]) atomicAdd(&a.stamps[8 + i], racc2[1]);
+  }
+  (void)racc;
+  (void)rslot;
+#endif
+#undef ROLE_BEGIN
+#undef ROLE_END
+  const int fin = maxnf - 1;  // the slots of the latest states ("frame -1" if there were none)
+  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
+    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
+    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] = L.ceps[s][i];
+  }
+  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
+    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
+    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] = L.dist[s][i];
+  }
+  for (int idx = tid; idx < S * kBands; idx += NT) {
+    const int s = idx / kBands, i = idx - s * kBands;
+    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] = L.lastg[s][i];
+  }
+  for (int idx = tid; idx < S * 96; idx += NT) {
+    const int s = idx / 96, i = idx - s * 96;
+    if (sb + s >= a.n_streams || L.nfs[s] <= 0) continue;
+    float *stp = a.state + (size_t)(sb + s) * st::kWords;
+    if (i < 24) stp[st::kVadGru + i] = L.gvT[fin & 3][i * S + s];
+    if (i < 48) stp[st::kNoiseGru + i] = L.gnT[fin & 1][i * S + s];
+    stp[st::kDenGru + i] = L.gdT[fin & 1][i * S + s];
+  }
+  if (tid < S && sb + tid < a.n_streams && L.nfs[tid] > 0)
+    reinterpret_cast<int *>(a.state)[(size_t)(sb + tid) * st::kWords + st::kMemId] = L.memid[tid];
+}
+
+// ---------------------------------------------------------------------------
 // k_synth: pitch_filter + gain application (no recurrence left once g / the
 // smoothed gains are known), then the inverse transform (forward FFT of the
 // Hermitian extension) and the synthesis window
@@ -2444,321 +2714,19 @@ __global__ void __launch_bounds__(64) k_vadm(StagedArgs a) {
 // ---------------------------------------------------------------------------
 // launcher
 // ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// Wave-per-frame frame kernels (k_fftAw, k_pspecw, k_synthw): one wave owns a
-// frame at a time and runs its 960-point transform in registers (fvad_wfft.h)
-// with its own LDS region, so a workgroup never waits at a barrier between
-// FFT stages; band terms go to the same region once the transform is done and
-// the 22 band chains run on lanes 0..21 (k_pspecw: Ep on 0..21 beside Exp on
-// 32..53).  Same arithmetic as k_fftA / k_pspec / k_synth.  Frames are taken
-// in batches of kWB consecutive frames per wave (dynamic, per-XCD queues as
-// take_group); k_fftAw runs each batch's serial Ly chains lane per frame.
-// ---------------------------------------------------------------------------
-constexpr int kWB = 8;   // frames per wave batch
-constexpr int kWNW = 4;  // waves per workgroup
-constexpr int kWOcc = 3;  // workgroups per CU (<= 168 VGPRs, <= 53 KB LDS)
-
-__device__ __forceinline__ long long wave_take(const StagedArgs &a, int slot, int lane) {
-  const int x = blockIdx.x % kQueues;
-  unsigned v = 0;
-  if (lane == 0) v = atomicAdd(&a.work[slot * kQueues + x], 1u);
-  v = __shfl(v, 0);
-  return x + (long long)kQueues * v;
-}
-
-// A per-iteration zero the compiler cannot see through: table reads indexed
-// with it stay inside the frame loop instead of being hoisted into registers
-// for the whole kernel (which would cost occupancy).
-__device__ __forceinline__ int opaque0() {
-  int z = 0;
-  asm volatile("" : "+s"(z));
-  return z;
-}
-
-struct WaveTabs {
-  BandTab T;
-  wfft::TwTab tw;
-  float hw[kFrame];
-};
-__device__ __forceinline__ void wave_tabs_load(WaveTabs &w, const Plan *__restrict__ P, int tid) {
-  bandtab_load(w.T, P, tid, 64 * kWNW);
-  wfft::load_twtab(w.tw, reinterpret_cast<const float2 *>(P->tw960), tid, 64 * kWNW);
-  for (int i = tid; i < kFrame; i += 64 * kWNW) w.hw[i] = P->half_window[i];
-}
-
-// layout-A input of a 960-sample analysis window at pb (x * w / 960, imag 0)
-__device__ __forceinline__ void wave_window(const float *__restrict__ pb, const float *hw, int lane,
-                                            float2 (&v)[16]) {
-  hw += opaque0();
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int i = wfft::in_index(lane, k);
-    float val = lane < 60 ? pb[i] : 0.0f;
-    val *= lane < 60 ? win960(hw, i) : 0.0f;
-    v[k] = make_float2(kScale960 * val, kScale960 * 0.0f);
-  }
-}
-
-__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
-  __shared__ WaveTabs tb;
-  __shared__ float exb[kWNW][kWB][kBands + 2], lyb[kWNW][kWB][kBands + 2];
-  __shared__ int silb[kWNW][kWB];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  wave_tabs_load(tb, a.plan, tid);
-  wfft::Tw tw;
-  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
-  __syncthreads();
-  const BandTab &T = tb.T;
-  float2 *R = Rg[wv];
-  float *tr = reinterpret_cast<float *>(R);
-  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
-  for (long long g = wave_take(a, kWorkFftA, lane); g < nb; g = wave_take(a, kWorkFftA, lane)) {
-    for (int fr = 0; fr < kWB; fr++) {
-      const int f = frame_of(a, g, kWB, fr);
-      if (f < 0) continue;
-      float2 v[16];
-      wave_window(frame_pb(a, f) + (kPitchBuf - kWin), tb.hw, lane, v);
-      wfft::run(v, tw, tb.tw, R, lane);
-      float2 *X = a.X + (size_t)f * kFreq;
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-        if (64 * r + lane < kFreq) X[64 * r + lane] = v[r];
-#pragma unroll
-      for (int r = 0; r < 7; r++) {
-        const int n = 64 * r + lane;
-        if (n < 400) band_terms(v[r], v[r], T, n, tr[n], tr[400 + n]);
-      }
-      wfft::wsync();
-      if (lane < kBands) {
-        const float ex = band_chain(tr, tr + 400, T, lane);
-        a.Ex[(size_t)f * kBands + lane] = ex;
-        exb[wv][fr][lane] = ex;
-        lyb[wv][fr][lane] = (float)log10(1e-2 + (double)ex);
-      }
-      wfft::wsync();
-    }
-    // the Ly floor chain and the silence gate, lane per frame
-    if (lane < kWB) {
-      const int f = frame_of(a, g, kWB, lane);
-      if (f >= 0) {
-        float *Ly = lyb[wv][lane];
-        const float *Exl = exb[wv][lane];
-        float logMax = -2, follow = -2, E = 0;
-        for (int i = 0; i < kBands; i++) {
-          const float ly0 = Ly[i];
-          const double bb = (follow - 1.5 > (double)ly0) ? follow - 1.5 : (double)ly0;
-          const double aa = ((double)(logMax - 7) > bb) ? (double)(logMax - 7) : bb;
-          const float ly = (float)aa;
-          Ly[i] = ly;
-          logMax = (logMax > ly) ? logMax : ly;
-          follow = (float)((follow - 1.5 > (double)ly) ? follow - 1.5 : (double)ly);
-          E += Exl[i];
-        }
-        const int sil = ((double)E < 0.04) ? 1 : 0;
-        silb[wv][lane] = sil;
-        a.silence[f] = sil;
-      }
-    }
-    wfft::wsync();
-    for (int idx = lane; idx < kWB * kBands; idx += 64) {
-      const int fr = idx / kBands, b = idx - fr * kBands;
-      const int f = frame_of(a, g, kWB, fr);
-      if (f >= 0 && !silb[wv][fr]) {
-        const float *Ly = lyb[wv][fr];
-        float sum = 0;
-#pragma unroll
-        for (int j = 0; j < kBands; j++) sum += Ly[j] * T.dct[j * kBands + b];
-        float val = (float)(sum * sqrt(2. / 22));
-        if (b == 0) val -= 12;
-        if (b == 1) val -= 4;
-        a.Lyf[(size_t)f * kBands + b] = val;
-      }
-    }
-    wfft::wsync();
-  }
-}
-
-__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
-  __shared__ WaveTabs tb;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  wave_tabs_load(tb, a.plan, tid);
-  wfft::Tw tw;
-  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
-  __syncthreads();
-  const BandTab &T = tb.T;
-  float2 *R = Rg[wv];
-  float *tr = reinterpret_cast<float *>(R);
-  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
-  for (long long g = wave_take(a, kWorkPspec, lane); g < nb; g = wave_take(a, kWorkPspec, lane)) {
-    for (int fr = 0; fr < kWB; fr++) {
-      const int f = frame_of(a, g, kWB, fr);
-      if (f < 0) continue;
-      const int pit = a.pitch[f];
-      // X of bins < 400 (Exp terms), issued before the transform
-      float2 xr[7];
-      const float2 *X = a.X + (size_t)f * kFreq;
-#pragma unroll
-      for (int r = 0; r < 7; r++) xr[r] = (64 * r + lane < 400) ? X[64 * r + lane] : make_float2(0, 0);
-      float2 v[16];
-      wave_window(frame_pb(a, f) + (kPitchBuf - kWin - pit), tb.hw, lane, v);
-      wfft::run(v, tw, tb.tw, R, lane);
-      float2 *P = a.P + (size_t)f * kFreq;
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-        if (64 * r + lane < kFreq) P[64 * r + lane] = v[r];
-#pragma unroll
-      for (int r = 0; r < 7; r++) {
-        const int n = 64 * r + lane;
-        if (n < 400) {
-          band_terms(v[r], v[r], T, n, tr[n], tr[400 + n]);
-          band_terms(xr[r], v[r], T, n, tr[800 + n], tr[1200 + n]);
-        }
-      }
-      wfft::wsync();
-      // Ep chains on lanes 0..21, Exp chains on lanes 32..53
-      const int h = lane >> 5, b = lane & 31;
-      float cv = 0;
-      if (b < kBands) cv = band_chain(tr + 800 * h, tr + 800 * h + 400, T, b);
-      const float expv = __shfl(cv, lane + 32);
-      float e = 0;
-      if (lane < kBands) {
-        const size_t o = (size_t)f * kBands + lane;
-        const float ex = a.Ex[o];
-        e = (float)((double)expv / sqrt(.001 + (double)(ex * cv)));
-        a.Ep[o] = cv;
-        a.Exp[o] = e;
-      }
-      float sum = 0;
-#pragma unroll
-      for (int j = 0; j < kBands; j++)
-        sum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), j)) * T.dct[j * kBands + (lane < 6 ? lane : 0)];
-      if (lane < 6) {
-        float val = (float)(sum * sqrt(2. / 22));
-        if (lane == 0) val = (float)(val - 1.3);
-        if (lane == 1) val = (float)(val - 0.9);
-        a.f34[(size_t)f * 8 + lane] = val;
-      } else if (lane == 6) {
-        a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pit - 300));
-      }
-      wfft::wsync();
-    }
-  }
-}
-
-__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
-  __shared__ WaveTabs tb;
-  __shared__ float bp[kWNW][3][kBands + 2];  // r, nrm, smoothed gains of the wave's frame
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  wave_tabs_load(tb, a.plan, tid);
-  wfft::Tw tw;
-  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
-  __syncthreads();
-  const BandTab &T = tb.T;
-  float2 *R = Rg[wv];
-  float *tr = reinterpret_cast<float *>(R);
-  float *rr = bp[wv][0], *nrm = bp[wv][1], *gsm = bp[wv][2];
-  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
-  for (long long g = wave_take(a, kWorkSynth, lane); g < nb; g = wave_take(a, kWorkSynth, lane)) {
-    for (int fr = 0; fr < kWB; fr++) {
-      const int f = frame_of(a, g, kWB, fr);
-      if (f < 0) continue;
-      const bool fil = !a.silence[f];  // silent frames: X passes through
-      const float2 *X = a.X + (size_t)f * kFreq;
-      const float2 *P = a.P + (size_t)f * kFreq;
-      float2 xv[8];
-#pragma unroll
-      for (int r = 0; r < 8; r++) xv[r] = (64 * r + lane < kFreq) ? X[64 * r + lane] : make_float2(0, 0);
-      if (fil) {
-        float2 pv[8];
-#pragma unroll
-        for (int r = 0; r < 8; r++) pv[r] = (64 * r + lane < kFreq) ? P[64 * r + lane] : make_float2(0, 0);
-        if (lane < kBands) {
-          const size_t o = (size_t)f * kBands + lane;
-          const float Exp = a.Exp[o], gg = a.gr[o], Ex = a.Ex[o], Ep = a.Ep[o];
-          float r;
-          if (Exp > gg)
-            r = 1;
-          else
-            r = (float)((double)((Exp * Exp) * (1 - (gg * gg))) / (.001 + (double)((gg * gg) * (1 - (Exp * Exp)))));
-          float cl = (0 > r) ? 0 : r;
-          cl = (1 < cl) ? 1 : cl;
-          r = (float)sqrt((double)cl);
-          r = (float)((double)r * sqrt((double)Ex / (1e-8 + (double)Ep)));
-          rr[lane] = r;
-          gsm[lane] = a.gs[o];
-        }
-        wfft::wsync();
-        // pitch filter X += r P; band terms of the filtered X
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-          const int n = 64 * r + lane;
-          if (n < kFreq) {
-            const float rf = interp_gain_t(rr, T, n);
-            xv[r].x += rf * pv[r].x;
-            xv[r].y += rf * pv[r].y;
-            if (n < 400) band_terms(xv[r], xv[r], T, n, tr[n], tr[400 + n]);
-          }
-        }
-        wfft::wsync();
-        if (lane < kBands) {
-          const float newE = band_chain(tr, tr + 400, T, lane);
-          nrm[lane] = (float)sqrt((double)a.Ex[(size_t)f * kBands + lane] / (1e-8 + (double)newE));
-        }
-        wfft::wsync();
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-          const int n = 64 * r + lane;
-          if (n < kFreq) {
-            const float nf = interp_gain_t(nrm, T, n);
-            xv[r].x *= nf;
-            xv[r].y *= nf;
-            const float gf = interp_gain_t(gsm, T, n);
-            xv[r].x *= gf;
-            xv[r].y *= gf;
-          }
-        }
-      }
-      // Hermitian extension, gathered into layout A through the region
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-        if (64 * r + lane < kFreq) R[64 * r + lane] = xv[r];
-      wfft::wsync();
-      float2 v[16];
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const int i = wfft::in_index(lane, k);
-        float2 val = make_float2(0, 0);
-        if (lane < 60) {
-          if (i < kFreq) {
-            val = R[i];
-          } else {
-            const float2 c = R[kWin - i];
-            val = make_float2(c.x, -c.y);
-          }
-        }
-        v[k] = make_float2(kScale960 * val.x, kScale960 * val.y);
-      }
-      wfft::wsync();
-      wfft::run(v, tw, tb.tw, R, lane);
-      float *y = a.ys + (size_t)f * kWin;
-#pragma unroll
-      for (int r = 0; r < 15; r++) {
-        const int n = 64 * r + lane;
-        const int i = (n == 0) ? 0 : kWin - n;
-        const float yv = kWin * v[r].x;
-        y[i] = yv * win960(tb.hw, i);
-      }
-      wfft::wsync();
-    }
-  }
-}
-
 const char *staged_kernel_name(int i) {
-  static const char *const names[kStagedKernels] = {"k_prep3", "k_fftA", "k_plpc",  "k_pcorr",   "k_select", "k_pspec",
-                                                     "k_rnn2",   "k_synth", "k_ola", "k_winmeta", "k_fftb"};
+  // the variants launch_staged runs (FVAD_WFFT=0 / FVAD_RNN=2 select the older ones)
+  static const bool wfft = [] {
+    const char *v = getenv("FVAD_WFFT");
+    return !(v && atoi(v) == 0);
+  }();
+  static const bool rnn2 = [] {
+    const char *v = getenv("FVAD_RNN");
+    return v && atoi(v) == 2;
+  }();
+  static const char *const names[kStagedKernels] = {
+      "k_prep3", wfft ? "k_fftAw" : "k_fftA", "k_plpc", "k_pcorr", "k_select", wfft ? "k_pspecw" : "k_pspec",
+      rnn2 ? "k_rnn2" : "k_rnn3", wfft ? "k_synthw" : "k_synth", "k_ola", "k_winmeta", wfft ? "k_fftbw" : "k_fftb"};
   return (i >= 0 && i < kStagedKernels) ? names[i] : nullptr;
 }
 
@@ -2789,9 +2757,6 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   static const int g_pspec = resident_blocks(k_pspec<FF>, 256, n_cu);
   static const int g_synth = resident_blocks(k_synth<FF>, 256, n_cu);
   static const int g_plpc = resident_blocks(k_plpc, 256, n_cu);
-  static const int g_fftAw = resident_blocks(k_fftAw, 64 * kWNW, n_cu);
-  static const int g_pspecw = resident_blocks(k_pspecw, 64 * kWNW, n_cu);
-  static const int g_synthw = resident_blocks(k_synthw, 64 * kWNW, n_cu);
   // FVAD_WFFT=0 selects the workgroup-per-4-frames FFT kernels (comparison)
   static const bool wfft = [] {
     const char *v = getenv("FVAD_WFFT");
@@ -2802,7 +2767,6 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   // chains over more CUs (each chain is latency-bound, not lane-bound)
   const int lane_blocks = (a.n_streams + 15) / 16;
   const long long frames = (long long)a.n_streams * a.V;
-  const long long wbatches = (frames + kWB - 1) / kWB;
   auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
   (void)hipGetLastError();
   static_assert(kWorkSlots * kQueues <= kWorkCounters, "work counters");
@@ -2820,7 +2784,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   (void)hipStreamWaitEvent(st.aux, st.fork, 0);
   rec_aux(2);
   if (wfft)
-    hipLaunchKernelGGL(k_fftAw, grid(wbatches, g_fftAw), dim3(64 * kWNW), 0, st.aux, a);
+    (void)launch_wave(kWaveFftA, a, n_cu, st.aux);
   else
     hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, st.aux, a);
   rec_aux(3);
@@ -2838,15 +2802,23 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   (void)hipStreamWaitEvent(stream, st.join, 0);  // join
   rec(7);
   if (wfft)
-    hipLaunchKernelGGL(k_pspecw, grid(wbatches, g_pspecw), dim3(64 * kWNW), 0, stream, a);
+    (void)launch_wave(kWavePspec, a, n_cu, stream);
   else
     hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
   rec(8);
+  // FVAD_RNN=2 selects k_rnn2 (three phases, 2 streams per lane; comparison)
+  static const bool rnn2 = [] {
+    const char *v = getenv("FVAD_RNN");
+    return v && atoi(v) == 2;
+  }();
+  if (rnn2)
   hipLaunchKernelGGL((k_rnn2<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
                      stream, a);
+  else
+    hipLaunchKernelGGL(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
   rec(9);
   if (wfft)
-    hipLaunchKernelGGL(k_synthw, grid(wbatches, g_synthw), dim3(64 * kWNW), 0, stream, a);
+    (void)launch_wave(kWaveSynth, a, n_cu, stream);
   else
     hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
   rec(10);
@@ -2855,7 +2827,10 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   rec(11);
   hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(16), 0, stream, a);
   rec(12);
-  hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
+  if (wfft && a.nfft_b == 2048)
+    (void)launch_wave(kWaveFftB, a, n_cu, stream);
+  else
+    hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
   rec(13);
   return hipGetLastError();
 }

@@ -1,0 +1,562 @@
+// Wave-per-frame FFT kernels of the staged pipeline (k_fftAw, k_pspecw,
+// k_synthw).  A translation unit of their own: they are built without SLP
+// vectorisation (Makefile), which keeps their f32 arithmetic in single
+// (non-packed) VALU instructions -- measured faster for these kernels, while
+// the GRU kernel in fvad_staged.hip prefers the packed form.
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "fvad_device.h"
+#include "fvad_internal.h"
+#include "fvad_staged.h"
+#include "fvad_staged_dev.h"
+#include "fvad_wfft.h"
+
+namespace fvad {
+
+// ---------------------------------------------------------------------------
+// Wave-per-frame frame kernels (k_fftAw, k_pspecw, k_synthw): one wave owns a
+// frame at a time and runs its 960-point transform in registers (fvad_wfft.h)
+// with its own LDS region, so a workgroup never waits at a barrier between
+// FFT stages; band terms go to the same region once the transform is done and
+// the 22 band chains run on lanes 0..21 (k_pspecw: Ep on 0..21 beside Exp on
+// 32..53).  Same arithmetic as k_fftA / k_pspec / k_synth.  Frames are taken
+// in batches of kWB consecutive frames per wave (dynamic, per-XCD queues as
+// take_group); k_fftAw runs each batch's serial Ly chains lane per frame.
+// ---------------------------------------------------------------------------
+constexpr int kWB = 8;   // frames per wave batch
+constexpr int kWNW = 4;  // waves per workgroup
+constexpr int kWOcc = 3;  // workgroups per CU (<= 168 VGPRs, <= 53 KB LDS)
+
+__device__ __forceinline__ long long wave_take(const StagedArgs &a, int slot, int lane) {
+  const int x = blockIdx.x % kQueues;
+  unsigned v = 0;
+  if (lane == 0) v = atomicAdd(&a.work[slot * kQueues + x], 1u);
+  v = __shfl(v, 0);
+  return x + (long long)kQueues * v;
+}
+
+// Batches of a wave: dynamic (per-XCD queues, wave_take) or static striding
+// over the grid's waves, per kernel (a.wave_static bit 1 << kind).  k_fftAw
+// runs beside the next push's k_prep3 and balances better dynamically; the
+// others run alone, where static striding saves the queue atomics.
+__device__ __forceinline__ bool wave_is_static(const StagedArgs &a, WaveKernel k) { return (a.wave_static >> k) & 1; }
+__device__ __forceinline__ long long wave_first(const StagedArgs &a, WaveKernel k, int slot, int lane) {
+  return wave_is_static(a, k) ? (long long)blockIdx.x * kWNW + (threadIdx.x >> 6) : wave_take(a, slot, lane);
+}
+__device__ __forceinline__ long long wave_next(const StagedArgs &a, WaveKernel k, int slot, int lane, long long g) {
+  return wave_is_static(a, k) ? g + (long long)gridDim.x * kWNW : wave_take(a, slot, lane);
+}
+
+// A per-iteration zero the compiler cannot see through: table reads indexed
+// with it stay inside the frame loop instead of being hoisted into registers
+// for the whole kernel (which would cost occupancy).
+__device__ __forceinline__ int opaque0() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+
+struct WaveTabs {
+  BandTab T;
+  wfft::TwTab tw;
+  float hw[kFrame];
+};
+__device__ __forceinline__ void wave_tabs_load(WaveTabs &w, const Plan *__restrict__ P, int tid) {
+  bandtab_load(w.T, P, tid, 64 * kWNW);
+  wfft::load_twtab(w.tw, reinterpret_cast<const float2 *>(P->tw960), tid, 64 * kWNW);
+  for (int i = tid; i < kFrame; i += 64 * kWNW) w.hw[i] = P->half_window[i];
+}
+
+// layout-A input of a 960-sample analysis window at pb (x * w / 960, imag 0)
+__device__ __forceinline__ void wave_window(const float *__restrict__ pb, const float *hw, int lane,
+                                            float2 (&v)[16]) {
+  hw += opaque0();
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int i = wfft::in_index(lane, k);
+    float val = lane < 60 ? pb[i] : 0.0f;
+    val *= lane < 60 ? win960(hw, i) : 0.0f;
+    v[k] = make_float2(kScale960 * val, kScale960 * 0.0f);
+  }
+}
+
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
+  __shared__ WaveTabs tb;
+  __shared__ float exb[kWNW][kWB][kBands + 2], lyb[kWNW][kWB][kBands + 2];
+  __shared__ int silb[kWNW][kWB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  wave_tabs_load(tb, a.plan, tid);
+  wfft::Tw tw;
+  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
+  __syncthreads();
+  const BandTab &T = tb.T;
+  float2 *R = Rg[wv];
+  float *tr = reinterpret_cast<float *>(R);
+  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
+  for (long long g = wave_first(a, kWaveFftA, kWorkFftA, lane); g < nb; g = wave_next(a, kWaveFftA, kWorkFftA, lane, g)) {
+    for (int fr = 0; fr < kWB; fr++) {
+      const int f = frame_of(a, g, kWB, fr);
+      if (f < 0) continue;
+      float2 v[16];
+      wave_window(frame_pb(a, f) + (kPitchBuf - kWin), tb.hw, lane, v);
+      wfft::run(v, tw, tb.tw, R, lane);
+      float2 *X = a.X + (size_t)f * kFreq;
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        if (64 * r + lane < kFreq) X[64 * r + lane] = v[r];
+#pragma unroll
+      for (int r = 0; r < 7; r++) {
+        const int n = 64 * r + lane;
+        if (n < 400) band_terms(v[r], v[r], T, n, tr[n], tr[400 + n]);
+      }
+      wfft::wsync();
+      if (lane < kBands) {
+        const float ex = band_chain(tr, tr + 400, T, lane);
+        a.Ex[(size_t)f * kBands + lane] = ex;
+        exb[wv][fr][lane] = ex;
+        lyb[wv][fr][lane] = (float)log10(1e-2 + (double)ex);
+      }
+      wfft::wsync();
+    }
+    // the Ly floor chain and the silence gate, lane per frame
+    if (lane < kWB) {
+      const int f = frame_of(a, g, kWB, lane);
+      if (f >= 0) {
+        float *Ly = lyb[wv][lane];
+        const float *Exl = exb[wv][lane];
+        float logMax = -2, follow = -2, E = 0;
+        for (int i = 0; i < kBands; i++) {
+          const float ly0 = Ly[i];
+          const double bb = (follow - 1.5 > (double)ly0) ? follow - 1.5 : (double)ly0;
+          const double aa = ((double)(logMax - 7) > bb) ? (double)(logMax - 7) : bb;
+          const float ly = (float)aa;
+          Ly[i] = ly;
+          logMax = (logMax > ly) ? logMax : ly;
+          follow = (float)((follow - 1.5 > (double)ly) ? follow - 1.5 : (double)ly);
+          E += Exl[i];
+        }
+        const int sil = ((double)E < 0.04) ? 1 : 0;
+        silb[wv][lane] = sil;
+        a.silence[f] = sil;
+      }
+    }
+    wfft::wsync();
+    for (int idx = lane; idx < kWB * kBands; idx += 64) {
+      const int fr = idx / kBands, b = idx - fr * kBands;
+      const int f = frame_of(a, g, kWB, fr);
+      if (f >= 0 && !silb[wv][fr]) {
+        const float *Ly = lyb[wv][fr];
+        float sum = 0;
+#pragma unroll
+        for (int j = 0; j < kBands; j++) sum += Ly[j] * T.dct[j * kBands + b];
+        float val = (float)(sum * sqrt(2. / 22));
+        if (b == 0) val -= 12;
+        if (b == 1) val -= 4;
+        a.Lyf[(size_t)f * kBands + b] = val;
+      }
+    }
+    wfft::wsync();
+  }
+}
+
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
+  __shared__ WaveTabs tb;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  wave_tabs_load(tb, a.plan, tid);
+  wfft::Tw tw;
+  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
+  __syncthreads();
+  const BandTab &T = tb.T;
+  float2 *R = Rg[wv];
+  float *tr = reinterpret_cast<float *>(R);
+  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
+  for (long long g = wave_first(a, kWavePspec, kWorkPspec, lane); g < nb; g = wave_next(a, kWavePspec, kWorkPspec, lane, g)) {
+    for (int fr = 0; fr < kWB; fr++) {
+      const int f = frame_of(a, g, kWB, fr);
+      if (f < 0) continue;
+      const int pit = a.pitch[f];
+      // X of bins < 400 (Exp terms), issued before the transform
+      float2 xr[7];
+      const float2 *X = a.X + (size_t)f * kFreq;
+#pragma unroll
+      for (int r = 0; r < 7; r++) xr[r] = (64 * r + lane < 400) ? X[64 * r + lane] : make_float2(0, 0);
+      float2 v[16];
+      wave_window(frame_pb(a, f) + (kPitchBuf - kWin - pit), tb.hw, lane, v);
+      wfft::run(v, tw, tb.tw, R, lane);
+      float2 *P = a.P + (size_t)f * kFreq;
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        if (64 * r + lane < kFreq) P[64 * r + lane] = v[r];
+#pragma unroll
+      for (int r = 0; r < 7; r++) {
+        const int n = 64 * r + lane;
+        if (n < 400) {
+          band_terms(v[r], v[r], T, n, tr[n], tr[400 + n]);
+          band_terms(xr[r], v[r], T, n, tr[800 + n], tr[1200 + n]);
+        }
+      }
+      wfft::wsync();
+      // Ep chains on lanes 0..21, Exp chains on lanes 32..53
+      const int h = lane >> 5, b = lane & 31;
+      float cv = 0;
+      if (b < kBands) cv = band_chain(tr + 800 * h, tr + 800 * h + 400, T, b);
+      const float expv = __shfl(cv, lane + 32);
+      float e = 0;
+      if (lane < kBands) {
+        const size_t o = (size_t)f * kBands + lane;
+        const float ex = a.Ex[o];
+        e = (float)((double)expv / sqrt(.001 + (double)(ex * cv)));
+        a.Ep[o] = cv;
+        a.Exp[o] = e;
+      }
+      float sum = 0;
+#pragma unroll
+      for (int j = 0; j < kBands; j++)
+        sum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), j)) * T.dct[j * kBands + (lane < 6 ? lane : 0)];
+      if (lane < 6) {
+        float val = (float)(sum * sqrt(2. / 22));
+        if (lane == 0) val = (float)(val - 1.3);
+        if (lane == 1) val = (float)(val - 0.9);
+        a.f34[(size_t)f * 8 + lane] = val;
+      } else if (lane == 6) {
+        a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pit - 300));
+      }
+      wfft::wsync();
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
+  __shared__ WaveTabs tb;
+  __shared__ float bp[kWNW][3][kBands + 2];  // r, nrm, smoothed gains of the wave's frame
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  wave_tabs_load(tb, a.plan, tid);
+  wfft::Tw tw;
+  wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
+  __syncthreads();
+  const BandTab &T = tb.T;
+  float2 *R = Rg[wv];
+  float *tr = reinterpret_cast<float *>(R);
+  float *rr = bp[wv][0], *nrm = bp[wv][1], *gsm = bp[wv][2];
+  const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
+  for (long long g = wave_first(a, kWaveSynth, kWorkSynth, lane); g < nb; g = wave_next(a, kWaveSynth, kWorkSynth, lane, g)) {
+    for (int fr = 0; fr < kWB; fr++) {
+      const int f = frame_of(a, g, kWB, fr);
+      if (f < 0) continue;
+      const bool fil = !a.silence[f];  // silent frames: X passes through
+      const float2 *X = a.X + (size_t)f * kFreq;
+      const float2 *P = a.P + (size_t)f * kFreq;
+      float2 xv[8];
+#pragma unroll
+      for (int r = 0; r < 8; r++) xv[r] = (64 * r + lane < kFreq) ? X[64 * r + lane] : make_float2(0, 0);
+      if (fil) {
+        float2 pv[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) pv[r] = (64 * r + lane < kFreq) ? P[64 * r + lane] : make_float2(0, 0);
+        if (lane < kBands) {
+          const size_t o = (size_t)f * kBands + lane;
+          const float Exp = a.Exp[o], gg = a.gr[o], Ex = a.Ex[o], Ep = a.Ep[o];
+          float r;
+          if (Exp > gg)
+            r = 1;
+          else
+            r = (float)((double)((Exp * Exp) * (1 - (gg * gg))) / (.001 + (double)((gg * gg) * (1 - (Exp * Exp)))));
+          float cl = (0 > r) ? 0 : r;
+          cl = (1 < cl) ? 1 : cl;
+          r = (float)sqrt((double)cl);
+          r = (float)((double)r * sqrt((double)Ex / (1e-8 + (double)Ep)));
+          rr[lane] = r;
+          gsm[lane] = a.gs[o];
+        }
+        wfft::wsync();
+        // pitch filter X += r P; band terms of the filtered X
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const int n = 64 * r + lane;
+          if (n < kFreq) {
+            const float rf = interp_gain_t(rr, T, n);
+            xv[r].x += rf * pv[r].x;
+            xv[r].y += rf * pv[r].y;
+            if (n < 400) band_terms(xv[r], xv[r], T, n, tr[n], tr[400 + n]);
+          }
+        }
+        wfft::wsync();
+        if (lane < kBands) {
+          const float newE = band_chain(tr, tr + 400, T, lane);
+          nrm[lane] = (float)sqrt((double)a.Ex[(size_t)f * kBands + lane] / (1e-8 + (double)newE));
+        }
+        wfft::wsync();
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const int n = 64 * r + lane;
+          if (n < kFreq) {
+            const float nf = interp_gain_t(nrm, T, n);
+            xv[r].x *= nf;
+            xv[r].y *= nf;
+            const float gf = interp_gain_t(gsm, T, n);
+            xv[r].x *= gf;
+            xv[r].y *= gf;
+          }
+        }
+      }
+      // Hermitian extension, gathered into layout A through the region
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        if (64 * r + lane < kFreq) R[64 * r + lane] = xv[r];
+      wfft::wsync();
+      float2 v[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int i = wfft::in_index(lane, k);
+        float2 val = make_float2(0, 0);
+        if (lane < 60) {
+          if (i < kFreq) {
+            val = R[i];
+          } else {
+            const float2 c = R[kWin - i];
+            val = make_float2(c.x, -c.y);
+          }
+        }
+        v[k] = make_float2(kScale960 * val.x, kScale960 * val.y);
+      }
+      wfft::wsync();
+      wfft::run(v, tw, tb.tw, R, lane);
+      float *y = a.ys + (size_t)f * kWin;
+#pragma unroll
+      for (int r = 0; r < 15; r++) {
+        const int n = 64 * r + lane;
+        const int i = (n == 0) ? 0 : kWin - n;
+        const float yv = kWin * v[r].x;
+        y[i] = yv * win960(tb.hw, i);
+      }
+      wfft::wsync();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_fftbw: FFT B (kiss_fftr, nfft 2048 = a 1024-point complex kissfft, radix
+// 4 x 5) of one (stream, completed window, channel) per wave, in registers.
+// Transform index n = d0 + 4 d1 + 16 d2 + 64 d3 + 256 d4; kf_work's leaf
+// copy puts packed input k = rev4(n) at n, and stage s (m = 4^(s-1)) mixes
+// digit d(s-1) with twiddles twb[u fstride], u = n mod m.  Lane layouts:
+//   X  lane = d4 + 4 d3 + 16 d2, registers d1 + 4 d0: input k = lane + 64 r
+//      (coalesced); stages 1, 2
+//   Y  lane = d4 + 4 d0 + 16 d1, registers d2 + 4 d3: stages 3, 4
+//   Z  lane = d0 + 4 d1 + 16 d2, registers d3 + 4 d4: stage 5; register r of
+//      lane l = bin 64 r + l
+// Exchanges through the wave's LDS region (bank-conflict free, bijective):
+//   X -> Y  slot = d4 + 4 d0 + 16 d1 + 64 d2 + 260 d3
+//   Y -> Z  slot = d0 + 4 d1 + 16 d2 + 64 d3 + 260 d4
+// Butterflies are bfly4 (the kissfft kf_bfly4 expressions), twiddles at every
+// stage (kissfft has no degenerate m = 1 case), so results equal k_fftb's.
+// ---------------------------------------------------------------------------
+constexpr int kFbSlots = 1040;  // float2 slots of a wave's region (1036 used)
+constexpr int kFbMag = 256;     // magnitude slots (bin_hi_all - bin_lo_all < 256, host-checked)
+
+struct FbTabs {
+  float2 t4[4][3][16];  // stage 4: [d2][r][u16]: twb[4 (r + 1) (u16 + 16 d2)]
+  float2 t5[4][3][64];  // stage 5: [d3][r][lane]: twb[(r + 1) (lane + 64 d3)]
+};
+
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftbw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][kFbSlots];
+  __shared__ float mg[kWNW][kFbMag];
+  __shared__ FbTabs tb;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const Plan *__restrict__ P = a.plan;
+  const float2 *__restrict__ twb = reinterpret_cast<const float2 *>(P->twb);
+  const float2 *__restrict__ sup = reinterpret_cast<const float2 *>(P->superb);
+  for (int i = tid; i < 4 * 3 * 16; i += 64 * kWNW) {
+    const int d2 = i / 48, r = (i / 16) % 3, u = i % 16;
+    tb.t4[d2][r][u] = twb[4 * (r + 1) * (u + 16 * d2)];
+  }
+  for (int i = tid; i < 4 * 3 * 64; i += 64 * kWNW) {
+    const int d3 = i / 192, r = (i / 64) % 3, l = i % 64;
+    tb.t5[d3][r][l] = twb[(r + 1) * (l + 64 * d3)];
+  }
+  float2 s2[4][3], s3[3];
+#pragma unroll
+  for (int d0 = 0; d0 < 4; d0++)
+#pragma unroll
+    for (int r = 0; r < 3; r++) s2[d0][r] = twb[64 * (r + 1) * d0];
+#pragma unroll
+  for (int r = 0; r < 3; r++) s3[r] = twb[16 * (r + 1) * (lane >> 2)];
+  const float2 tw0 = twb[0];
+  __syncthreads();
+  float2 *R = Rg[wv];
+  float *mag = mg[wv];
+  const int C = a.n_channels, nb = a.n_bands, lo = a.bin_lo_all, hi = a.bin_hi_all;
+  const long long items = (long long)a.n_streams * a.wmax * C;
+  // static assignment: most (stream, slot) items are empty slots, and a queue
+  // atomic per item costs more than the skip
+  const long long nw = (long long)gridDim.x * kWNW;
+  for (long long it = (long long)blockIdx.x * kWNW + wv; it < items; it += nw) {
+    const int c = (int)(it % C);
+    const long long sj = it / C;
+    const int s = (int)(sj / a.wmax), j = (int)(sj - (long long)s * a.wmax);
+    const int t = a.win_tick[(size_t)s * a.wmax + j];
+    if (t < 0) continue;
+    const long long wstart = a.win_start[(size_t)s * a.wmax + j];
+    const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
+    // layout X: register r = d1 + 4 d0 holds packed input k = lane + 64 r
+    float2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int k = lane + 64 * r;
+      const float t0 = ring[(wstart + 2 * k) % a.ring_len] * P->hannb[2 * k];
+      const float t1 = ring[(wstart + 2 * k + 1) % a.ring_len] * P->hannb[2 * k + 1];
+      v[r] = make_float2(t0, t1);
+    }
+    // stage 1 (m = 1, over d0), stage 2 (m = 4, over d1, u = d0)
+#pragma unroll
+    for (int d1 = 0; d1 < 4; d1++) {
+      float2 F[4] = {v[d1], v[d1 + 4], v[d1 + 8], v[d1 + 12]};
+      bfly4(F, 1, tw0, tw0, tw0);
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[d1 + 4 * u] = F[u];
+    }
+#pragma unroll
+    for (int d0 = 0; d0 < 4; d0++) {
+      float2 F[4] = {v[4 * d0], v[4 * d0 + 1], v[4 * d0 + 2], v[4 * d0 + 3]};
+      bfly4(F, 1, s2[d0][0], s2[d0][1], s2[d0][2]);
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[4 * d0 + u] = F[u];
+    }
+    // X -> Y
+    {
+      float2 *w = R + (lane & 3) + 260 * ((lane >> 2) & 3) + 64 * (lane >> 4);  // + 4 d0 + 16 d1
+#pragma unroll
+      for (int r = 0; r < 16; r++) w[4 * (r >> 2) + 16 * (r & 3)] = v[r];
+    }
+    wfft::wsync();
+    {
+      const float2 *rd = R + lane;  // + 64 d2 + 260 d3
+#pragma unroll
+      for (int r = 0; r < 16; r++) v[r] = rd[64 * (r & 3) + 260 * (r >> 2)];
+    }
+    // stage 3 (m = 16, over d2, u = lane >> 2), stage 4 (m = 64, over d3, u = (lane >> 2) + 16 d2)
+#pragma unroll
+    for (int d3 = 0; d3 < 4; d3++) {
+      float2 F[4] = {v[4 * d3], v[4 * d3 + 1], v[4 * d3 + 2], v[4 * d3 + 3]};
+      bfly4(F, 1, s3[0], s3[1], s3[2]);
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[4 * d3 + u] = F[u];
+    }
+#pragma unroll
+    for (int d2 = 0; d2 < 4; d2++) {
+      float2 F[4] = {v[d2], v[d2 + 4], v[d2 + 8], v[d2 + 12]};
+      const int u16 = lane >> 2;
+      bfly4(F, 1, tb.t4[d2][0][u16], tb.t4[d2][1][u16], tb.t4[d2][2][u16]);
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[d2 + 4 * u] = F[u];
+    }
+    wfft::wsync();
+    // Y -> Z
+    {
+      float2 *w = R + (lane >> 2) + 260 * (lane & 3);  // + 16 d2 + 64 d3
+#pragma unroll
+      for (int r = 0; r < 16; r++) w[16 * (r & 3) + 64 * (r >> 2)] = v[r];
+    }
+    wfft::wsync();
+    {
+      const float2 *rd = R + lane;  // + 64 d3 + 260 d4
+#pragma unroll
+      for (int r = 0; r < 16; r++) v[r] = rd[64 * (r & 3) + 260 * (r >> 2)];
+    }
+    // stage 5 (m = 256, over d4, u = lane + 64 d3)
+#pragma unroll
+    for (int d3 = 0; d3 < 4; d3++) {
+      float2 F[4] = {v[d3], v[d3 + 4], v[d3 + 8], v[d3 + 12]};
+      bfly4(F, 1, tb.t5[d3][0][lane], tb.t5[d3][1][lane], tb.t5[d3][2][lane]);
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[d3 + 4 * u] = F[u];
+    }
+    wfft::wsync();
+    // natural order into the region (bins 64 r + lane), then kiss_fftr's
+    // split for the bins the bands use, magnitudes, band sums in bin order
+#pragma unroll
+    for (int r = 0; r < 16; r++) R[64 * r + lane] = v[r];
+    wfft::wsync();
+    const int nc = 1024;
+    for (int k = lo + lane; k <= hi; k += 64) {
+      float re, imv;
+      if (k == 0) {
+        re = R[0].x + R[0].y;
+        imv = 0;
+      } else if (k == nc) {
+        re = R[0].x - R[0].y;
+        imv = 0;
+      } else {
+        const int kk = (k < nc / 2) ? k : nc - k;
+        const float2 fpk = R[kk];
+        const float2 fpnk = make_float2(R[nc - kk].x, -R[nc - kk].y);
+        const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
+        const float2 tw2 = cmul(f2k, sup[kk - 1]);
+        if (k < nc / 2) {
+          re = (f1k.x + tw2.x) * ((float).5);
+          imv = (f1k.y + tw2.y) * ((float).5);
+        } else {
+          re = (f1k.x - tw2.x) * ((float).5);
+          imv = (tw2.y - f1k.y) * ((float).5);
+        }
+      }
+      const float r2 = re * re, i2 = imv * imv;
+      mag[k - lo] = sqrtf(r2 + i2) * P->norm_b;
+    }
+    wfft::wsync();
+    if (lane < nb) {
+      float acc = 0.0f;
+      for (int k = a.band_lo[lane]; k <= a.band_hi[lane]; k++) acc += mag[k - lo];
+      a.out_band[(((size_t)t * a.n_streams + s) * C + c) * nb + lane] = acc;
+    }
+    wfft::wsync();
+  }
+}
+
+namespace {
+template <typename K>
+int wave_resident_blocks(K kernel, int n_cu) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64 * kWNW, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  return per_cu * n_cu;
+}
+}  // namespace
+
+hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream) {
+  static const int g_fftA = wave_resident_blocks(k_fftAw, n_cu);
+  static const int g_pspec = wave_resident_blocks(k_pspecw, n_cu);
+  static const int g_synth = wave_resident_blocks(k_synthw, n_cu);
+  static const int g_fftb = wave_resident_blocks(k_fftbw, n_cu);
+  if (which == kWaveFftB) {
+    const long long items = (long long)a.n_streams * a.wmax * a.n_channels;
+    hipLaunchKernelGGL(k_fftbw, dim3((unsigned)std::min<long long>(std::max<long long>((items + kWNW - 1) / kWNW, 1), g_fftb)),
+                       dim3(64 * kWNW), 0, stream, a);
+    return hipGetLastError();
+  }
+  const long long batches = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
+  // dynamic mode: queue x is served by the blocks with blockIdx % 8 == x, so
+  // the grid covers min(batches, 8) blocks at least; static mode: batches /
+  // kWNW blocks suffice
+  auto grid = [&](int resident) {
+    const long long want = ((a.wave_static >> which) & 1) ? (batches + kWNW - 1) / kWNW : batches;
+    return dim3((unsigned)std::min<long long>(std::max<long long>(want, 1), resident));
+  };
+  if (which == kWaveFftA)
+    hipLaunchKernelGGL(k_fftAw, grid(g_fftA), dim3(64 * kWNW), 0, stream, a);
+  else if (which == kWavePspec)
+    hipLaunchKernelGGL(k_pspecw, grid(g_pspec), dim3(64 * kWNW), 0, stream, a);
+  else
+    hipLaunchKernelGGL(k_synthw, grid(g_synth), dim3(64 * kWNW), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace fvad

@@ -138,6 +138,10 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_vadm": (p["VADMachine share"], (4218 + 4 + 11 + 2) * 4 * FRAME / fft_size / C + 16),
     }
     k["k_vadm_hbm"] = k["k_vadm"]
+    # wave-per-frame / 4-streams-per-lane variants: same algorithmic work
+    for old, new in (("k_fftA", "k_fftAw"), ("k_pspec", "k_pspecw"), ("k_synth", "k_synthw"), ("k_fftb", "k_fftbw"),
+                     ("k_rnn2", "k_rnn3")):
+        k[new] = k[old]
     return {n: {"flops": f, "bytes": b} for n, (f, b) in k.items()}
 
 

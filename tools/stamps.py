@@ -17,7 +17,15 @@ NAMES = ["load state", "pitch shift", "analysis window+scatter", "FFT A (X) + co
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 MODE = sys.argv[3] if len(sys.argv) > 3 else "fused"
-if MODE == "staged" and os.environ.get("FVAD_RNN2", "1") == "1":
+FFTA = []
+if MODE == "staged" and os.environ.get("FVAD_RNN", "3") == "3":
+    NAMES = ["P1 z|r gates + features(t+1) + gains(t-5)",
+             "P2 candidates, dense(t), outputs, spectral variability",
+             "  P1 role: denoise z|r", "  P1 role: noise z|r", "  P1 role: vad z|r", "  P1 role: features",
+             "  P1 role: gains", "", "  P2 role: denoise h", "  P2 role: noise h", "  P2 role: vad h",
+             "  P2 role: dense", "  P2 role: denoise_output", "  P2 role: vad_output", "  P2 role: spectral var"]
+    ROLES = True
+elif MODE == "staged" and os.environ.get("FVAD_RNN") == "2":
     NAMES = ["P1 z|r gates + features(t+1) + gains(t-3)", "P2 candidates + spectral variability",
              "P3 outputs, dense(t+1), vad_out"] + [""] * 9
 elif MODE == "staged":
@@ -38,12 +46,14 @@ e.run_resident(T)
 e.sync()
 buf = (C.c_ulonglong * 64)()
 assert L.fvad_engine_stamps(e.h, buf, 64) == 0
-tot = sum(buf[:24]) if MODE == "fused" else sum(buf[:12])
+tot = sum(buf[:24]) if MODE == "fused" else (sum(buf[:2]) if len(NAMES) > 12 else sum(buf[:12]))
 frames = B * 2 * T
 if MODE == "staged":
     frames = (B // 8) * 2 * T  # k_rnn: one workgroup per 8 streams, stamps = frame steps of thread 0
 print("total stamped cycles per frame step per WG: %.0f" % (tot / frames))
 for i, n in enumerate(NAMES[:24]):
+    if not n:
+        continue
     print("%2d %-28s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[i] / tot, buf[i] / frames))
 if MODE == "fused":
     print("   %-28s %6.2f%%" % ("store state", 100.0 * buf[23] / tot if len(buf) > 23 else 0))
