@@ -792,11 +792,11 @@ __global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
   __syncthreads();
   long long g = gq;
   while (g < ngroups) {
-    const long long t = g >> 2;
-    const int q = (int)(g & 3);
-    const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
     const float *T = a.ptile + (size_t)g * ptile::kRows * ptile::kQuarter;
     if (tid < kPcF) {
+      const long long t = g >> 2;
+      const int q = (int)(g & 3);
+      const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
       const int s = sb * 64 + q * 16 + tid;
       fval[tid] = s < a.n_streams && v < ticks_of(a, s) * a.n_channels;
       fidx[tid] = (long long)s * a.V + v;
@@ -2329,28 +2329,35 @@ __global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
 
 // ---------------------------------------------------------------------------
 // k_ola: out = x[0..479] + synthesis_mem; denoised * 1/32767; re-block ring;
-// per-tick vad_low (min over channels in channel order)
+// per-tick vad_low (min over channels in channel order).  Two frames per
+// 256-thread workgroup, a float4 of samples per thread (32-bit frame
+// arithmetic; the ring position of a frame is reduced once per thread).
 // ---------------------------------------------------------------------------
+static_assert(st::kSyn % 4 == 0 && kFrame % 4 == 0, "k_ola float4 rows");
 __global__ void __launch_bounds__(256) k_ola(StagedArgs a) {
   const int C = a.n_channels, V = a.V;
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long total = (long long)a.n_streams * V * kFrame;
-  if (gid >= total) return;
-  const int i = (int)(gid % kFrame);
-  const long long fv = gid / kFrame;
-  const int s = (int)(fv / V), v = (int)(fv - (long long)s * V);
+  const int q = threadIdx.x & 127;
+  const long long fl = (long long)blockIdx.x * 2 + (threadIdx.x >> 7);
+  if (fl >= (long long)a.n_streams * V || q >= kFrame / 4) return;
+  const int s = (int)(fl / V), v = (int)(fl - (long long)s * V);
   const int nt = ticks_of(a, s);
   if (v >= nt * C) return;
-  const int t = v / C, c = v - t * C;
+  const int t = v / C, c = v - t * C, i = 4 * q;
   const float *stp = a.state + (size_t)s * st::kWords;
   const size_t f = (size_t)s * V + v;
-  const float prev = (v == 0) ? stp[st::kSyn + i] : a.ys[(f - 1) * kWin + kFrame + i];
-  const float o = a.ys[f * kWin + i] + prev;
-  const float dn = a.raw_s16 ? o : o * (1.0f / (float)32767);
+  const float4 prev = (v == 0) ? *reinterpret_cast<const float4 *>(stp + st::kSyn + i)
+                               : *reinterpret_cast<const float4 *>(a.ys + (f - 1) * kWin + kFrame + i);
+  const float4 cur = *reinterpret_cast<const float4 *>(a.ys + f * kWin + i);
+  float4 o = make_float4(cur.x + prev.x, cur.y + prev.y, cur.z + prev.z, cur.w + prev.w);
+  if (!a.raw_s16) {
+    const float k = 1.0f / (float)32767;
+    o = make_float4(o.x * k, o.y * k, o.z * k, o.w * k);
+  }
   const int frames_done = reinterpret_cast<const int *>(stp)[st::kFramesDone];
-  const long long absi = (long long)(frames_done + t) * kFrame + i;
-  a.ring[((size_t)s * C + c) * a.ring_len + (size_t)(absi % a.ring_len)] = dn;
-  if (a.out_den) a.out_den[(((size_t)t * a.n_streams + s) * C + c) * kFrame + i] = dn;
+  long long ri = (long long)(frames_done + t) * kFrame % a.ring_len + i;  // ring_len % 4 == 0: no float4 wraps
+  if (ri >= a.ring_len) ri -= a.ring_len;
+  *reinterpret_cast<float4 *>(a.ring + ((size_t)s * C + c) * a.ring_len + ri) = o;
+  if (a.out_den) *reinterpret_cast<float4 *>(a.out_den + (((size_t)t * a.n_streams + s) * C + c) * kFrame + i) = o;
   if (i == 0 && c == 0) {
     float vad_low = 1;
     for (int cc = 0; cc < C; cc++) {
@@ -2362,55 +2369,68 @@ __global__ void __launch_bounds__(256) k_ola(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_winmeta: window completion bookkeeping (VAD.zig:298-348), lane per stream
+// k_winmeta: window completion bookkeeping (VAD.zig:298-348): lane per stream
+// for the serial tick walk (16 streams per 64-thread workgroup), then the
+// whole workgroup copies the streams' synthesis memory (second half of each
+// stream's last frame) into the state.
 // ---------------------------------------------------------------------------
+constexpr int kWmS = 16;
 __global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= a.n_streams) return;
-  const int nt = ticks_of(a, s);
-  int *wt = a.win_tick + (size_t)s * a.wmax;
-  long long *wsx = a.win_start + (size_t)s * a.wmax;
-  int j = 0;
-  if (nt > 0) {
-    float *stp = a.state + (size_t)s * st::kWords;
-    int *istp = reinterpret_cast<int *>(stp);
-    int fd = istp[st::kFramesDone];
-    float vol = stp[st::kVolAcc];
-    const int FB = a.plan->nfft_b;
-    for (int t = 0; t < nt; t++) {
-      const size_t o = (size_t)t * a.n_streams + s;
-      const float ratio = a.ratio[o];
-      const long long a0 = (long long)fd * kFrame;
-      const long long wdone = a0 / FB;
-      const long long next_end = (wdone + 1) * FB;
-      const bool complete = a0 + kFrame >= next_end;
-      if (complete) {
-        const int r = (int)(next_end - a0);
-        vol += ratio * ((float)r / (float)FB);
-        a.out_win_ratio[o] = vol;
-        a.out_win_vad[o] = a.out_vad[o];
-        vol = 0;
-        if (kFrame - r > 0) vol += ratio * ((float)(kFrame - r) / (float)FB);
-        wt[j] = t;
-        wsx[j] = wdone * FB;
-        j++;
-      } else {
-        vol += ratio * ((float)kFrame / (float)FB);
-        a.out_win_ratio[o] = 0.0f;
-        a.out_win_vad[o] = 0.0f;
-        // no window completes in this tick: band sums are defined as 0
-        for (int i = 0; i < a.n_channels * a.n_bands; i++) a.out_band[o * a.n_channels * a.n_bands + i] = 0.0f;
+  const int sb = blockIdx.x * kWmS, tid = threadIdx.x;
+  if (tid < kWmS && sb + tid < a.n_streams) {
+    const int s = sb + tid;
+    const int nt = ticks_of(a, s);
+    int *wt = a.win_tick + (size_t)s * a.wmax;
+    long long *wsx = a.win_start + (size_t)s * a.wmax;
+    int j = 0;
+    if (nt > 0) {
+      float *stp = a.state + (size_t)s * st::kWords;
+      int *istp = reinterpret_cast<int *>(stp);
+      int fd = istp[st::kFramesDone];
+      float vol = stp[st::kVolAcc];
+      const int FB = a.plan->nfft_b;
+      for (int t = 0; t < nt; t++) {
+        const size_t o = (size_t)t * a.n_streams + s;
+        const float ratio = a.ratio[o];
+        const long long a0 = (long long)fd * kFrame;
+        const long long wdone = a0 / FB;
+        const long long next_end = (wdone + 1) * FB;
+        const bool complete = a0 + kFrame >= next_end;
+        if (complete) {
+          const int r = (int)(next_end - a0);
+          vol += ratio * ((float)r / (float)FB);
+          a.out_win_ratio[o] = vol;
+          a.out_win_vad[o] = a.out_vad[o];
+          vol = 0;
+          if (kFrame - r > 0) vol += ratio * ((float)(kFrame - r) / (float)FB);
+          wt[j] = t;
+          wsx[j] = wdone * FB;
+          j++;
+        } else {
+          vol += ratio * ((float)kFrame / (float)FB);
+          a.out_win_ratio[o] = 0.0f;
+          a.out_win_vad[o] = 0.0f;
+          // no window completes in this tick: band sums are defined as 0
+          for (int i = 0; i < a.n_channels * a.n_bands; i++) a.out_band[o * a.n_channels * a.n_bands + i] = 0.0f;
+        }
+        a.out_win_flag[o] = complete ? 1 : 0;
+        fd++;
       }
-      a.out_win_flag[o] = complete ? 1 : 0;
-      fd++;
+      istp[st::kFramesDone] = fd;
+      stp[st::kVolAcc] = vol;
     }
-    istp[st::kFramesDone] = fd;
-    stp[st::kVolAcc] = vol;
-    // synthesis_mem for the next launch = second half of the last frame's window
-    const float *yl = a.ys + ((size_t)s * a.V + (size_t)nt * a.n_channels - 1) * kWin + kFrame;
-    for (int i = 0; i < kFrame; i++) stp[st::kSyn + i] = yl[i];
+    for (; j < a.wmax; j++) wt[j] = -1;
   }
-  for (; j < a.wmax; j++) wt[j] = -1;
+  // synthesis_mem for the next launch = second half of the last frame's window
+  for (int idx = tid; idx < kWmS * (kFrame / 4); idx += 64) {
+    const int sl = idx / (kFrame / 4), q = idx - sl * (kFrame / 4), s = sb + sl;
+    if (s >= a.n_streams) break;
+    const int nt = ticks_of(a, s);
+    if (nt <= 0) continue;
+    const float *yl = a.ys + ((size_t)s * a.V + (size_t)nt * a.n_channels - 1) * kWin + kFrame;
+    *reinterpret_cast<float4 *>(a.state + (size_t)s * st::kWords + st::kSyn + 4 * q) =
+        reinterpret_cast<const float4 *>(yl)[q];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2822,10 +2842,9 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   else
     hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
   rec(10);
-  const long long ola_threads = frames * kFrame;
-  hipLaunchKernelGGL(k_ola, dim3((unsigned)((ola_threads + 255) / 256)), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(k_ola, dim3((unsigned)((frames + 1) / 2)), dim3(256), 0, stream, a);
   rec(11);
-  hipLaunchKernelGGL(k_winmeta, dim3(lane_blocks), dim3(16), 0, stream, a);
+  hipLaunchKernelGGL(k_winmeta, dim3((a.n_streams + kWmS - 1) / kWmS), dim3(64), 0, stream, a);
   rec(12);
   if (wfft && a.nfft_b == 2048)
     (void)launch_wave(kWaveFftB, a, n_cu, stream);

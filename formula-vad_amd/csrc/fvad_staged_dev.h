@@ -28,6 +28,18 @@ __device__ __forceinline__ long long take_group(const StagedArgs &a, int slot) {
   return x + (long long)kQueues * atomicAdd(&a.work[slot * kQueues + x], 1u);
 }
 
+// Per-wave variant: lane 0 of the wave takes the next unit of its
+// workgroup's queue (blockIdx % 8), broadcast to the wave.  A grid must have
+// at least min(units, kQueues) workgroups so that every queue with units is
+// served.
+__device__ __forceinline__ long long wave_take(const StagedArgs &a, int slot, int lane) {
+  const int x = blockIdx.x % kQueues;
+  unsigned v = 0;
+  if (lane == 0) v = atomicAdd(&a.work[slot * kQueues + x], 1u);
+  v = __shfl(v, 0);
+  return x + (long long)kQueues * v;
+}
+
 // analysis / synthesis window value for index i of the 960-sample window
 __device__ __forceinline__ float win960(const float *__restrict__ hw, int i) {
   return (i < kFrame) ? hw[i] : hw[kWin - 1 - i];

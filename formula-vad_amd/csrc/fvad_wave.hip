@@ -31,13 +31,6 @@ constexpr int kWB = 8;   // frames per wave batch
 constexpr int kWNW = 4;  // waves per workgroup
 constexpr int kWOcc = 3;  // workgroups per CU (<= 168 VGPRs, <= 53 KB LDS)
 
-__device__ __forceinline__ long long wave_take(const StagedArgs &a, int slot, int lane) {
-  const int x = blockIdx.x % kQueues;
-  unsigned v = 0;
-  if (lane == 0) v = atomicAdd(&a.work[slot * kQueues + x], 1u);
-  v = __shfl(v, 0);
-  return x + (long long)kQueues * v;
-}
 
 // Batches of a wave: dynamic (per-XCD queues, wave_take) or static striding
 // over the grid's waves, per kernel (a.wave_static bit 1 << kind).  k_fftAw
