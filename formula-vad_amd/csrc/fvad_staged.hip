@@ -759,8 +759,9 @@ __global__ void __launch_bounds__(256, 2) k_plpc(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_pcorr: one workgroup per quarter tile (16 streams at one frame position;
-// its tile rows are one contiguous block).
+// k_pcorr: one 128-thread workgroup per half quarter tile (8 streams at one
+// frame position; 38.5 KB of LDS, so 4 workgroups share a CU and a barrier
+// stalls 2 waves, not 4).
 //   Q0 xf (rows 0..863) and the coarse Syy sequence -> LDS
 //   Q1 coarse xcorr: lane = (frame, 10 consecutive lags), a register window of
 //      10 y values slides one sample per step (2 LDS reads per 10 MACs)
@@ -769,15 +770,20 @@ __global__ void __launch_bounds__(256, 2) k_plpc(StagedArgs a) {
 //   Q3 fine xcorr at the <= 10 lags within +-2 of 2*best (others are 0)
 //   Q4 fine find_best_pitch + pseudo-interpolation -> T0, candidate count
 //   Q5 remove_doubling products: lane = (frame, candidate c); candidate c's
-//      xcorr at T-1, T, T+1 share a sliding window of 3, plus xcorr(T1b)
+//      xcorr at T-1, T, T+1 share a sliding window of 3, plus xcorr(T1b);
+//      operands are read as aligned pairs (ds_read_b64: 64 banks, 2 steps
+//      per read), the lane's window parity resolved by selects
 // ---------------------------------------------------------------------------
-constexpr int kPcF = ptile::kQuarter;
-constexpr int kPcXS = 869;  // xf row pitch (odd: frames fall in distinct bank classes)
+constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
+constexpr int kPcNT = 16 * kPcF;       // 16 lanes per frame in Q1
+static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
+constexpr int kPcXS = 870;  // xf row pitch: even (8-byte aligned pairs in Q5), = 6 mod 8 (conflict-free Q0 stores)
 constexpr int kPcSP = 153;  // coarse xcorr / Syy row pitch (odd; >= 147 rounded up to the scan block)
 
-__global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
-  constexpr int NT = 256;
-  __shared__ float xf[kPcF][kPcXS];
+__global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
+  constexpr int NT = kPcNT;
+  constexpr int kHalves = ptile::kQuarter / kPcF;
+  __shared__ __attribute__((aligned(16))) float xf[kPcF][kPcXS];
   __shared__ float scl[kPcF][kPcSP], xc[kPcF][kPcSP];
   __shared__ float sfl[kPcF][10], fine[kPcF][10];
   __shared__ int best[kPcF][2], T0s[kPcF], nvs[kPcF], fval[kPcF];
@@ -785,34 +791,39 @@ __global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
   const int tid = threadIdx.x;
   const int Vr = a.n_ticks * a.n_channels;
   const int n_sb = (a.n_streams + 63) >> 6;
-  const long long ngroups = (long long)n_sb * Vr * 4;
+  const long long ngroups = (long long)n_sb * Vr * 4 * kHalves;
   STAMP_INIT();
   __shared__ long long gq;
   if (threadIdx.x == 0) gq = take_group(a, kWorkPcorr);
   __syncthreads();
   long long g = gq;
   while (g < ngroups) {
-    const float *T = a.ptile + (size_t)g * ptile::kRows * ptile::kQuarter;
+    // group g = (quarter tile g / kHalves, frame columns h*kPcF ..): T is
+    // the group's first column, rows keep the quarter's 16-column pitch
+    const long long gq4 = g / kHalves;
+    const int h = (int)(g - gq4 * kHalves);
+    const float *T = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter + h * kPcF;
     if (tid < kPcF) {
-      const long long t = g >> 2;
-      const int q = (int)(g & 3);
+      const long long t = gq4 >> 2;
+      const int q = (int)(gq4 & 3);
       const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
-      const int s = sb * 64 + q * 16 + tid;
+      const int s = sb * 64 + q * 16 + h * kPcF + tid;
       fval[tid] = s < a.n_streams && v < ticks_of(a, s) * a.n_channels;
       fidx[tid] = (long long)s * a.V + v;
     }
     // Q0
-    for (int idx = tid; idx < kXlp * 4; idx += NT) {
-      const int r = idx >> 2, p = idx & 3;
-      const float4 w4 = reinterpret_cast<const float4 *>(T)[idx];
+    constexpr int P4 = kPcF / 4;  // float4s per row and group
+    for (int idx = tid; idx < kXlp * P4; idx += NT) {
+      const int r = idx / P4, p = idx % P4;
+      const float4 w4 = *reinterpret_cast<const float4 *>(T + r * ptile::kQuarter + 4 * p);
       xf[4 * p][r] = w4.x;
       xf[4 * p + 1][r] = w4.y;
       xf[4 * p + 2][r] = w4.z;
       xf[4 * p + 3][r] = w4.w;
     }
-    for (int idx = tid; idx < 147 * 4; idx += NT) {
-      const int r = idx >> 2, p = idx & 3;
-      const float4 w4 = reinterpret_cast<const float4 *>(T + ptile::kSc * ptile::kQuarter)[idx];
+    for (int idx = tid; idx < 147 * P4; idx += NT) {
+      const int r = idx / P4, p = idx % P4;
+      const float4 w4 = *reinterpret_cast<const float4 *>(T + (ptile::kSc + r) * ptile::kQuarter + 4 * p);
       scl[4 * p][r] = w4.x;
       scl[4 * p + 1][r] = w4.y;
       scl[4 * p + 2][r] = w4.z;
@@ -971,18 +982,45 @@ __global__ void __launch_bounds__(256) k_pcorr(StagedArgs a) {
         const float xx = T[ptile::kXx * ptile::kQuarter + fr];
         const float *X = xf[fr] + (kPitchMax >> 1);
         float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
-        float win[3] = {X[-Tc - 1], X[-Tc], X[-Tc + 1]};
-        for (int j0 = 0; j0 < 480; j0 += 3) {
-#pragma unroll
-          for (int u = 0; u < 3; u++) {
-            const int j = j0 + u;
-            const float xv = X[j];
-            aM = aM + xv * win[u % 3];
-            a0 = a0 + xv * win[(u + 1) % 3];
-            aP = aP + xv * win[(u + 2) % 3];
-            aB = aB + xv * X[j - Tb];
-            win[u] = X[j + 2 - Tc];  // lag T-1 at step j+1
-          }
+        // Operands come in 8-byte aligned pairs (ds_read_b64): the broadcast
+        // x[j], x[j+1]; the window stream X[j - Tc - 1 + t] and the T1b stream
+        // X[j - Tb + t], each read from the even index at or below its start
+        // and shifted by the lane's parity (ow, ob) through selects.  Each sum
+        // still adds its products in j order.
+        const int m0 = -Tc - 1, ow = m0 & 1;
+        const int mb = c == 0 ? 0 : -Tb, ob = mb & 1;  // candidate 0 needs no T1b (broadcast address)
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        const v2f *W = reinterpret_cast<const v2f *>(X + (m0 - ow));
+        const v2f *Bq = reinterpret_cast<const v2f *>(X + (mb - ob));
+        const v2f *Xp = reinterpret_cast<const v2f *>(X);
+        v2f q0 = W[0], q1 = W[1], qp = W[2];
+        float w0 = ow ? q0.y : q0.x, w1 = ow ? q1.x : q0.y;
+        float w2 = ow ? q1.y : q1.x, w3 = ow ? qp.x : q1.y;
+        v2f r0 = Bq[0], rp = Bq[1];
+        float b0 = ob ? r0.y : r0.x, b1 = ob ? rp.x : r0.y;
+#pragma unroll 4
+        for (int i = 0; i < 240; i++) {  // j = 2i, 2i + 1
+          // an offset the compiler cannot see through keeps every pair load a
+          // single ds_read_b64 (64 banks) instead of merged ds_read2_b64s
+          int o = i;
+          asm volatile("" : "+v"(o));
+          const v2f xp = Xp[o], qn = W[o + 3], rn = Bq[o + 2];
+          aM = aM + xp.x * w0;
+          a0 = a0 + xp.x * w1;
+          aP = aP + xp.x * w2;
+          aB = aB + xp.x * b0;
+          aM = aM + xp.y * w1;
+          a0 = a0 + xp.y * w2;
+          aP = aP + xp.y * w3;
+          aB = aB + xp.y * b1;
+          w0 = w2;
+          w1 = w3;
+          w2 = ow ? qp.y : qp.x;
+          w3 = ow ? qn.x : qp.y;
+          qp = qn;
+          b0 = ob ? rp.y : rp.x;
+          b1 = ob ? rn.x : rp.y;
+          rp = rn;
         }
         float *rg = a.rec + fidx[fr] * rec::kSize;
         const int off = pitch_offset(aP, a0, aM);
@@ -2782,7 +2820,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
     const char *v = getenv("FVAD_WFFT");
     return !(v && atoi(v) == 0);
   }();
-  static const int g_pcorr = resident_blocks(k_pcorr, 256, n_cu);
+  static const int g_pcorr = resident_blocks(k_pcorr, kPcNT, n_cu);
   // lane-per-stream kernels: 16 streams per workgroup spreads the serial
   // chains over more CUs (each chain is latency-bound, not lane-bound)
   const int lane_blocks = (a.n_streams + 15) / 16;
@@ -2814,7 +2852,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
     rec(14);
     hipLaunchKernelGGL(k_plpc, grid((tiles + 3) / 4, g_plpc), dim3(256), 0, stream, a);
     rec(4);
-    hipLaunchKernelGGL(k_pcorr, grid(tiles * 4, g_pcorr), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_pcorr, grid(tiles * 4 * (ptile::kQuarter / kPcF), g_pcorr), dim3(kPcNT), 0, stream, a);
   }
   rec(5);
   hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(16), 0, stream, a);
