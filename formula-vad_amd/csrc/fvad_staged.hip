@@ -95,8 +95,11 @@ static_assert(kTermOff >= 2 * kFreq && kTermOff % 4 == 0 && kTermOff + 800 <= 2 
 // the per-tick RMS sums and the volume ratio (channels of a stream are
 // neighbouring lanes).
 // ---------------------------------------------------------------------------
-constexpr int kPrepSlots = 16;  // channel-slots per workgroup (8 stereo streams)
-constexpr int kPrepRing = 8;    // float4 loads in flight per lane
+constexpr int kPrepSlots = 64;  // channel-slots per workgroup (32 stereo streams)
+#ifndef FVAD_PREP_RING
+#define FVAD_PREP_RING 8
+#endif
+constexpr int kPrepRing = FVAD_PREP_RING;  // float4 loads in flight per lane
 static_assert((kFrame / 4) % kPrepRing == 0, "prep ring must divide a frame");
 
 // One lane's input sequence of float4 chunks: per tick the C * 480 samples of
