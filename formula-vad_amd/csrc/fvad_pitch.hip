@@ -1,0 +1,321 @@
+// k_pcorr in a translation unit of its own: built without SLP vectorisation
+// (Makefile), which keeps its f32 sums in single VALU instructions -- measured
+// faster for this kernel (1.60 -> 1.46 ms), while k_plpc and the GRU kernel
+// in fvad_staged.hip prefer the packed form.
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include "fvad_device.h"
+#include "fvad_internal.h"
+#include "fvad_staged.h"
+#include "fvad_staged_dev.h"
+
+#include <algorithm>
+
+namespace fvad {
+
+// ---------------------------------------------------------------------------
+// k_pcorr: one 128-thread workgroup per half quarter tile (8 streams at one
+// frame position; 38.5 KB of LDS, so 4 workgroups share a CU and a barrier
+// stalls 2 waves, not 4).
+//   Q0 xf (rows 0..863) and the coarse Syy sequence -> LDS
+//   Q1 coarse xcorr: lane = (frame, 10 consecutive lags), a register window of
+//      10 y values slides one sample per step (2 LDS reads per 10 MACs)
+//   Q2 coarse find_best_pitch, lane per frame; the fine Syy values at the
+//      <= 10 candidate lags are fetched here, used in Q4
+//   Q3 fine xcorr at the <= 10 lags within +-2 of 2*best (others are 0)
+//   Q4 fine find_best_pitch + pseudo-interpolation -> T0, candidate count
+//   Q5 remove_doubling products: lane = (frame, candidate c); candidate c's
+//      xcorr at T-1, T, T+1 share a sliding window of 3, plus xcorr(T1b);
+//      operands are read as aligned pairs (ds_read_b64: 64 banks, 2 steps
+//      per read), the lane's window parity resolved by selects
+// ---------------------------------------------------------------------------
+constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
+constexpr int kPcNT = 16 * kPcF;       // 16 lanes per frame in Q1
+static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
+constexpr int kPcXS = 870;  // xf row pitch: even (8-byte aligned pairs in Q5), = 6 mod 8 (conflict-free Q0 stores)
+constexpr int kPcSP = 153;  // coarse xcorr / Syy row pitch (odd; >= 147 rounded up to the scan block)
+
+__global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
+  constexpr int NT = kPcNT;
+  constexpr int kHalves = ptile::kQuarter / kPcF;
+  __shared__ __attribute__((aligned(16))) float xf[kPcF][kPcXS];
+  __shared__ float scl[kPcF][kPcSP], xc[kPcF][kPcSP];
+  __shared__ float sfl[kPcF][10], fine[kPcF][10];
+  __shared__ int best[kPcF][2], T0s[kPcF], nvs[kPcF], fval[kPcF];
+  __shared__ long long fidx[kPcF];
+  const int tid = threadIdx.x;
+  const int Vr = a.n_ticks * a.n_channels;
+  const int n_sb = (a.n_streams + 63) >> 6;
+  const long long ngroups = (long long)n_sb * Vr * 4 * kHalves;
+  STAMP_INIT();
+  __shared__ long long gq;
+  if (threadIdx.x == 0) gq = take_group(a, kWorkPcorr);
+  __syncthreads();
+  long long g = gq;
+  while (g < ngroups) {
+    // group g = (quarter tile g / kHalves, frame columns h*kPcF ..): T is
+    // the group's first column, rows keep the quarter's 16-column pitch
+    const long long gq4 = g / kHalves;
+    const int h = (int)(g - gq4 * kHalves);
+    const float *T = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter + h * kPcF;
+    if (tid < kPcF) {
+      const long long t = gq4 >> 2;
+      const int q = (int)(gq4 & 3);
+      const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
+      const int s = sb * 64 + q * 16 + h * kPcF + tid;
+      fval[tid] = s < a.n_streams && v < ticks_of(a, s) * a.n_channels;
+      fidx[tid] = (long long)s * a.V + v;
+    }
+    // Q0
+    constexpr int P4 = kPcF / 4;  // float4s per row and group
+    for (int idx = tid; idx < kXlp * P4; idx += NT) {
+      const int r = idx / P4, p = idx % P4;
+      const float4 w4 = *reinterpret_cast<const float4 *>(T + r * ptile::kQuarter + 4 * p);
+      xf[4 * p][r] = w4.x;
+      xf[4 * p + 1][r] = w4.y;
+      xf[4 * p + 2][r] = w4.z;
+      xf[4 * p + 3][r] = w4.w;
+    }
+    for (int idx = tid; idx < 147 * P4; idx += NT) {
+      const int r = idx / P4, p = idx % P4;
+      const float4 w4 = *reinterpret_cast<const float4 *>(T + (ptile::kSc + r) * ptile::kQuarter + 4 * p);
+      scl[4 * p][r] = w4.x;
+      scl[4 * p + 1][r] = w4.y;
+      scl[4 * p + 2][r] = w4.z;
+      scl[4 * p + 3][r] = w4.w;
+    }
+    __syncthreads();
+    RSTAMP(0);
+    // Q1: xcorr[k] = sum_j x_lp4[j] y_lp4[j+k], x_lp4[j] = xf[384+2j], y_lp4[m] = xf[2m]
+    {
+      constexpr int R = 10;
+      const int fr = tid >> 4, k0 = R * (tid & 15);
+      if (k0 < 147) {
+        const float *X = xf[fr] + (kPitchMax >> 1);
+        const float *Y = xf[fr] + 2 * k0;
+        float acc[R], win[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          acc[r] = 0.0f;
+          win[r] = Y[2 * r];
+        }
+        for (int jb = 0; jb < 240; jb += R) {
+#pragma unroll
+          for (int u = 0; u < R; u++) {
+            const float xv = X[2 * (jb + u)];
+#pragma unroll
+            for (int r = 0; r < R; r++) acc[r] = acc[r] + xv * win[(r + u) % R];
+            win[u] = Y[2 * (jb + u + R)];  // lag k0+R-1 at step jb+u+1
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++)
+          if (k0 + r < 147) xc[fr][k0 + r] = acc[r];
+      } else if (k0 < kPcSP) {
+        // lags 147.. pad the scan blocks: xcorr <= 0 never updates the best pair
+        for (int k = 147; k < kPcSP; k++) xc[fr][k] = -1.0f;
+      }
+    }
+    __syncthreads();
+    RSTAMP(1);
+    // Q2
+    float sfv[10];
+    if (tid < kPcF) {
+      const int fr = tid;
+      int bst[2] = {0, 1};
+      float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
+      // operands of the next 8 lags load while these 8 are visited
+      constexpr int B = 8;
+      float xb[B], yb[B];
+#pragma unroll
+      for (int u = 0; u < B; u++) {
+        xb[u] = xc[fr][u];
+        yb[u] = scl[fr][u];
+      }
+      for (int i0 = 0; i0 < 147; i0 += B) {
+        float xn[B], yn[B];
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+          const int i = min(i0 + B + u, kPcSP - 1);
+          xn[u] = xc[fr][i];
+          yn[u] = scl[fr][i];
+        }
+#pragma unroll
+        for (int u = 0; u < B; u++) best_pitch_visit(xb[u], yb[u], i0 + u, bn0, bn1, bd0, bd1, bst);
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+          xb[u] = xn[u];
+          yb[u] = yn[u];
+        }
+      }
+      best[fr][0] = bst[0];
+      best[fr][1] = bst[1];
+#pragma unroll
+      for (int u = 0; u < 10; u++) {
+        const int i = 2 * bst[u / 5] - 2 + (u % 5);
+        sfv[u] = (i >= 0 && i < 294) ? T[(ptile::kSf + i) * ptile::kQuarter + fr] : 0.0f;
+      }
+    }
+    __syncthreads();
+    RSTAMP(2);
+    // Q3
+    if (tid < 10 * kPcF) {
+      const int fr = tid / 10, u = tid - 10 * fr;
+      const int bp0 = best[fr][0], bp1 = best[fr][1];
+      const int i = (u < 5 ? 2 * bp0 : 2 * bp1) - 2 + (u % 5);
+      const bool dup = u >= 5 && abs(i - 2 * bp0) <= 2;
+      if (i >= 0 && i < 294 && !dup) {
+        const float *xl = xf[fr] + (kPitchMax >> 1), *y = xf[fr] + i;
+        const float sum = dot_seq(0.0f, xl, 1, y, 1, 480);
+        fine[fr][u] = (-1 > sum) ? -1 : sum;
+      }
+    }
+    __syncthreads();
+    RSTAMP(3);
+    // Q4
+    if (tid < kPcF) {
+      const int fr = tid;
+#pragma unroll
+      for (int u = 0; u < 10; u++) sfl[fr][u] = sfv[u];
+      const int bp0 = best[fr][0], bp1 = best[fr][1];
+      const int w0 = 2 * bp0 - 2, w1 = 2 * bp1 - 2;
+      // lags of the first window take its values (a duplicate lag of the
+      // second window was not computed in Q3)
+      auto slot = [&](int i) -> int { return (i >= w0 && i <= w0 + 4) ? i - w0 : ((i >= w1 && i <= w1 + 4) ? 5 + i - w1 : -1); };
+      auto xcf = [&](int i) -> float {
+        const int s = slot(i);
+        return s < 0 ? 0.0f : fine[fr][s];
+      };
+      int bst[2] = {0, 1};
+      float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
+      int lo0 = w0, hi0 = w0 + 4, lo1 = w1, hi1 = w1 + 4;
+      if (lo1 < lo0) {
+        const int t0 = lo0, t1 = hi0;
+        lo0 = lo1;
+        hi0 = hi1;
+        lo1 = t0;
+        hi1 = t1;
+      }
+      for (int i = max(0, lo0); i <= min(293, hi0); i++) best_pitch_visit(xcf(i), sfl[fr][slot(i)], i, bn0, bn1, bd0, bd1, bst);
+      for (int i = max(max(0, lo1), hi0 + 1); i <= min(293, hi1); i++)
+        best_pitch_visit(xcf(i), sfl[fr][slot(i)], i, bn0, bn1, bd0, bd1, bst);
+      int offset;
+      if (bst[0] > 0 && bst[0] < 294 - 1) {
+        const float aa = xcf(bst[0] - 1), bb = xcf(bst[0]), cc = xcf(bst[0] + 1);
+        if ((cc - aa) > .7f * (bb - aa))
+          offset = 1;
+        else if ((aa - cc) > .7f * (bb - cc))
+          offset = -1;
+        else
+          offset = 0;
+      } else {
+        offset = 0;
+      }
+      const int pitch = 2 * bst[0] - offset;
+      int T0 = (kPitchMax - pitch) / 2;
+      if (T0 >= 384) T0 = 383;
+      int nv = 0;
+      for (int k = 2; k <= 15; k++) {
+        if (rd_T1(T0, k) < 30) break;
+        nv++;
+      }
+      T0s[fr] = T0;
+      nvs[fr] = nv;
+    }
+    __syncthreads();
+    RSTAMP(4);
+    // Q5
+    if (tid < 15 * kPcF) {
+      const int fr = tid / 15, c = tid - 15 * fr;
+      if (fval[fr] && (c == 0 || c - 1 < nvs[fr])) {
+        const int T0 = T0s[fr];
+        const int Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
+        const int Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
+        // yy_lookup and xx gathers, consumed after the products
+        const float yyA = T[(ptile::kYy + Tc) * ptile::kQuarter + fr];
+        const float yyB = T[(ptile::kYy + Tb) * ptile::kQuarter + fr];
+        const float xx = T[ptile::kXx * ptile::kQuarter + fr];
+        const float *X = xf[fr] + (kPitchMax >> 1);
+        float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
+        // Operands come in 8-byte aligned pairs (ds_read_b64): the broadcast
+        // x[j], x[j+1]; the window stream X[j - Tc - 1 + t] and the T1b stream
+        // X[j - Tb + t], each read from the even index at or below its start
+        // and shifted by the lane's parity (ow, ob) through selects.  Each sum
+        // still adds its products in j order.
+        const int m0 = -Tc - 1, ow = m0 & 1;
+        const int mb = c == 0 ? 0 : -Tb, ob = mb & 1;  // candidate 0 needs no T1b (broadcast address)
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        const v2f *W = reinterpret_cast<const v2f *>(X + (m0 - ow));
+        const v2f *Bq = reinterpret_cast<const v2f *>(X + (mb - ob));
+        const v2f *Xp = reinterpret_cast<const v2f *>(X);
+        v2f q0 = W[0], q1 = W[1], qp = W[2];
+        float w0 = ow ? q0.y : q0.x, w1 = ow ? q1.x : q0.y;
+        float w2 = ow ? q1.y : q1.x, w3 = ow ? qp.x : q1.y;
+        v2f r0 = Bq[0], rp = Bq[1];
+        float b0 = ob ? r0.y : r0.x, b1 = ob ? rp.x : r0.y;
+#pragma unroll 4
+        for (int i = 0; i < 240; i++) {  // j = 2i, 2i + 1
+          // an offset the compiler cannot see through keeps every pair load a
+          // single ds_read_b64 (64 banks) instead of merged ds_read2_b64s
+          int o = i;
+          asm volatile("" : "+v"(o));
+          const v2f xp = Xp[o], qn = W[o + 3], rn = Bq[o + 2];
+          aM = aM + xp.x * w0;
+          a0 = a0 + xp.x * w1;
+          aP = aP + xp.x * w2;
+          aB = aB + xp.x * b0;
+          aM = aM + xp.y * w1;
+          a0 = a0 + xp.y * w2;
+          aP = aP + xp.y * w3;
+          aB = aB + xp.y * b1;
+          w0 = w2;
+          w1 = w3;
+          w2 = ow ? qp.y : qp.x;
+          w3 = ow ? qn.x : qp.y;
+          qp = qn;
+          b0 = ob ? rp.y : rp.x;
+          b1 = ob ? rn.x : rp.y;
+          rp = rn;
+        }
+        float *rg = a.rec + fidx[fr] * rec::kSize;
+        const int off = pitch_offset(aP, a0, aM);
+        if (c == 0) {
+          rg[rec::kT0] = __int_as_float(T0);
+          rg[rec::kNValid] = __int_as_float(nvs[fr]);
+          rg[rec::kG0] = pitch_gain(a0, xx, yyA);
+          rg[rec::kXy0] = a0;
+          rg[rec::kYy0] = yyA;
+          rg[rec::kOff0] = __int_as_float(off);
+        } else {
+          float *qk = rg + rec::kK + (c - 1) * rec::kKStride;
+          const float xy = .5f * (a0 + aB), yy = .5f * (yyA + yyB);
+          qk[0] = __int_as_float(Tc);
+          qk[1] = pitch_gain(xy, xx, yy);
+          qk[2] = xy;
+          qk[3] = yy;
+          qk[4] = __int_as_float(off);
+        }
+      }
+    }
+    if (tid == 0) gq = take_group(a, kWorkPcorr);
+    __syncthreads();
+    RSTAMP(5);
+    g = gq;
+  }
+  STAMP_FLUSH(32, 6);
+}
+
+hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream) {
+  static const int resident = [n_cu] {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcorr, kPcNT, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    return per_cu * n_cu;
+  }();
+  const long long groups = tiles * 4 * (ptile::kQuarter / kPcF);
+  hipLaunchKernelGGL(k_pcorr, dim3((unsigned)std::min<long long>(groups, resident)), dim3(kPcNT), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace fvad

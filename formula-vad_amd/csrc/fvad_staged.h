@@ -117,6 +117,8 @@ hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev);
 // Launch the other 10 kernels; when ev != nullptr their timing events are
 // recorded.
 hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev);
+// k_pcorr over `tiles` pitch tiles (fvad_pitch.hip)
+hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream);
 const char *staged_kernel_name(int i);
 // The wave-per-frame FFT kernels (fvad_wave.hip), persistent grids; kWaveFftB
 // needs fft_size 2048 (a 1024-point complex transform).

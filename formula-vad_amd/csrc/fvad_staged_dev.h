@@ -1,9 +1,10 @@
 // Device helpers shared by the staged kernels' translation units
-// (fvad_staged.hip, fvad_wave.hip).
+// (fvad_staged.hip, fvad_wave.hip, fvad_pitch.hip).
 #pragma once
 #pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
 
+#include "fvad_device.h"
 #include "fvad_internal.h"
 #include "fvad_staged.h"
 
@@ -55,6 +56,65 @@ __device__ __forceinline__ int frame_of(const StagedArgs &a, long long g, int F,
   if (f >= (long long)a.n_streams * a.V) return -1;
   const int s = (int)(f / a.V), v = (int)(f - (long long)s * a.V);
   return v < ticks_of(a, s) * a.n_channels ? (int)f : -1;
+}
+
+// Diagnostic build only (-DFVAD_STAMPS): per-phase s_memtime totals of
+// thread 0 (it joins every barrier, so a phase's stamp is its critical path),
+// accumulated into a.stamps[base + id]; no other code reads them.
+#ifdef FVAD_STAMPS
+#define STAMP_INIT()                \
+  unsigned long long st_acc[16] = {}; \
+  unsigned long long st_last = __builtin_amdgcn_s_memtime()
+#define RSTAMP(id)                                                \
+  do {                                                            \
+    if (tid == 0) {                                               \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+      st_acc[id] += t_ - st_last;                                 \
+      st_last = t_;                                               \
+    }                                                             \
+  } while (0)
+#define STAMP_FLUSH(base, n)                                                  \
+  do {                                                                        \
+    if (tid == 0 && a.stamps)                                                 \
+      for (int i_ = 0; i_ < (n); i_++) atomicAdd(&a.stamps[(base) + i_], st_acc[i_]); \
+  } while (0)
+#else
+#define STAMP_INIT() \
+  do {               \
+  } while (0)
+#define RSTAMP(id) \
+  do {             \
+  } while (0)
+#define STAMP_FLUSH(base, n) \
+  do {                       \
+  } while (0)
+#endif
+
+// remove_doubling's candidate loop that does not depend on the previous
+// frame, so k_select's serial part is compares only.
+//   T0, candidate count, g0 = pitch_gain(xcorr(T0), xx, yy[T0]), xcorr(T0),
+//   yy[T0], the pseudo-interpolation offset of T0; then per k = 2..15:
+//   T1, g1 = pitch_gain(xy, xx, yy), xy = (xcorr(T1) + xcorr(T1b)) / 2,
+//   yy = (yy[T1] + yy[T1b]) / 2, the offset of T1.
+namespace rec {
+constexpr int kT0 = 0, kNValid = 1, kG0 = 2, kXy0 = 3, kYy0 = 4, kOff0 = 5;
+constexpr int kK = 8, kKStride = 5;  // T1, g1, xy, yy, offset
+constexpr int kSize = 80;
+}  // namespace rec
+static_assert(rec::kSize == kPitchRecord, "pitch record size");
+static_assert(rec::kK + 14 * rec::kKStride <= rec::kSize && rec::kSize % 4 == 0, "pitch record layout");
+
+// remove_doubling's final pseudo-interpolation from the xcorr at T-1, T, T+1
+__device__ __forceinline__ int pitch_offset(float x0, float x1, float x2) {
+  if ((x2 - x0) > .7f * (x1 - x0)) return 1;
+  if ((x0 - x2) > .7f * (x1 - x2)) return -1;
+  return 0;
+}
+
+__device__ __forceinline__ int rd_T1(int T0, int k) { return (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k)); }
+__device__ __forceinline__ int rd_T1b(int T0, int T1, int k) {
+  if (k == 2) return (T1 + T0 > 384) ? T0 : T0 + T1;
+  return (int)((unsigned)(2 * second_check(k) * T0 + k) / (unsigned)(2 * k));
 }
 
 }  // namespace fvad

@@ -11,7 +11,7 @@ cp -r "$ROOT/formula-vad_amd/csrc" "$ROOT/formula-vad_amd/Makefile" "$W/"
 mkdir -p "$W/include" && cp "$ROOT/include/fvad.h" "$W/include/"
 # the Makefile refers to ../include/fvad.h relative to the package dir
 mkdir -p "$W/pkg" && mv "$W/csrc" "$W/Makefile" "$W/pkg/"
-make -s -j8 -C "$W/pkg" EXTRA_HIPFLAGS="${2:-}" lib/libfvad.so
+make -s -j8 -C "$W/pkg" EXTRA_HIPFLAGS="${2:-}" ${3:-} lib/libfvad.so
 mkdir -p "$ROOT/formula-vad_amd/lib/var"
 cp "$W/pkg/lib/libfvad.so" "$ROOT/formula-vad_amd/lib/var/libfvad_$NAME.so"
 echo "built formula-vad_amd/lib/var/libfvad_$NAME.so"
