@@ -1724,21 +1724,33 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     if (mid == kCeps) mid = 0;
     L.memid[s] = mid;
   };
-  // prologue: features of frame 0; frame 1's staged
+  // prologue: features of frame 0 (its spectral variability: P1 of step 0)
   if (pf_lane) L.pf[pfs][pfi] = fetch(0);
   __syncthreads();
   for (int idx = tid; idx < S * (kBands + 7 + kCeps); idx += NT) feat_c(0, idx);
   __syncthreads();
-  if (tid < S) feat_d(0, tid);
-  if (pf_lane) L.pf[pfs][pfi] = fetch(1);
-  __syncthreads();
-  // P1 thread plan: denoise z|r tasks 0..383, noise z|r 0..191, vad z|r 0..95,
-  // then features (296 items) and gains (176 items)
-  constexpr int kP1Den = 0, kP1Noise = 384, kP1Vad = 576, kP1Feat = 672, kP1Gain = 968;
+  // P1 wave plan (w = tid >> 6).  Waves w, w+4, w+8, w+12 share a SIMD under
+  // the cyclic wave placement, so the heavy roles are spread over the four
+  // residue classes -- {den, den}, {den, den}, {den, noise, noise}, {den,
+  // noise, vad, vad} -- and no wave holds lanes of two roles (it would run
+  // both branches one after the other): denoise z|r waves 0..5 (384 tasks),
+  // noise z|r waves 6, 7, 10 (192), vad z|r waves 11, 15 (96), gain smoothing
+  // + vad_output store wave 8, spectral variability of frame t wave 9.
+  // (The constants name each role's first thread, for the stamps build.)
+  constexpr int kP1Den = 0, kP1Noise = 384, kP1Vad = 704, kP1Var = 576, kP1Gain = 512;
   // P2: denoise h 0..191, noise h 0..95, vad h 0..47, dense 0..47,
-  // denoise_output 0..43, vad_output (one lane, 8 streams), spectral variability
-  constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 288, kP2Dense = 336, kP2Out = 384, kP2VadOut = 428,
-                kP2Var = 448;
+  // denoise_output 0..43, vad_output (one lane, 8 streams), features of frame
+  // t+1 (296 items)
+  // every role starts on a wave boundary: a wave holding lanes of two roles
+  // runs both branches one after the other (measured: the wave with noise h
+  // and vad h lanes set the phase at 19.6 k cycles)
+  constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 384, kP2Out = 448, kP2VadOut = 512,
+                kP2Feat = 576;
+  constexpr int kFeatItems = S * (kBands + 7 + kCeps);
+  static_assert(kP2Feat + kFeatItems <= NT, "P2 feature lanes");
+  static_assert(kP2Noise - kP2Den >= 96 * kR3G && kP2Vad - kP2Noise >= 48 * kR3G && kP2Dense - kP2Vad >= 24 * kR3G &&
+                    kP2Out - kP2Dense >= 24 * kR3G && kP2VadOut - kP2Out >= 22 * kR3G && kP2Feat - kP2VadOut >= kR3G,
+                "P2 roles");
   STAMP_INIT();
 #ifdef FVAD_STAMPS
   // role finish times: the first thread of each role adds (its role's end -
@@ -1746,8 +1758,8 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   unsigned long long ph0 = 0, racc = 0;
   int rslot = -1;
   {
-    const int l1[5] = {kP1Den, kP1Noise, kP1Vad, kP1Feat, kP1Gain};
-    const int l2[7] = {kP2Den, kP2Noise, kP2Vad, kP2Dense, kP2Out, kP2VadOut, kP2Var};
+    const int l1[5] = {kP1Den, kP1Noise, kP1Vad, kP1Var, kP1Gain};
+    const int l2[7] = {kP2Den, kP2Noise, kP2Vad, kP2Dense, kP2Out, kP2VadOut, kP2Feat};
     for (int i = 0; i < 5; i++)
       if (tid == l1[i]) rslot = i;
     for (int i = 0; i < 7; i++)
@@ -1767,28 +1779,27 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   for (int t = 0; t <= maxnf + 4; t++) {
     const int fv = t - 1, fn = t - 2, fd = t - 3;
     ROLE_BEGIN();
-    // frame t+2's features, staged at the end of this step: issued here, so
-    // no load is outstanding across a step boundary (a loop-carried register
-    // would make the step's last barrier wait for it)
-    const float pf_now = fetch(t + 2);
+    // frame t+1's raw features, staged at the end of P1 for P2's feat_c:
+    // issued here, so no load is outstanding across a step boundary (a
+    // loop-carried register would make the step's last barrier wait for it)
+    const float pf_now = fetch(t + 1);
     // ---- P1
-    if (tid < kP1Noise) {
+    const int wv = tid >> 6, ln = tid & 63;
+    if (wv < 6) {
       if (fd >= 0 && fd < maxnf)
         rnn_gates<5, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, L.gdT[(fd + 1) & 1], L.zrd,
-                              kActSigmoid, L.tt, tid - kP1Den);
-    } else if (tid < kP1Vad) {
+                              kActSigmoid, L.tt, tid);
+    } else if (wv == 6 || wv == 7 || wv == 10) {
       if (fn >= 0 && fn < maxnf)
         rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
-                              kActSigmoid, L.tt, tid - kP1Noise);
-    } else if (tid < kP1Feat) {
+                              kActSigmoid, L.tt, (wv == 10 ? 128 : 64 * (wv - 6)) + ln);
+    } else if (wv == 11 || wv == 15) {
       if (fv >= 0 && fv < maxnf)
         rnn_gates<1, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, kActSigmoid,
-                              L.tt, tid - kP1Vad);
-    } else if (tid < kP1Gain) {
-      if (t + 1 < maxnf) feat_c(t + 1, tid - kP1Feat);
-    } else if (tid < kP1Gain + 48) {  // gain smoothing g = max(g, .6*lastg) (denoise.c), frame t-5
+                              L.tt, (wv == 15 ? 64 : 0) + ln);
+    } else if (wv == 8 && ln < 48) {  // gain smoothing g = max(g, .6*lastg) (denoise.c), frame t-5
       const int f5 = t - 5;
-      for (int idx = tid - kP1Gain; f5 >= 0 && idx < S * kBands; idx += 48) {
+      for (int idx = ln; f5 >= 0 && idx < S * kBands; idx += 48) {
         const int s = idx / kBands, i = idx - s * kBands;
         if (!L.act[f5 & 7][s]) continue;
         const long long f = L.fbase[s] + f5;
@@ -1799,11 +1810,14 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
         a.gr[f * kBands + i] = gi;
         a.gs[f * kBands + i] = gsm;
       }
-    } else if (tid < kP1Gain + 48 + S) {  // vad_output of frame t-3 (P2 of step t-1)
-      const int s = tid - kP1Gain - 48, fw = t - 3;
+    } else if (wv == 8 && ln < 48 + S) {  // vad_output of frame t-3 (P2 of step t-1)
+      const int s = ln - 48, fw = t - 3;
       if (fw >= 0 && fw < maxnf && L.act[fw & 7][s]) a.vadf[L.fbase[s] + fw] = L.vo[s];
+    } else if (wv == 9 && ln < S) {  // spectral variability of frame t (features: P2 of step t-1)
+      if (t < maxnf) feat_d(t, ln);
     }
     ROLE_END(0);
+    if (pf_lane) L.pf[pfs][pfi] = pf_now;
     __syncthreads();
     RSTAMP(0);
     ROLE_BEGIN();
@@ -1833,11 +1847,10 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       if (fn >= 0 && fn < maxnf)
         rnn_gates<8, S, G, 0>(L.W, RnnIn{L.gvT[fn & 3], nullptr, nullptr}, nullptr, L.vo, ra[8], L.tt,
                               tid - kP2VadOut);
-    } else if (tid >= kP2Var && tid < kP2Var + S) {
-      if (t + 1 < maxnf) feat_d(t + 1, tid - kP2Var);
+    } else if (tid >= kP2Feat && tid < kP2Feat + kFeatItems) {
+      if (t + 1 < maxnf) feat_c(t + 1, tid - kP2Feat);
     }
     ROLE_END(1);
-    if (pf_lane) L.pf[pfs][pfi] = pf_now;
     __syncthreads();
     RSTAMP(1);
   }
@@ -1846,8 +1859,8 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   // P1 roles -> stamps[2..6], P2 roles -> stamps[8..14] (tid 0 and 384 lead a
   // role in both phases)
   if (a.stamps) {
-    const int p1[5] = {kP1Den, kP1Noise, kP1Vad, kP1Feat, kP1Gain};
-    const int p2[7] = {kP2Den, kP2Noise, kP2Vad, kP2Dense, kP2Out, kP2VadOut, kP2Var};
+    const int p1[5] = {kP1Den, kP1Noise, kP1Vad, kP1Var, kP1Gain};
+    const int p2[7] = {kP2Den, kP2Noise, kP2Vad, kP2Dense, kP2Out, kP2VadOut, kP2Feat};
     for (int i = 0; i < 5; i++)
       if (tid == p1[i]) atomicAdd(&a.stamps[2 + i], racc2[0]);
     for (int i = 0; i < 7; i++)

@@ -19,11 +19,11 @@ T = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 MODE = sys.argv[3] if len(sys.argv) > 3 else "fused"
 FFTA = []
 if MODE == "staged" and os.environ.get("FVAD_RNN", "3") == "3":
-    NAMES = ["P1 z|r gates + features(t+1) + gains(t-5)",
-             "P2 candidates, dense(t), outputs, spectral variability",
-             "  P1 role: denoise z|r", "  P1 role: noise z|r", "  P1 role: vad z|r", "  P1 role: features",
+    NAMES = ["P1 z|r gates + spectral variability(t) + gains(t-5)",
+             "P2 candidates, dense(t), outputs, features(t+1)",
+             "  P1 role: denoise z|r", "  P1 role: noise z|r", "  P1 role: vad z|r", "  P1 role: spectral var",
              "  P1 role: gains", "", "  P2 role: denoise h", "  P2 role: noise h", "  P2 role: vad h",
-             "  P2 role: dense", "  P2 role: denoise_output", "  P2 role: vad_output", "  P2 role: spectral var"]
+             "  P2 role: dense", "  P2 role: denoise_output", "  P2 role: vad_output", "  P2 role: features"]
     ROLES = True
 elif MODE == "staged" and os.environ.get("FVAD_RNN") == "2":
     NAMES = ["P1 z|r gates + features(t+1) + gains(t-3)", "P2 candidates + spectral variability",
@@ -68,9 +68,9 @@ if MODE == "staged":
 if MODE == "staged":
     PIT = ["Q0 xf + coarse Syy -> LDS", "Q1 coarse xcorr", "Q2 coarse scan", "Q3 fine xcorr", "Q4 fine scan",
            "Q5 remove_doubling products"]
-    groups = B * 2 * T / 16.0
+    groups = B * 2 * T / 8.0
     pt = sum(buf[32:38])
-    print("k_pcorr: stamped cycles per 16-frame group per WG: %.0f" % (pt / max(1, groups)))
+    print("k_pcorr: stamped cycles per 8-frame group per WG: %.0f" % (pt / max(1, groups)))
     for i, n in enumerate(PIT):
         print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[32 + i] / max(1, pt), buf[32 + i] / groups))
 
