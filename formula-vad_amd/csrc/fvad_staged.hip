@@ -1738,19 +1738,17 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   // + vad_output store wave 8, spectral variability of frame t wave 9.
   // (The constants name each role's first thread, for the stamps build.)
   constexpr int kP1Den = 0, kP1Noise = 384, kP1Vad = 704, kP1Var = 576, kP1Gain = 512;
-  // P2: denoise h 0..191, noise h 0..95, vad h 0..47, dense 0..47,
-  // denoise_output 0..43, vad_output (one lane, 8 streams), features of frame
-  // t+1 (296 items)
-  // every role starts on a wave boundary: a wave holding lanes of two roles
-  // runs both branches one after the other (measured: the wave with noise h
-  // and vad h lanes set the phase at 19.6 k cycles)
-  constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 384, kP2Out = 448, kP2VadOut = 512,
+  // P2 wave plan, balanced over the residue classes the same way (a wave
+  // holding lanes of two roles set the phase at 19.6 k cycles before): denoise
+  // h waves 0..2 (192 tasks), noise h waves 3, 7 (96), denoise_output wave 4
+  // (44), vad h wave 5 (48), dense of frame t wave 6 (48), vad_output wave 8
+  // (2 lanes), features of frame t+1 waves 9..13 (296 items).
+  constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 384, kP2Out = 256, kP2VadOut = 512,
                 kP2Feat = 576;
   constexpr int kFeatItems = S * (kBands + 7 + kCeps);
-  static_assert(kP2Feat + kFeatItems <= NT, "P2 feature lanes");
-  static_assert(kP2Noise - kP2Den >= 96 * kR3G && kP2Vad - kP2Noise >= 48 * kR3G && kP2Dense - kP2Vad >= 24 * kR3G &&
-                    kP2Out - kP2Dense >= 24 * kR3G && kP2VadOut - kP2Out >= 22 * kR3G && kP2Feat - kP2VadOut >= kR3G,
-                "P2 roles");
+  static_assert(kP2Feat + kFeatItems <= 14 * 64 && 96 * kR3G == 192 && 48 * kR3G <= 128 && 22 * kR3G <= 64 &&
+                    24 * kR3G <= 64,
+                "P2 wave plan");
   STAMP_INIT();
 #ifdef FVAD_STAMPS
   // role finish times: the first thread of each role adds (its role's end -
@@ -1823,30 +1821,28 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     ROLE_BEGIN();
     // ---- P2
     const int fo = t - 4;
-    if (tid < kP2Noise) {
+    if (wv < 3) {
       if (fd >= 0 && fd < maxnf)
         rnn_cand<6, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, L.gdT[(fd + 1) & 1], L.zrd,
-                             L.gdT[fd & 1], L.act[fd & 7], ra[6], L.tt, tid - kP2Den);
-    } else if (tid < kP2Vad) {
+                             L.gdT[fd & 1], L.act[fd & 7], ra[6], L.tt, tid);
+    } else if (wv == 3 || wv == 7) {
       if (fn >= 0 && fn < maxnf)
         rnn_cand<4, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
-                             L.gnT[fn & 1], L.act[fn & 7], ra[4], L.tt, tid - kP2Noise);
-    } else if (tid < kP2Dense) {
+                             L.gnT[fn & 1], L.act[fn & 7], ra[4], L.tt, (wv == 7 ? 64 : 0) + ln);
+    } else if (wv == 5) {
       if (fv >= 0 && fv < maxnf)
         rnn_cand<2, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, L.gvT[fv & 3],
-                             L.act[fv & 7], ra[2], L.tt, tid - kP2Vad);
-    } else if (tid < kP2Out) {
+                             L.act[fv & 7], ra[2], L.tt, ln);
+    } else if (wv == 6) {
       if (t < maxnf)
-        rnn_gates<0, S, G, 0>(L.W, RnnIn{L.featT[t & 7], nullptr, nullptr}, nullptr, L.doutT[t & 3], ra[0], L.tt,
-                              tid - kP2Dense);
-    } else if (tid < kP2VadOut) {
+        rnn_gates<0, S, G, 0>(L.W, RnnIn{L.featT[t & 7], nullptr, nullptr}, nullptr, L.doutT[t & 3], ra[0], L.tt, ln);
+    } else if (wv == 4) {
       if (fo >= 0 && fo < maxnf)
-        rnn_gates<7, S, G, 0>(L.W, RnnIn{L.gdT[fo & 1], nullptr, nullptr}, nullptr, L.gout, ra[7], L.tt, tid - kP2Out);
-    } else if (tid < kP2VadOut + G) {
+        rnn_gates<7, S, G, 0>(L.W, RnnIn{L.gdT[fo & 1], nullptr, nullptr}, nullptr, L.gout, ra[7], L.tt, ln);
+    } else if (wv == 8 && ln < G) {
       // vad_output(t-2) -> L.vo, stored by the next step's P1
       if (fn >= 0 && fn < maxnf)
-        rnn_gates<8, S, G, 0>(L.W, RnnIn{L.gvT[fn & 3], nullptr, nullptr}, nullptr, L.vo, ra[8], L.tt,
-                              tid - kP2VadOut);
+        rnn_gates<8, S, G, 0>(L.W, RnnIn{L.gvT[fn & 3], nullptr, nullptr}, nullptr, L.vo, ra[8], L.tt, ln);
     } else if (tid >= kP2Feat && tid < kP2Feat + kFeatItems) {
       if (t + 1 < maxnf) feat_c(t + 1, tid - kP2Feat);
     }
