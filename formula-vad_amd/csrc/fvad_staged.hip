@@ -716,18 +716,21 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
   int *istp = reinterpret_cast<int *>(stp);
   int last_period = istp[st::kLastPeriod];
   float last_gain = stp[st::kLastGain];
-  // the next frame's record loads while this frame's candidates are compared
+  // records load two frames ahead of the comparisons through a 3-slot
+  // register ring (slot names fixed by the 3-way unrolled loop), so each
+  // frame's loads have two frames of compares to land (one frame ahead made
+  // every step wait for its own prefetch)
   constexpr int N4 = rec::kSize / 4;
-  float r[rec::kSize], rn[rec::kSize];
   const float4 *src = reinterpret_cast<const float4 *>(a.rec + (size_t)s * a.V * rec::kSize);
+  float r0[rec::kSize], r1[rec::kSize], r2[rec::kSize];
+  auto load = [&](float (&r)[rec::kSize], int v) {
+    if (v < nf) {
 #pragma unroll
-  for (int i = 0; i < N4; i++) *reinterpret_cast<float4 *>(&r[4 * i]) = src[i];
-  for (int v = 0; v < nf; v++) {
-    const size_t f = (size_t)s * a.V + v;
-    if (v + 1 < nf) {
-#pragma unroll
-      for (int i = 0; i < N4; i++) *reinterpret_cast<float4 *>(&rn[4 * i]) = src[(size_t)(v + 1) * N4 + i];
+      for (int i = 0; i < N4; i++) *reinterpret_cast<float4 *>(&r[4 * i]) = src[(size_t)v * N4 + i];
     }
+  };
+  auto step = [&](const float (&r)[rec::kSize], int v) {
+    const size_t f = (size_t)s * a.V + v;
     const int T0 = __float_as_int(r[rec::kT0]);
     const int nv = __float_as_int(r[rec::kNValid]);
     const int prev_period = last_period / 2;
@@ -782,8 +785,18 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
     a.pitch[f] = pi;
     last_period = pi;
     last_gain = pg;
-#pragma unroll
-    for (int i = 0; i < rec::kSize; i++) r[i] = rn[i];
+  };
+  load(r0, 0);
+  load(r1, 1);
+  for (int v = 0; v < nf; v += 3) {
+    load(r2, v + 2);
+    step(r0, v);
+    if (v + 1 >= nf) break;
+    load(r0, v + 3);
+    step(r1, v + 1);
+    if (v + 2 >= nf) break;
+    load(r1, v + 4);
+    step(r2, v + 2);
   }
   istp[st::kLastPeriod] = last_period;
   stp[st::kLastGain] = last_gain;
@@ -1742,7 +1755,9 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   // holding lanes of two roles set the phase at 19.6 k cycles before): denoise
   // h waves 0..2 (192 tasks), noise h waves 3, 7 (96), denoise_output wave 4
   // (44), vad h wave 5 (48), dense of frame t wave 6 (48), vad_output wave 8
-  // (2 lanes), features of frame t+1 waves 9..13 (296 items).
+  // (2 lanes), features of frame t+1 waves 9..13 (296 items).  (Denoise h with
+  // 2 streams per lane on 6 waves shortened its chain to 11.1 k cycles but the
+  // extra waves stretched the other roles: 15.3 vs 14.6 k per phase.)
   constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 384, kP2Out = 256, kP2VadOut = 512,
                 kP2Feat = 576;
   constexpr int kFeatItems = S * (kBands + 7 + kCeps);

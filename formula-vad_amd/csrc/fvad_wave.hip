@@ -399,13 +399,20 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftbw(StagedArgs a) {
     if (t < 0) continue;
     const long long wstart = a.win_start[(size_t)s * a.wmax + j];
     const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
-    // layout X: register r = d1 + 4 d0 holds packed input k = lane + 64 r
+    // layout X: register r = d1 + 4 d0 holds packed input k = lane + 64 r;
+    // ring positions: one 64-bit remainder per item, then 2k + 1 < 2048 <=
+    // ring_len needs at most one wrap
+    const int rl = a.ring_len, w0 = (int)(wstart % rl);
     float2 v[16];
 #pragma unroll
     for (int r = 0; r < 16; r++) {
       const int k = lane + 64 * r;
-      const float t0 = ring[(wstart + 2 * k) % a.ring_len] * P->hannb[2 * k];
-      const float t1 = ring[(wstart + 2 * k + 1) % a.ring_len] * P->hannb[2 * k + 1];
+      int i0 = w0 + 2 * k;
+      i0 -= (i0 >= rl) ? rl : 0;
+      int i1 = i0 + 1;
+      i1 -= (i1 >= rl) ? rl : 0;
+      const float t0 = ring[i0] * P->hannb[2 * k];
+      const float t1 = ring[i1] * P->hannb[2 * k + 1];
       v[r] = make_float2(t0, t1);
     }
     // stage 1 (m = 1, over d0), stage 2 (m = 4, over d1, u = d0)
