@@ -720,7 +720,12 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
   e->ev = e->evs[e->ev_slot];
   int rc = collect_slot(e, e->ev_slot);
   if (rc) return rc;
-  return launch(e, n_ticks, false, true);
+  // FVAD_NO_EVENTS=1: no timing events (diagnostic: their cost on the push)
+  static const bool no_events = [] {
+    const char *v = getenv("FVAD_NO_EVENTS");
+    return v && atoi(v) == 1;
+  }();
+  return launch(e, n_ticks, false, !no_events);
 }
 
 extern "C" int fvad_engine_sync(fvad_engine *e) {
