@@ -47,17 +47,29 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
   const int tid = threadIdx.x;
   const int Vr = a.n_ticks * a.n_channels;
   const int n_sb = (a.n_streams + 63) >> 6;
-  const long long ngroups = (long long)n_sb * Vr * 4 * kHalves;
+  const long long nquarters = (long long)n_sb * Vr * 4;
+  const long long ngroups = (nquarters + 7) / 8 * 16;  // whole blocks of 16 units; units past the quarters skip
   STAMP_INIT();
   __shared__ long long gq;
   if (threadIdx.x == 0) gq = take_group(a, kWorkPcorr);
   __syncthreads();
   long long g = gq;
   while (g < ngroups) {
-    // group g = (quarter tile g / kHalves, frame columns h*kPcF ..): T is
-    // the group's first column, rows keep the quarter's 16-column pitch
-    const long long gq4 = g / kHalves;
-    const int h = (int)(g - gq4 * kHalves);
+    // group g -> (quarter tile, frame columns h*kPcF ..): T is the group's
+    // first column, rows keep the quarter's 16-column pitch.  The halves of a
+    // quarter are units x + 16 b and x + 16 b + 8, both from queue x (one
+    // XCD), so the second half's 64-byte row reads find the first half's
+    // 128-byte lines in that XCD's L2.
+    static_assert(kHalves == 2 && kQueues == 8, "k_pcorr unit map");
+    const long long gq4 = (g >> 4) * 8 + (g & 7);
+    const int h = (int)((g >> 3) & 1);
+    if (gq4 >= nquarters) {  // padding unit of the last block (uniform branch)
+      __syncthreads();
+      if (tid == 0) gq = take_group(a, kWorkPcorr);
+      __syncthreads();
+      g = gq;
+      continue;
+    }
     const float *T = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter + h * kPcF;
     if (tid < kPcF) {
       const long long t = gq4 >> 2;
