@@ -547,7 +547,12 @@ __device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, float
 }
 static_assert(384 % kLpStep == 0 && 480 % kLpStep == 0 && kLpStep % 2 == 0, "pass-2 regions");
 
-__global__ void __launch_bounds__(256, 2) k_plpc(StagedArgs a) {
+// occupancy: 186 VGPRs, 2 workgroups per CU; 3 measured the same (the kernel
+// is HBM-bound), 4 slower (spills)
+#ifndef FVAD_PLPC_OCC
+#define FVAD_PLPC_OCC 2
+#endif
+__global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
   __shared__ float stg_all[4][kLpRows * kLpCols];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   float *stg = stg_all[w];
