@@ -2577,6 +2577,10 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
 // k_vadm_hbm: the same machine, long-term buffers walked in HBM, no LDS, 16
 // lanes per workgroup: a light kernel that co-runs with the next push's
 // pipeline on the engine's side stream.
+#ifndef FVAD_VADM_LANES
+#define FVAD_VADM_LANES 64
+#endif
+constexpr int kVadmHbmLanes = FVAD_VADM_LANES;  // streams per workgroup (one wave); 16 / 32 / 64 measured within noise, 64 takes fewest wave slots
 __global__ void __launch_bounds__(64) k_vadm_hbm(StagedArgs a) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.n_streams || ticks_of(a, s) <= 0) return;
@@ -2587,7 +2591,8 @@ __global__ void __launch_bounds__(64) k_vadm_hbm(StagedArgs a) {
 hipError_t launch_vadm(const StagedArgs &a, bool overlap, hipStream_t stream) {
   (void)hipGetLastError();
   if (overlap)
-    hipLaunchKernelGGL(k_vadm_hbm, dim3((a.n_streams + 15) / 16), dim3(16), 0, stream, a);
+    hipLaunchKernelGGL(k_vadm_hbm, dim3((a.n_streams + kVadmHbmLanes - 1) / kVadmHbmLanes), dim3(kVadmHbmLanes), 0,
+                       stream, a);
   else
     hipLaunchKernelGGL(k_vadm, dim3((a.n_streams + kVadmS - 1) / kVadmS), dim3(64), 0, stream, a);
   return hipGetLastError();
