@@ -710,74 +710,86 @@ __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_select: remove_doubling's sequential selection (one lane per stream).
+// k_select: remove_doubling's sequential selection.  The frames of a stream
+// stay sequential (prev_period / prev_gain), but a frame's 14 candidate tests
+// are independent given them: 16 lanes per stream (4 streams per wave), lane
+// k tests candidate k (T1 of k + 2), a ballot finds the last passing one (the
+// reference loop keeps overwriting, so the highest k wins) and its values are
+// read from its lane.  Every comparison and value is the reference's.  A
+// frame's record loads four frames ahead through a 4-slot register ring.
 // ---------------------------------------------------------------------------
+constexpr int kSelStreams = 4;  // streams per 64-thread workgroup
+struct SelRec {
+  int T0, nv, Tk, offk, off0;
+  float g0, xy0, yy0, gk, xyk, yyk;
+};
+__device__ __forceinline__ void sel_load(SelRec &r, const float *__restrict__ row, int k, bool on) {
+  if (!on) return;
+  r.T0 = __float_as_int(row[rec::kT0]);
+  r.nv = __float_as_int(row[rec::kNValid]);
+  r.g0 = row[rec::kG0];
+  r.xy0 = row[rec::kXy0];
+  r.yy0 = row[rec::kYy0];
+  r.off0 = __float_as_int(row[rec::kOff0]);
+  const float *q = row + rec::kK + min(k, 13) * rec::kKStride;
+  r.Tk = __float_as_int(q[0]);
+  r.gk = q[1];
+  r.xyk = q[2];
+  r.yyk = q[3];
+  r.offk = __float_as_int(q[4]);
+}
+
 __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= a.n_streams) return;
-  const int nf = ticks_of(a, s) * a.n_channels;
-  if (nf <= 0) return;
-  float *stp = a.state + (size_t)s * st::kWords;
-  int *istp = reinterpret_cast<int *>(stp);
-  int last_period = istp[st::kLastPeriod];
-  float last_gain = stp[st::kLastGain];
-  // records load two frames ahead of the comparisons through a 3-slot
-  // register ring (slot names fixed by the 3-way unrolled loop), so each
-  // frame's loads have two frames of compares to land (one frame ahead made
-  // every step wait for its own prefetch)
-  constexpr int N4 = rec::kSize / 4;
-  const float4 *src = reinterpret_cast<const float4 *>(a.rec + (size_t)s * a.V * rec::kSize);
-  float r0[rec::kSize], r1[rec::kSize], r2[rec::kSize];
-  auto load = [&](float (&r)[rec::kSize], int v) {
-    if (v < nf) {
+  const int lane = threadIdx.x, sl = lane >> 4, k = lane & 15;
+  const int s = blockIdx.x * kSelStreams + sl;
+  const bool sok = s < a.n_streams;
+  const int nf = sok ? ticks_of(a, s) * a.n_channels : 0;
+  int nfw = nf;  // frames of the wave's longest stream (shuffles need every lane)
 #pragma unroll
-      for (int i = 0; i < N4; i++) *reinterpret_cast<float4 *>(&r[4 * i]) = src[(size_t)v * N4 + i];
-    }
-  };
-  auto step = [&](const float (&r)[rec::kSize], int v) {
-    const size_t f = (size_t)s * a.V + v;
-    const int T0 = __float_as_int(r[rec::kT0]);
-    const int nv = __float_as_int(r[rec::kNValid]);
+  for (int d = 16; d < 64; d <<= 1) nfw = max(nfw, __shfl_xor(nfw, d));
+  if (nfw <= 0) return;
+  float *stp = a.state + (size_t)(sok ? s : 0) * st::kWords;
+  int *istp = reinterpret_cast<int *>(stp);
+  int last_period = sok ? istp[st::kLastPeriod] : 0;
+  float last_gain = sok ? stp[st::kLastGain] : 0.0f;
+  const float *rows = a.rec + (size_t)(sok ? s : 0) * a.V * rec::kSize;
+  const int K = k + 2;  // remove_doubling's k for this lane's candidate
+  auto step = [&](const SelRec &r, int v) {
+    const bool on = v < nf;
     const int prev_period = last_period / 2;
     const float prev_gain = last_gain;
-    const float g0 = r[rec::kG0];
-    float best_xy = r[rec::kXy0], best_yy = r[rec::kYy0], gg = g0;
-    int T = T0, offset = __float_as_int(r[rec::kOff0]);
-#pragma unroll
-    for (int k = 2; k <= 15; k++) {
-      const int kk = k - 2;
-      const float *q = r + rec::kK + kk * rec::kKStride;
-      const int T1 = __float_as_int(q[0]);
-      const float g1 = q[1];
+    bool pass = false;
+    if (on && k < 14 && k < r.nv) {
+      const int T1 = r.Tk;
       float cont;
       if (abs(T1 - prev_period) <= 1)
         cont = prev_gain;
-      else if (abs(T1 - prev_period) <= 2 && 5 * k * k < T0)
+      else if (abs(T1 - prev_period) <= 2 && 5 * K * K < r.T0)
         cont = .5f * prev_gain;
       else
         cont = 0;
       float thresh;
       {
-        const float vv = .7f * g0 - cont;
+        const float vv = .7f * r.g0 - cont;
         thresh = (.3f > vv) ? .3f : vv;
       }
       if (T1 < 3 * 30) {
-        const float vv = .85f * g0 - cont;
+        const float vv = .85f * r.g0 - cont;
         thresh = (.4f > vv) ? .4f : vv;
       } else if (T1 < 2 * 30) {
-        const float vv = .9f * g0 - cont;
+        const float vv = .9f * r.g0 - cont;
         thresh = (.5f > vv) ? .5f : vv;
       }
-      // candidates are a prefix (k < 2 + nv): the reference loop stops at the
-      // first T1 < 30
-      if (kk < nv && g1 > thresh) {
-        best_xy = q[2];
-        best_yy = q[3];
-        T = T1;
-        gg = g1;
-        offset = __float_as_int(q[4]);
-      }
+      pass = r.gk > thresh;
     }
+    const unsigned seg = (unsigned)(__ballot(pass) >> (16 * sl)) & 0x3fffu;
+    const int win = seg ? 31 - __clz(seg) : 0;
+    const int src = 16 * sl + win;
+    const float wxy = __shfl(r.xyk, src), wyy = __shfl(r.yyk, src), wg = __shfl(r.gk, src);
+    const int wT = __shfl(r.Tk, src), woff = __shfl(r.offk, src);
+    float best_xy = seg ? wxy : r.xy0, best_yy = seg ? wyy : r.yy0, gg = seg ? wg : r.g0;
+    const int T = seg ? wT : r.T0, offset = seg ? woff : r.off0;
+    if (!on) return;
     best_xy = (0 > best_xy) ? 0 : best_xy;
     float pg;
     if (best_yy <= best_xy)
@@ -787,24 +799,31 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
     if (pg > gg) pg = gg;
     int pi = 2 * T + offset;
     if (pi < kPitchMin) pi = kPitchMin;
-    a.pitch[f] = pi;
+    if (k == 0) a.pitch[(size_t)s * a.V + v] = pi;
     last_period = pi;
     last_gain = pg;
   };
-  load(r0, 0);
-  load(r1, 1);
-  for (int v = 0; v < nf; v += 3) {
-    load(r2, v + 2);
+  SelRec r0{}, r1{}, r2{}, r3{};
+  sel_load(r0, rows, k, 0 < nf);
+  sel_load(r1, rows + rec::kSize, k, 1 < nf);
+  sel_load(r2, rows + 2 * rec::kSize, k, 2 < nf);
+  for (int v = 0; v < nfw; v += 4) {
+    sel_load(r3, rows + (size_t)(v + 3) * rec::kSize, k, v + 3 < nf);
     step(r0, v);
-    if (v + 1 >= nf) break;
-    load(r0, v + 3);
+    if (v + 1 >= nfw) break;
+    sel_load(r0, rows + (size_t)(v + 4) * rec::kSize, k, v + 4 < nf);
     step(r1, v + 1);
-    if (v + 2 >= nf) break;
-    load(r1, v + 4);
+    if (v + 2 >= nfw) break;
+    sel_load(r1, rows + (size_t)(v + 5) * rec::kSize, k, v + 5 < nf);
     step(r2, v + 2);
+    if (v + 3 >= nfw) break;
+    sel_load(r2, rows + (size_t)(v + 6) * rec::kSize, k, v + 6 < nf);
+    step(r3, v + 3);
   }
-  istp[st::kLastPeriod] = last_period;
-  stp[st::kLastGain] = last_gain;
+  if (sok && nf > 0 && k == 0) {
+    istp[st::kLastPeriod] = last_period;
+    stp[st::kLastGain] = last_gain;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2537,7 +2556,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
     (void)launch_pcorr(a, tiles, n_cu, stream);
   }
   rec(5);
-  hipLaunchKernelGGL(k_select, dim3(lane_blocks), dim3(16), 0, stream, a);
+  hipLaunchKernelGGL(k_select, dim3((a.n_streams + kSelStreams - 1) / kSelStreams), dim3(64), 0, stream, a);
   rec(6);
   (void)hipStreamWaitEvent(stream, st.join, 0);  // join
   rec(7);
