@@ -227,6 +227,7 @@ def main():
     compute_bound = c["flops"] / c["bytes"] >= ridge
     traffic = None
     pmc_src = None
+    push_bytes = None
     if os.path.exists(args.pmc_json):
         try:
             with open(args.pmc_json) as f:
@@ -234,6 +235,8 @@ def main():
             if (pm.get("streams"), pm.get("ticks"), pm.get("channels"), pm.get("mode")) == (B, T, Ch, args.mode):
                 traffic = pm.get("bytes_per_launch", {}).get(dom)
                 pmc_src = os.path.relpath(args.pmc_json, ROOT)
+                # every kernel of a push (the side-stream ones included)
+                push_bytes = sum(v for n, v in pm.get("bytes_per_launch", {}).items() if n in kt["kernels"])
         except Exception:
             traffic = None
     if compute_bound:
@@ -252,6 +255,11 @@ def main():
         "timed_launches": kt["runs"],
         "kernels": kernels,
     }
+    if push_bytes:
+        # whole-push HBM traffic (PMC bytes of all its kernels) over the
+        # measured time per push: the pipeline's average HBM utilisation
+        gbs = push_bytes / (ms_per_step / 1000.0) / 1e9
+        roofline["push_hbm"] = {"bytes": push_bytes, "gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
     cpu = None
     if args.cpu_baseline and world == 1:
         try:
