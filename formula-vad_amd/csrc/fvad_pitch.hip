@@ -15,12 +15,12 @@
 namespace fvad {
 
 // ---------------------------------------------------------------------------
-// k_pcorr: one 128-thread workgroup per half quarter tile (8 streams at one
-// frame position; 38.5 KB of LDS, so 4 workgroups share a CU and a barrier
-// stalls 2 waves, not 4).
+// k_pcorr: one 256-thread workgroup per half quarter tile (8 streams at one
+// frame position; 38.5 KB of LDS, so 4 workgroups share a CU, 4 waves per
+// SIMD at <= 128 VGPRs).
 //   Q0 xf (rows 0..863) and the coarse Syy sequence -> LDS
-//   Q1 coarse xcorr: lane = (frame, 10 consecutive lags), a register window of
-//      10 y values slides one sample per step (2 LDS reads per 10 MACs)
+//   Q1 coarse xcorr: lane = (frame, 5 consecutive lags), a register window of
+//      5 y values slides one sample per step (2 LDS reads per 5 MACs)
 //   Q2 coarse find_best_pitch, lane per frame; the fine Syy values at the
 //      <= 10 candidate lags are fetched here, used in Q4
 //   Q3 fine xcorr at the <= 10 lags within +-2 of 2*best (others are 0)
@@ -31,7 +31,8 @@ namespace fvad {
 //      per read), the lane's window parity resolved by selects
 // ---------------------------------------------------------------------------
 constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
-constexpr int kPcNT = 16 * kPcF;       // 16 lanes per frame in Q1
+constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
+constexpr int kPcNT = kPcL * kPcF;
 static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
 constexpr int kPcXS = 870;  // xf row pitch: even (8-byte aligned pairs in Q5), = 6 mod 8 (conflict-free Q0 stores)
 constexpr int kPcSP = 153;  // coarse xcorr / Syy row pitch (odd; >= 147 rounded up to the scan block)
@@ -101,8 +102,9 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(0);
     // Q1: xcorr[k] = sum_j x_lp4[j] y_lp4[j+k], x_lp4[j] = xf[384+2j], y_lp4[m] = xf[2m]
     {
-      constexpr int R = 10;
-      const int fr = tid >> 4, k0 = R * (tid & 15);
+      constexpr int R = 5;
+      static_assert(R * (kPcL - 1) >= 147 && 240 % R == 0, "Q1 lag blocks");
+      const int fr = tid / kPcL, k0 = R * (tid % kPcL);
       if (k0 < 147) {
         const float *X = xf[fr] + (kPitchMax >> 1);
         const float *Y = xf[fr] + 2 * k0;
