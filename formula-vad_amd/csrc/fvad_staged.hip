@@ -55,16 +55,21 @@ static_assert(kTermOff >= 2 * kFreq && kTermOff % 4 == 0 && kTermOff + 800 <= 2 
 // ---------------------------------------------------------------------------
 // k_prep3: high-pass biquad (a serial IIR with f64 intermediates: no exact
 // parallel form exists, so one lane walks one stream), s16 scaling, RMS volume
-// ratio, pitch history.  It uses no LDS and 2 waves per 8 streams: the engine
-// runs it on its own stream beside the previous push's kernels (xs, ratio and
-// ticks are double-buffered), where it must not take the LDS or the wave
-// slots those kernels are sized for.  Wave 0: lane = stream, the biquad chain
-// straight from the input rows (16-byte loads through an 8-deep prefetch
-// ring, 16-byte stores into the stream's xs row); wave 1: lane = channel-slot,
-// the per-tick RMS sums and the volume ratio (channels of a stream are
-// neighbouring lanes).
+// ratio, pitch history.  It uses no LDS and one wave per 64 channel-slots:
+// the engine runs it on its own stream beside the previous push's kernels
+// (xs, ratio and ticks are double-buffered), where it must not take the LDS
+// or the wave slots those kernels are sized for.  Lane = stream: the biquad
+// chain straight from the input rows (16-byte loads through an 8-deep
+// prefetch ring, 16-byte stores into the stream's xs row), and beside it, off
+// the chain's dependency path, each channel's RMS sum and per tick the volume
+// ratio.  (A second wave that re-read the input for the RMS sums cost the
+// co-running kernels 0.17 ms per push.)
 // ---------------------------------------------------------------------------
-constexpr int kPrepSlots = 64;  // channel-slots per workgroup (32 stereo streams)
+#ifndef FVAD_PREP_SLOTS
+#define FVAD_PREP_SLOTS 64
+#endif
+constexpr int kPrepSlots = FVAD_PREP_SLOTS;  // channel-slots per workgroup (32 stereo streams)
+__host__ __device__ constexpr int prep_streams(int C) { return kPrepSlots / C < 64 ? kPrepSlots / C : 64; }
 #ifndef FVAD_PREP_RING
 #define FVAD_PREP_RING 8
 #endif
@@ -90,6 +95,8 @@ struct PrepSrc {
 
 template <bool Scaled>
 __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, float &mem0, float &mem1) {
+  constexpr int kChunksCh = kFrame / 4;  // float4 chunks of one channel's frame
+  static_assert(kChunksCh % kPrepRing == 0, "ring blocks end at channel boundaries");
   const int C = a.n_channels;
   const int per_tick = C * (kFrame / 4);
   PrepSrc src{a.pcm + (size_t)s * C * kFrame, 0, per_tick, (size_t)(a.n_streams - 1) * C * kFrame};
@@ -110,6 +117,11 @@ __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, f
     mem1 = (float)__builtin_fma(-(double)a1, yd, b1 * (double)xi);
     return yi;
   };
+  // RMS volume (VAD.zig:253-272): sum of squares of the raw samples of each
+  // channel's frame in sample order, vol = sqrt(sum / 480), ratio = min / max
+  // over the stream's channels in channel order
+  float sum = 0, vmin = 1, vmax = 0;
+  int jt = 0, t = 0;  // chunk within the tick, tick
   for (int j0 = 0; j0 < nch; j0 += kPrepRing) {
 #pragma unroll
     for (int u = 0; u < kPrepRing; u++) {
@@ -121,22 +133,40 @@ __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, f
       y.z = step(x.z);
       y.w = step(x.w);
       dst[j0 + u] = y;
+      sum += x.x * x.x;
+      sum += x.y * x.y;
+      sum += x.z * x.z;
+      sum += x.w * x.w;
+    }
+    jt += kPrepRing;
+    if (jt % kChunksCh == 0) {
+      const float vol = sqrtf(sum / (float)kFrame);
+      sum = 0;
+      if (vol < vmin) vmin = vol;
+      if (vol > vmax) vmax = vol;
+      if (jt == per_tick) {
+        a.ratio[(size_t)t * a.n_streams + s] = (vmax == 0) ? 0 : vmin / vmax;
+        vmin = 1;
+        vmax = 0;
+        jt = 0;
+        t++;
+      }
     }
   }
 }
 
-__global__ void __launch_bounds__(128) k_prep3(StagedArgs a) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int C = a.n_channels, S = kPrepSlots / C, sb = blockIdx.x * S;
+__global__ void __launch_bounds__(64) k_prep3(StagedArgs a) {
+  const int tid = threadIdx.x, lane = tid;
+  const int C = a.n_channels, S = prep_streams(C), sb = blockIdx.x * S;
   const int ns = min(S, a.n_streams - sb);  // streams in this workgroup
   if (ns <= 0) return;
   // pitch history of every stream -> xs[s][0..1248)
-  for (int idx = tid; idx < ns * kHist; idx += 128) {
+  for (int idx = tid; idx < ns * kHist; idx += 64) {
     const int s = idx / kHist, i = idx - s * kHist;
     if (ticks_of(a, sb + s) > 0)
       a.xs[(size_t)(sb + s) * a.L + i] = a.state[(size_t)(sb + s) * st::kWords + st::kPitch + kFrame + i];
   }
-  if (wave == 0) {
+  {
     // the chain wave shares its SIMD with the previous push's kernels: its
     // latency-bound instruction stream goes first
     __builtin_amdgcn_s_setprio(3);
@@ -153,46 +183,10 @@ __global__ void __launch_bounds__(128) k_prep3(StagedArgs a) {
         hp[1] = mem1;
       }
     }
-  } else {
-    // lane = channel-slot (s, c); every lane runs the tick loop (shuffles)
-    const int ls = min(lane, ns * C - 1);
-    const int sl = ls / C, c = ls - sl * C, s = sb + sl;
-    const int nt = lane < ns * C ? ticks_of(a, s) : 0;
-    const float *x = a.pcm + ((size_t)s * C + c) * kFrame;
-    const size_t tick_stride = (size_t)a.n_streams * C * kFrame;
-    for (int t = 0; t < a.n_ticks; t++) {
-      float sum = 0;
-      if (t < nt) {
-        const float4 *x4 = reinterpret_cast<const float4 *>(x + (size_t)t * tick_stride);
-        float4 ring[kPrepRing];
-#pragma unroll
-        for (int u = 0; u < kPrepRing; u++) ring[u] = x4[u];
-        for (int j0 = 0; j0 < kFrame / 4; j0 += kPrepRing) {
-#pragma unroll
-          for (int u = 0; u < kPrepRing; u++) {
-            const float4 v = ring[u];
-            if (j0 + u + kPrepRing < kFrame / 4) ring[u] = x4[j0 + u + kPrepRing];
-            sum += v.x * v.x;
-            sum += v.y * v.y;
-            sum += v.z * v.z;
-            sum += v.w * v.w;
-          }
-        }
-      }
-      const float vol = sqrtf(sum / (float)kFrame);
-      // volume ratio of the stream (VAD.zig:253-272): min / max over its channels
-      float vmin = 1, vmax = 0;
-      for (int c2 = 0; c2 < C; c2++) {
-        const float vl = __shfl(vol, sl * C + c2);
-        if (vl < vmin) vmin = vl;
-        if (vl > vmax) vmax = vl;
-      }
-      if (lane < ns * C && c == 0 && t < nt) a.ratio[(size_t)t * a.n_streams + s] = (vmax == 0) ? 0 : vmin / vmax;
-    }
   }
   __syncthreads();
   // pitch_buf after the last frame = the last 1728 samples of the row
-  for (int idx = tid; idx < ns * kPitchBuf; idx += 128) {
+  for (int idx = tid; idx < ns * kPitchBuf; idx += 64) {
     const int s = idx / kPitchBuf, i = idx - s * kPitchBuf;
     const int nt = ticks_of(a, sb + s);
     if (nt > 0)
@@ -2503,8 +2497,8 @@ int resident_blocks(K kernel, int threads, int n_cu) {
 
 hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], stream);
-  const int S = kPrepSlots / a.n_channels;
-  hipLaunchKernelGGL(k_prep3, dim3((a.n_streams + S - 1) / S), dim3(128), 0, stream, a);
+  const int S = prep_streams(a.n_channels);
+  hipLaunchKernelGGL(k_prep3, dim3((a.n_streams + S - 1) / S), dim3(64), 0, stream, a);
   if (ev) (void)hipEventRecord(ev[1], stream);
   return hipGetLastError();
 }
