@@ -88,6 +88,11 @@ struct fvad_engine {
   int n_events = 0;           // timing events per launch
   int last_event = 0;         // the one recorded last (the launch's end)
   hipEvent_t ev_copy = nullptr, ev_vadm = nullptr, ev_vt[2][2] = {};  // [slot][begin/end] timing pairs
+  // window outputs of push k in set k & 1 (the second set exists with VADMachines):
+  // k_vadm of push k reads them in place, push k + 2 rewrites them after it
+  int *wflag_b[2] = {};
+  float *wratio_b[2] = {}, *wvad_b[2] = {}, *band_b[2] = {};
+  hipEvent_t ev_vadm_b[2] = {};
   int32_t *d_vflag = nullptr, *d_vticks = nullptr;
   float *d_vwratio = nullptr, *d_vwvad = nullptr, *d_vband = nullptr;
   bool vadm_overlap = true;
@@ -250,7 +255,8 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
 void free_all(fvad_engine *e) {
   void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm,   e->d_xbuf, e->d_ratio_b[0],
                   e->d_ratio_b[1], e->d_ticks_b[0], e->d_ticks_b[1], e->d_xs_b[0], e->d_xs_b[1],
-                  e->d_vad,  e->d_wratio,  e->d_wvad,  e->d_band, e->d_den,   e->d_wflag,
+                  e->d_vad,  e->wratio_b[0] ? e->wratio_b[0] : e->d_wratio,  e->wvad_b[0] ? e->wvad_b[0] : e->d_wvad,
+                  e->band_b[0] ? e->band_b[0] : e->d_band, e->d_den,   e->wflag_b[0] ? e->wflag_b[0] : e->d_wflag,
                   e->d_model, e->d_stamps, e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->vadm.st, e->vadm.buf,
@@ -260,7 +266,8 @@ void free_all(fvad_engine *e) {
   for (auto &set : e->evs)
     for (auto &ev : set)
       if (ev) (void)hipEventDestroy(ev);
-  hipEvent_t evs[] = {e->ev_copy, e->ev_vadm, e->ev_vt[0][0], e->ev_vt[0][1], e->ev_vt[1][0], e->ev_vt[1][1]};
+  hipEvent_t evs[] = {e->ev_copy,     e->ev_vadm,     e->ev_vt[0][0],    e->ev_vt[0][1],
+                      e->ev_vt[1][0], e->ev_vt[1][1], e->ev_vadm_b[0], e->ev_vadm_b[1]};
   for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
   if (e->side) (void)hipStreamDestroy(e->side);
@@ -366,6 +373,10 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     return bail(rc);
   e->d_ratio = e->d_ratio_b[0];
   e->d_ticks = e->d_ticks_b[0];
+  e->wflag_b[0] = e->wflag_b[1] = e->d_wflag;
+  e->wratio_b[0] = e->wratio_b[1] = e->d_wratio;
+  e->wvad_b[0] = e->wvad_b[1] = e->d_wvad;
+  e->band_b[0] = e->band_b[1] = e->d_band;
   if (c.mode == FVAD_MODE_FUSED) {
     if ((rc = dalloc(&e->d_xbuf, frames))) return bail(rc);
   } else {
@@ -478,6 +489,10 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   e->d_xs = e->d_xs_b[b];
   e->d_ratio = e->d_ratio_b[b];
   e->d_ticks = e->d_ticks_b[b];
+  e->d_wflag = e->wflag_b[b];
+  e->d_wratio = e->wratio_b[b];
+  e->d_wvad = e->wvad_b[b];
+  e->d_band = e->band_b[b];
   a.ticks_valid = use_ticks ? e->d_ticks : nullptr;
   a.pcm = e->d_pcm;
   a.xs = e->d_xs;
@@ -538,26 +553,20 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   HIP_TRY(fvad::launch_prep(a, e->pstream, timed ? e->ev : nullptr));
   HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
   HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
+  // window output set b is free once push k-2's k_vadm has read it
+  if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
   HIP_TRY(fvad::launch_staged(a, e->grid_frames, st, timed ? e->ev : nullptr));
   if (e->vadm.n > 0) {
     const fvad_engine_config &c = e->cfg;
     const size_t TB = (size_t)n_ticks * c.n_streams;
-    // the copies may be overwritten only once the previous k_vadm has read them
+    (void)TB;
+    // the ticks copy may be overwritten only once the previous k_vadm has read it
     HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm, 0));
-    HIP_TRY(hipMemcpyAsync(e->d_vflag, e->d_wflag, TB * 4, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(e->d_vwratio, e->d_wratio, TB * 4, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(e->d_vwvad, e->d_wvad, TB * 4, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(e->d_vband, e->d_band, TB * c.n_channels * c.n_bands * 4, hipMemcpyDeviceToDevice,
-                           e->stream));
     if (use_ticks)
       HIP_TRY(hipMemcpyAsync(e->d_vticks, e->d_ticks, (size_t)c.n_streams * 4, hipMemcpyDeviceToDevice, e->stream));
     HIP_TRY(hipEventRecord(e->ev_copy, e->stream));
     HIP_TRY(hipStreamWaitEvent(e->side, e->ev_copy, 0));
     fvad::StagedArgs v = a;
-    v.out_win_flag = e->d_vflag;
-    v.out_win_ratio = e->d_vwratio;
-    v.out_win_vad = e->d_vwvad;
-    v.out_band = e->d_vband;
     v.ticks_valid = use_ticks ? e->d_vticks : nullptr;
     // k_vadm timing never blocks the host (it would serialise the overlap):
     // two event pairs alternate and are read once complete
@@ -572,6 +581,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
       e->vadm_pending[slot] = true;
     }
     HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
+    HIP_TRY(hipEventRecord(e->ev_vadm_b[b], e->side));
   }
   // every reader of buffer b (incl. the copy of ticks for k_vadm) is queued
   HIP_TRY(hipEventRecord(e->ev_buf_free[b], e->stream));
@@ -872,9 +882,18 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
       hipEventCreateWithFlags(&e->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_vadm, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&e->ev_vt[0][0]) != hipSuccess || hipEventCreate(&e->ev_vt[0][1]) != hipSuccess ||
-      hipEventCreate(&e->ev_vt[1][0]) != hipSuccess || hipEventCreate(&e->ev_vt[1][1]) != hipSuccess)
+      hipEventCreate(&e->ev_vt[1][0]) != hipSuccess || hipEventCreate(&e->ev_vt[1][1]) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_vadm_b[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_vadm_b[1], hipEventDisableTiming) != hipSuccess)
     return fail(FVAD_EDEVICE, "side stream / event creation failed");
   HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
+  HIP_TRY(hipEventRecord(e->ev_vadm_b[0], e->side));
+  HIP_TRY(hipEventRecord(e->ev_vadm_b[1], e->side));
+  // the second window-output set (push parity 1); set 0 is the engine's own
+  e->wflag_b[1] = e->d_vflag;
+  e->wratio_b[1] = e->d_vwratio;
+  e->wvad_b[1] = e->d_vwvad;
+  e->band_b[1] = e->d_vband;
   const char *ov = getenv("FVAD_VADM_LDS");  // tuning: run the LDS variant in-line instead
   e->vadm_overlap = !(ov && atoi(ov) == 1);
   return vadm_reset(e);
