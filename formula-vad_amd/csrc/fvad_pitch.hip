@@ -17,7 +17,7 @@ namespace fvad {
 // ---------------------------------------------------------------------------
 // k_pcorr: one 256-thread workgroup per half quarter tile (8 streams at one
 // frame position; 38.5 KB of LDS, so 4 workgroups share a CU, 4 waves per
-// SIMD at <= 128 VGPRs).
+// SIMD at 97 VGPRs, which leaves room beside them for k_prep3).
 //   Q0 xf (rows 0..863) and the coarse Syy sequence -> LDS
 //   Q1 coarse xcorr: lane = (frame, 5 consecutive lags), a register window of
 //      5 y values slides one sample per step (2 LDS reads per 5 MACs)
@@ -139,8 +139,10 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
       const int fr = tid;
       int bst[2] = {0, 1};
       float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
-      // operands of the next 8 lags load while these 8 are visited
-      constexpr int B = 8;
+      // operands of the next 4 lags load while these 4 are visited (8 ahead:
+      // 112 VGPRs, and 4 x 112 + k_prep3's 96 no longer fit one SIMD's 512,
+      // so the CUs that host k_prep3 lose a workgroup: 1.45 vs 1.39 ms)
+      constexpr int B = 4;
       float xb[B], yb[B];
 #pragma unroll
       for (int u = 0; u < B; u++) {
