@@ -76,35 +76,26 @@ __host__ __device__ constexpr int prep_streams(int C) { return kPrepSlots / C < 
 constexpr int kPrepRing = FVAD_PREP_RING;  // float4 loads in flight per lane
 static_assert((kFrame / 4) % kPrepRing == 0, "prep ring must divide a frame");
 
-// One lane's input sequence of float4 chunks: per tick the C * 480 samples of
-// stream s (contiguous), ticks B * C * 480 floats apart.
-struct PrepSrc {
-  const float *p;  // next chunk to load
-  int r, per_tick;  // chunk index within the tick, chunks per tick
-  size_t tick_jump;  // floats from a tick's end to the next tick's start
-  __device__ __forceinline__ float4 next() {
-    const float4 v = *reinterpret_cast<const float4 *>(p);
-    p += 4;
-    if (++r == per_tick) {
-      r = 0;
-      p += tick_jump;
-    }
-    return v;
-  }
-};
-
+// One lane walks its stream's input in blocks of kPrepRing float4 chunks: per
+// tick the C * 480 samples of stream s are contiguous, ticks B * C * 480
+// floats apart, and a tick holds a whole number of blocks, so a block is one
+// base pointer and kPrepRing immediate offsets.  The next block's chunks load
+// while this block's are filtered (the last block reloads itself).
 template <bool Scaled>
 __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, float &mem0, float &mem1) {
   constexpr int kChunksCh = kFrame / 4;  // float4 chunks of one channel's frame
   static_assert(kChunksCh % kPrepRing == 0, "ring blocks end at channel boundaries");
   const int C = a.n_channels;
-  const int per_tick = C * (kFrame / 4);
-  PrepSrc src{a.pcm + (size_t)s * C * kFrame, 0, per_tick, (size_t)(a.n_streams - 1) * C * kFrame};
+  const int per_tick = C * kChunksCh;
+  const int bpt = per_tick / kPrepRing;  // blocks per tick
+  const int nb = nt * bpt;
+  const size_t tick_stride = (size_t)a.n_streams * C * kFrame;
+  const float4 *tick_row = reinterpret_cast<const float4 *>(a.pcm + (size_t)s * C * kFrame);
   float4 *dst = reinterpret_cast<float4 *>(a.xs + (size_t)s * a.L + kHist);
-  const int nch = nt * per_tick;  // a multiple of kPrepRing
   float4 ring[kPrepRing];
 #pragma unroll
-  for (int u = 0; u < kPrepRing; u++) ring[u] = u < nch ? src.next() : make_float4(0, 0, 0, 0);
+  for (int u = 0; u < kPrepRing; u++) ring[u] = tick_row[u];
+  int rn = 1;  // block within the tick of the next block
   const float b0 = -2.0f, b1 = 1.0f, a0 = -1.99599f, a1 = 0.99600f;
   const float scalar = (float)32767;
   // b*x and a*y are exact in double (24-bit x 24-bit significands), so one
@@ -122,17 +113,23 @@ __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, f
   // over the stream's channels in channel order
   float sum = 0, vmin = 1, vmax = 0;
   int jt = 0, t = 0;  // chunk within the tick, tick
-  for (int j0 = 0; j0 < nch; j0 += kPrepRing) {
+  for (int b = 0; b < nb; b++) {
+    if (rn == bpt && b + 1 < nb) {
+      rn = 0;
+      tick_row = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(tick_row) + tick_stride);
+    }
+    const float4 *q = tick_row + (b + 1 < nb ? rn : rn - 1) * kPrepRing;
+    rn++;
 #pragma unroll
     for (int u = 0; u < kPrepRing; u++) {
       const float4 x = ring[u];
-      if (j0 + u + kPrepRing < nch) ring[u] = src.next();
+      ring[u] = q[u];
       float4 y;
       y.x = step(x.x);
       y.y = step(x.y);
       y.z = step(x.z);
       y.w = step(x.w);
-      dst[j0 + u] = y;
+      dst[b * kPrepRing + u] = y;
       sum += x.x * x.x;
       sum += x.y * x.y;
       sum += x.z * x.z;
