@@ -561,9 +561,10 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
     const size_t TB = (size_t)n_ticks * c.n_streams;
     (void)TB;
     // the ticks copy may be overwritten only once the previous k_vadm has read it
-    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm, 0));
-    if (use_ticks)
+    if (use_ticks) {
+      HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm, 0));
       HIP_TRY(hipMemcpyAsync(e->d_vticks, e->d_ticks, (size_t)c.n_streams * 4, hipMemcpyDeviceToDevice, e->stream));
+    }
     HIP_TRY(hipEventRecord(e->ev_copy, e->stream));
     HIP_TRY(hipStreamWaitEvent(e->side, e->ev_copy, 0));
     fvad::StagedArgs v = a;
