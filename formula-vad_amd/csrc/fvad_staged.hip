@@ -2530,15 +2530,20 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   // fork: k_fftA (aux) || pitch branch (main); both only read xs and write
   // disjoint buffers (X, Ex, Lyf, silence | ptile, rec, pitch, pitch state)
   const long long fgroups = (frames + FF - 1) / FF;
-  (void)hipEventRecord(st.fork, stream);
-  (void)hipStreamWaitEvent(st.aux, st.fork, 0);
+  // without the fork (the default, aux == main) no fork / join events: a wait
+  // on the stream's own event still costs a barrier packet between kernels
+  const bool forked = st.aux != stream;
+  if (forked) {
+    (void)hipEventRecord(st.fork, stream);
+    (void)hipStreamWaitEvent(st.aux, st.fork, 0);
+  }
   rec_aux(2);
   if (wfft)
     (void)launch_wave(kWaveFftA, a, n_cu, st.aux);
   else
     hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, st.aux, a);
   rec_aux(3);
-  (void)hipEventRecord(st.join, st.aux);
+  if (forked) (void)hipEventRecord(st.join, st.aux);
   {
     const long long tiles = (long long)((a.n_streams + 63) / 64) * a.n_ticks * a.n_channels;
     rec(14);
@@ -2549,7 +2554,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   rec(5);
   hipLaunchKernelGGL(k_select, dim3((a.n_streams + kSelStreams - 1) / kSelStreams), dim3(64), 0, stream, a);
   rec(6);
-  (void)hipStreamWaitEvent(stream, st.join, 0);  // join
+  if (forked) (void)hipStreamWaitEvent(stream, st.join, 0);  // join
   rec(7);
   if (wfft)
     (void)launch_wave(kWavePspec, a, n_cu, stream);
