@@ -1765,7 +1765,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   // noise z|r waves 6, 7, 10 (192), vad z|r waves 11, 15 (96), gain smoothing
   // + vad_output store wave 8, spectral variability of frame t wave 9.
   // (The constants name each role's first thread, for the stamps build.)
-  constexpr int kP1Den = 0, kP1Noise = 384, kP1Vad = 704, kP1Var = 576, kP1Gain = 512;
+  [[maybe_unused]] constexpr int kP1Den = 0, kP1Noise = 384, kP1Vad = 704, kP1Var = 576, kP1Gain = 512;
   // P2 wave plan, balanced over the residue classes the same way (a wave
   // holding lanes of two roles set the phase at 19.6 k cycles before): denoise
   // h waves 0..2 (192 tasks), noise h waves 3, 7 (96), denoise_output wave 4
@@ -1773,7 +1773,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   // (2 lanes), features of frame t+1 waves 9..13 (296 items).  (Denoise h with
   // 2 streams per lane on 6 waves shortened its chain to 11.1 k cycles but the
   // extra waves stretched the other roles: 15.3 vs 14.6 k per phase.)
-  constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 384, kP2Out = 256, kP2VadOut = 512,
+  [[maybe_unused]] constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 384, kP2Out = 256, kP2VadOut = 512,
                 kP2Feat = 576;
   constexpr int kFeatItems = S * (kBands + 7 + kCeps);
   static_assert(kP2Feat + kFeatItems <= 14 * 64 && 96 * kR3G == 192 && 48 * kR3G <= 128 && 22 * kR3G <= 64 &&
@@ -2513,9 +2513,6 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
     const char *v = getenv("FVAD_WFFT");
     return !(v && atoi(v) == 0);
   }();
-  // lane-per-stream kernels: 16 streams per workgroup spreads the serial
-  // chains over more CUs (each chain is latency-bound, not lane-bound)
-  const int lane_blocks = (a.n_streams + 15) / 16;
   const long long frames = (long long)a.n_streams * a.V;
   auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
   (void)hipGetLastError();
