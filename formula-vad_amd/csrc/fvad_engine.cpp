@@ -70,10 +70,10 @@ struct fvad_engine {
   int8_t *d_rnn_img = nullptr;
   // device VADMachines (fvad_engine_attach_vadm)
   fvad::VadmArgs vadm{};
-  // k_vadm runs on a side stream over copies of one push's window outputs,
+  // k_vadm_hbm runs on a side stream over copies of one push's window outputs,
   // overlapped with the next push (it only depends on its own state)
   hipStream_t side = nullptr;
-  hipStream_t aux = nullptr;  // staged mode: k_fftA concurrent with the pitch branch (FVAD_FORK)
+  hipStream_t aux = nullptr;  // staged mode: k_fftAw concurrent with the pitch branch (FVAD_FORK)
   // staged mode: k_prep3 runs on pstream, so push k's prep overlaps push k-1's
   // kernels; xs / ratio / ticks are double-buffered (d_xs, d_ratio, d_ticks
   // alias the buffer of the latest push), buffer b is reused once the push that
@@ -89,13 +89,12 @@ struct fvad_engine {
   int last_event = 0;         // the one recorded last (the launch's end)
   hipEvent_t ev_copy = nullptr, ev_vadm = nullptr, ev_vt[2][2] = {};  // [slot][begin/end] timing pairs
   // window outputs of push k in set k & 1 (the second set exists with VADMachines):
-  // k_vadm of push k reads them in place, push k + 2 rewrites them after it
+  // k_vadm_hbm of push k reads them in place, push k + 2 rewrites them after it
   int *wflag_b[2] = {};
   float *wratio_b[2] = {}, *wvad_b[2] = {}, *band_b[2] = {};
   hipEvent_t ev_vadm_b[2] = {};
   int32_t *d_vflag = nullptr, *d_vticks = nullptr;
   float *d_vwratio = nullptr, *d_vwvad = nullptr, *d_vband = nullptr;
-  bool vadm_overlap = true;
   double vadm_ms_sum = 0;
   int vadm_timed = 0;
   bool vadm_pending[2] = {false, false};
@@ -161,7 +160,7 @@ int dalloc(T **p, size_t count) {
   return FVAD_OK;
 }
 
-// int8 GRU-stack image for k_rnn (layout: fvad_internal.h rnnimg).  Term j of
+// int8 GRU-stack image for k_rnn3 (layout: fvad_internal.h rnnimg).  Term j of
 // a column's C-order sum lives in segment g at seg_off(g) + (j - start of g).
 void build_rnn_image(const fvad::HostModel &hm, std::vector<int8_t> &img, int *act) {
   namespace R = fvad::rnnimg;
@@ -542,7 +541,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.raw_s16 = e->raw_s16;
   a.vadm = e->vadm;
   a.stamps = e->d_stamps;
-  // FVAD_FORK=1 runs k_fftA on the aux stream beside the pitch branch.  Off by
+  // FVAD_FORK=1 runs k_fftAw on the aux stream beside the pitch branch.  Off by
   // default: both are persistent grids sized to the whole GPU, and sharing it
   // stretches the later one (measured 15.0 vs 14.1 ms per push).
   static const bool fork = [] {
@@ -553,14 +552,14 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   HIP_TRY(fvad::launch_prep(a, e->pstream, timed ? e->ev : nullptr));
   HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
   HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
-  // window output set b is free once push k-2's k_vadm has read it
+  // window output set b is free once push k-2's k_vadm_hbm has read it
   if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
   HIP_TRY(fvad::launch_staged(a, e->grid_frames, st, timed ? e->ev : nullptr));
   if (e->vadm.n > 0) {
     const fvad_engine_config &c = e->cfg;
     const size_t TB = (size_t)n_ticks * c.n_streams;
     (void)TB;
-    // the ticks copy may be overwritten only once the previous k_vadm has read it
+    // the ticks copy may be overwritten only once the previous k_vadm_hbm has read it
     if (use_ticks) {
       HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm, 0));
       HIP_TRY(hipMemcpyAsync(e->d_vticks, e->d_ticks, (size_t)c.n_streams * 4, hipMemcpyDeviceToDevice, e->stream));
@@ -569,14 +568,14 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
     HIP_TRY(hipStreamWaitEvent(e->side, e->ev_copy, 0));
     fvad::StagedArgs v = a;
     v.ticks_valid = use_ticks ? e->d_vticks : nullptr;
-    // k_vadm timing never blocks the host (it would serialise the overlap):
+    // k_vadm_hbm timing never blocks the host (it would serialise the overlap):
     // two event pairs alternate and are read once complete
     const int slot = e->vadm_slot ^= 1;
     if (timed) {
       e->vadm_pending[slot] = false;  // an unread older sample in this slot is dropped
       HIP_TRY(hipEventRecord(e->ev_vt[slot][0], e->side));
     }
-    HIP_TRY(fvad::launch_vadm(v, e->vadm_overlap, e->side));
+    HIP_TRY(fvad::launch_vadm(v, e->side));
     if (timed) {
       HIP_TRY(hipEventRecord(e->ev_vt[slot][1], e->side));
       e->vadm_pending[slot] = true;
@@ -584,7 +583,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
     HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
     HIP_TRY(hipEventRecord(e->ev_vadm_b[b], e->side));
   }
-  // every reader of buffer b (incl. the copy of ticks for k_vadm) is queued
+  // every reader of buffer b (incl. the copy of ticks for k_vadm_hbm) is queued
   HIP_TRY(hipEventRecord(e->ev_buf_free[b], e->stream));
   e->buf_busy[b] = true;
   e->next_buf = b ^ 1;
@@ -623,7 +622,7 @@ int collect_timing(fvad_engine *e) {
   return rc;
 }
 
-// k_vadm samples whose end event has completed (non-blocking)
+// k_vadm_hbm samples whose end event has completed (non-blocking)
 int collect_vadm_timing(fvad_engine *e) {
   for (int k = 0; k < 2; k++) {
     if (!e->vadm_pending[k] || hipEventQuery(e->ev_vt[k][1]) != hipSuccess) continue;
@@ -758,7 +757,7 @@ extern "C" int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_r
   if (rc) return rc;
   for (int i = 0; i < FVAD_MAX_TIMES; i++)
     ms_avg[i] = (e->n_timed && i <= e->n_kernels) ? e->ms_sum[i] / e->n_timed : 0.0;
-  // k_vadm (side stream, overlapped with the next push): reported after the
+  // k_vadm_hbm (side stream, overlapped with the next push): reported after the
   // pipeline kernels, not part of [0]
   if (e->vadm.n > 0 && e->n_kernels + 1 < FVAD_MAX_TIMES)
     ms_avg[e->n_kernels + 1] = e->vadm_timed ? e->vadm_ms_sum / e->vadm_timed : 0.0;
@@ -785,7 +784,7 @@ extern "C" int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out)
 }
 
 extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
-  if (e && i == e->n_kernels && e->vadm.n > 0) return e->vadm_overlap ? "k_vadm_hbm" : "k_vadm";
+  if (e && i == e->n_kernels && e->vadm.n > 0) return "k_vadm_hbm";
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
   if (e->cfg.mode == FVAD_MODE_FUSED) return i == 0 ? "k_prep" : "k_frame";
   return fvad::staged_kernel_name(i);
@@ -895,8 +894,6 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
   e->wratio_b[1] = e->d_vwratio;
   e->wvad_b[1] = e->d_vwvad;
   e->band_b[1] = e->d_vband;
-  const char *ov = getenv("FVAD_VADM_LDS");  // tuning: run the LDS variant in-line instead
-  e->vadm_overlap = !(ov && atoi(ov) == 1);
   return vadm_reset(e);
 }
 

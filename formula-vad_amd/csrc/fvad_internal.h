@@ -50,7 +50,7 @@ constexpr int kWords = ((kCepsDist + kCeps * kCeps + 63) / 64) * 64;
 }  // namespace st
 
 // ---------------------------------------------------------------------------
-// int8 image of the GRU stack for the staged recurrence kernel (k_rnn keeps it
+// int8 image of the GRU stack for the staged recurrence kernel (k_rnn3 keeps it
 // in LDS).  Nine column-major matrices; column c of matrix m holds the K
 // weights of one output neuron in summation order (input part, then the
 // recurrent part for GRU gates), so one lane walks one column.

@@ -96,12 +96,13 @@ struct StagedArgs {
   int raw_s16;
   VadmArgs vadm;
   unsigned *work;          // [kWorkCounters] dynamic group counters of the persistent kernels
-  unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn
+  unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn3
 };
 
-// Streams of one launch: k_fftA runs on `aux` concurrently with the pitch
-// branch (k_plpc -> k_pcorr -> k_select) on `main`; `fork` / `join` order
-// them (k_prep2 before both, k_pspec after both).
+// Streams of one launch: k_fftAw runs on `aux` concurrently with the pitch
+// branch (k_plpc -> k_pcorr -> k_select) on `main` (FVAD_FORK=1; by default
+// aux == main); `fork` / `join` order them (k_prep3 before both, k_pspecw
+// after both).
 struct StagedStreams {
   hipStream_t main, aux;
   hipEvent_t fork, join;
@@ -126,6 +127,6 @@ enum WaveKernel { kWaveFftA, kWavePspec, kWaveSynth, kWaveFftB };
 hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream);
 // Device VADMachines over the window outputs a.out_* of one push: overlap =
 // the light HBM variant meant to co-run with the next push on a side stream.
-hipError_t launch_vadm(const StagedArgs &a, bool overlap, hipStream_t stream);
+hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream);
 
 }  // namespace fvad

@@ -6,27 +6,31 @@
 //   k_prep3   lane/stream   HP biquad (serial IIR), s16 scaling, RMS volume
 //                           ratio; x written stream-contiguous with 1248 samples
 //                           of pitch history in front of the launch's frames
-//   k_fftA    wg/frame      analysis window + FFT A, band energies Ex, the
+//   k_fftAw   wave/frame    analysis window + FFT A, band energies Ex, the
 //                           log/floor chain (Ly, E, silence gate), DCT(Ly)
+//                           (fvad_wave.hip)
 //   k_plpc    lane/frame    pitch_downsample (x_lp, autocorr, LPC, FIR5) and
 //                           every serial energy recurrence (Syy, xx, yy)
-//   k_pcorr   wg/16 frames  coarse and fine xcorr + find_best_pitch, every
+//   k_pcorr   wg/8 frames   coarse and fine xcorr + find_best_pitch, every
 //                           remove_doubling inner product for every candidate
-//                           period (the final 3-lag xcorr speculatively for all 15)
-//   k_select  lane/stream   remove_doubling's sequential candidate selection
-//                           (needs last_period / last_gain) -> pitch index
-//   k_pspec   wg/frame      pitch window + FFT A -> P, Ep, Exp, DCT(Exp)
-//   k_rnn     wg/stream     the true recurrence: cepstral memory, spectral
-//                           variability, GRU stack, pitch filter, gain smoothing
-//   k_synth   wg/frame      Hermitian extension + FFT A + synthesis window
+//                           period (fvad_pitch.hip)
+//   k_select  lane/(stream, candidate)  remove_doubling's sequential candidate
+//                           selection (needs last_period / last_gain) -> pitch
+//   k_pspecw  wave/frame    pitch window + FFT A -> P, Ep, Exp, DCT(Exp)
+//   k_rnn3    wg/8 streams  the true recurrence: cepstral memory, spectral
+//                           variability, GRU stack, gain smoothing
+//   k_synthw  wave/frame    pitch filter, gains, Hermitian extension + FFT A +
+//                           synthesis window
 //   k_ola     per sample    overlap-add, 1/32767, re-block ring, per-tick vad
 //   k_winmeta lane/stream   window completion, share-weighted ratio, state
-//   k_fftb    wg/window     FFT B (kissfft radix-4), magnitudes, band sums
+//   k_fftbw   wave/window   FFT B (kissfft radix-4), magnitudes, band sums
+//                           (k_fftb, workgroup per window, for fft_size 512)
+//   k_vadm_hbm lane/stream  VADMachine.run per completed window (side stream)
 //
-// Each wg/frame kernel is persistent (grid-stride over frames) so per-thread
-// table values stay in registers across frames.  All arithmetic reproduces the
-// oracle's operation order (see fvad_kernels.hip), so results are
-// bit-identical to the fused kernel and the CPU oracle.
+// The wave kernels are persistent (batches of frames from per-XCD queues) so
+// per-lane table values stay in registers across frames.  All arithmetic
+// reproduces the oracle's operation order (see fvad_kernels.hip), so results
+// are bit-identical to the fused kernel and the CPU oracle.
 #pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
 
@@ -40,7 +44,6 @@
 #include "fvad_staged_dev.h"
 
 namespace fvad {
-
 
 namespace {
 // LDS row pitch of the 960-point transforms (float2): frames 16 banks apart,
@@ -190,179 +193,6 @@ __global__ void __launch_bounds__(64) k_prep3(StagedArgs a) {
       a.state[(size_t)(sb + s) * st::kWords + st::kPitch + i] =
           a.xs[(size_t)(sb + s) * a.L + (size_t)(nt * C - 1) * kFrame + i];
   }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent 256-thread frame kernels (k_fftA, k_pspec, k_synth) work on F
-// frames per workgroup iteration: each phase covers all F frames, so the
-// per-band serial sums (band energies, the Ly chain, DCTs) of F frames share
-// wave instructions and every barrier is amortised over F frames.  Per-thread
-// setup, loaded once: the element indices a thread owns in the 960-point
-// windowed scatter (i = tid + 256 r), their digit-reversed destinations and
-// window values, and the FFT twiddles.
-// ---------------------------------------------------------------------------
-constexpr int kFftFrames = 4;
-
-struct FrameCtx {
-  Fft960Tw tw;
-  int dst[4];      // scatter form: W[dst[r]] <- element tid + 256 r
-  float win[4];    //   and its window value
-  int src[4];      // gather form: W[tid + 256 r] <- element src[r]
-  float wsrc[4];   //   and its window value
-};
-__device__ __forceinline__ void frame_ctx_load(FrameCtx &c, const Plan *__restrict__ P, int tid) {
-  fft960_load(c.tw, reinterpret_cast<const float2 *>(P->tw960), tid);
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int i = tid + 256 * r;
-    c.dst[r] = i < kWin ? P->bitrev960[i] : 0;
-    c.win[r] = i < kWin ? win960(P->half_window, i) : 0.0f;
-    c.src[r] = i < kWin ? P->ibitrev960[i] : 0;
-    c.wsrc[r] = i < kWin ? win960(P->half_window, c.src[r]) : 0.0f;
-  }
-}
-
-// frame indices of group g (-1: past the end or beyond the stream's valid ticks)
-template <int F>
-__device__ __forceinline__ void group_frames(const StagedArgs &a, long long g, int tid, int *fidx) {
-  if (tid < F) {
-    const long long f = g * F + tid;
-    int ok = -1;
-    if (f < (long long)a.n_streams * a.V) {
-      const int s = (int)(f / a.V), v = (int)(f - (long long)s * a.V);
-      if (v < ticks_of(a, s) * a.n_channels) ok = (int)f;
-    }
-    fidx[tid] = ok;
-  }
-}
-// This thread's 4 samples of the 960-sample analysis window of every frame of
-// group g (issued one group ahead so the HBM latency hides behind the work)
-// (gathered in digit-reversed order: sample src[r] lands in W[tid + 256 r])
-template <int F>
-__device__ __forceinline__ void load_window(const StagedArgs &a, long long g, int tid, const FrameCtx &cx,
-                                            float (&buf)[F][4]) {
-#pragma unroll
-  for (int fr = 0; fr < F; fr++) {
-    const int f = frame_of(a, g, F, fr);
-    const float *pb = f >= 0 ? frame_pb(a, f) + (kPitchBuf - kWin) : nullptr;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int i = tid + 256 * r;
-      buf[fr][r] = (pb && i < kWin) ? pb[cx.src[r]] : 0.0f;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_fftA: X, Ex, Ly chain, silence, DCT(Ly)
-// ---------------------------------------------------------------------------
-template <int F>
-__global__ void __launch_bounds__(256) k_fftA(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[F][kWinP];
-  __shared__ BandTab T;
-  __shared__ float Ly[F][kBands + 2], Exl[F][kBands + 2];
-  __shared__ int sil[F], fidx[F];
-  const int tid = threadIdx.x;
-  FrameCtx cx;
-  frame_ctx_load(cx, a.plan, tid);
-  bandtab_load(T, a.plan, tid, 256);
-  const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
-  STAMP_INIT();
-  __shared__ long long gq;
-  if (tid == 0) gq = take_group(a, kWorkFftA);
-  __syncthreads();
-  long long g = gq;
-  __syncthreads();
-  if (tid == 0) gq = take_group(a, kWorkFftA);
-  float win_cur[F][4];
-  if (g < ngroups) load_window<F>(a, g, tid, cx, win_cur);
-  __syncthreads();
-  long long gn = gq;  // the group after g (its window is prefetched)
-  while (g < ngroups) {
-    group_frames<F>(a, g, tid, fidx);
-    float win_nxt[F][4];
-    if (gn < ngroups) load_window<F>(a, gn, tid, cx, win_nxt);
-    __syncthreads();
-    RSTAMP(0);
-#pragma unroll
-    for (int fr = 0; fr < F; fr++) {
-      if (fidx[fr] < 0) continue;
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int i = tid + 256 * r;
-        if (i < kWin) {
-          float val = win_cur[fr][r];
-          val *= cx.wsrc[r];
-          W[fr][i] = make_float2(kScale960 * val, kScale960 * 0.0f);
-        }
-      }
-    }
-#pragma unroll
-    for (int fr = 0; fr < F; fr++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) win_cur[fr][r] = win_nxt[fr][r];
-    __syncthreads();
-    RSTAMP(1);
-    fft960_run<F, kWinP>(cx.tw, W, tid);
-    RSTAMP(2);
-    // X out; band-energy terms into the dead upper half of each row
-    for (int idx = tid; idx < F * kFreq; idx += 256) {
-      const int fr = idx / kFreq, k = idx - fr * kFreq;
-      const float2 x = W[fr][k];
-      if (fidx[fr] >= 0) a.X[(size_t)fidx[fr] * kFreq + k] = x;
-      if (k < 400) {
-        float *tr = reinterpret_cast<float *>(W[fr]) + kTermOff;
-        band_terms(x, x, T, k, tr[k], tr[400 + k]);
-      }
-    }
-    __syncthreads();
-    if (tid < F * kBands) {
-      const int fr = tid / kBands, b = tid - fr * kBands;
-      const float *tr = reinterpret_cast<const float *>(W[fr]) + kTermOff;
-      const float ex = band_chain(tr, tr + 400, T, b);
-      Exl[fr][b] = ex;
-      if (fidx[fr] >= 0) a.Ex[(size_t)fidx[fr] * kBands + b] = ex;
-      Ly[fr][b] = (float)log10(1e-2 + (double)ex);
-    }
-    __syncthreads();
-    RSTAMP(3);
-    if (tid < F) {
-      const int fr = tid;
-      float logMax = -2, follow = -2, E = 0;
-      for (int i = 0; i < kBands; i++) {
-        const float ly0 = Ly[fr][i];
-        const double bb = (follow - 1.5 > (double)ly0) ? follow - 1.5 : (double)ly0;
-        const double aa = ((double)(logMax - 7) > bb) ? (double)(logMax - 7) : bb;
-        const float ly = (float)aa;
-        Ly[fr][i] = ly;
-        logMax = (logMax > ly) ? logMax : ly;
-        follow = (float)((follow - 1.5 > (double)ly) ? follow - 1.5 : (double)ly);
-        E += Exl[fr][i];
-      }
-      sil[fr] = ((double)E < 0.04) ? 1 : 0;
-      if (fidx[fr] >= 0) a.silence[fidx[fr]] = sil[fr];
-    }
-    __syncthreads();
-    RSTAMP(4);
-    if (tid < F * kBands) {
-      const int fr = tid / kBands, b = tid - fr * kBands;
-      if (fidx[fr] >= 0 && !sil[fr]) {
-        float sum = 0;
-#pragma unroll
-        for (int j = 0; j < kBands; j++) sum += Ly[fr][j] * T.dct[j * kBands + b];
-        float val = (float)(sum * sqrt(2. / 22));
-        if (b == 0) val -= 12;
-        if (b == 1) val -= 4;
-        a.Lyf[(size_t)fidx[fr] * kBands + b] = val;
-      }
-    }
-    if (tid == 0 && gn < ngroups) gq = take_group(a, kWorkFftA);
-    __syncthreads();
-    RSTAMP(5);
-    g = gn;
-    gn = (g < ngroups) ? gq : ngroups;
-  }
-  STAMP_FLUSH(16, 6);
 }
 
 // ---------------------------------------------------------------------------
@@ -818,148 +648,15 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_pspec: pitch spectrum P, Ep, normalised Exp, DCT(Exp)[0..5], feature 40
+// GRU helpers of k_rnn3.  The whole GRU stack is resident in LDS as an int8
+// image (rnnimg, 88 KB; int8 -> f32 is exact), so weights never come from L2
+// per frame.  A matrix column = one neuron's C-order sum: lane (column, stream
+// group) accumulates SL streams of that column with one weight fetch per term;
+// per-stream vectors are stored [j][S] so the SL inputs of a term are one LDS
+// read.  GRU inputs are read in place from their segments (no concatenation
+// copies) and GRU states live in rings indexed by frame (no copy-back phase).
 // ---------------------------------------------------------------------------
-template <int F>
-__global__ void __launch_bounds__(256, 3) k_pspec(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[F][kWinP];
-  __shared__ __attribute__((aligned(16))) float2 Xl[F][kFreq + 1];
-  __shared__ BandTab T;
-  __shared__ float Ep[F][kBands + 2], Exp[F][kBands + 2];
-  __shared__ int fidx[F], pit[F];
-  const int tid = threadIdx.x;
-  FrameCtx cx;
-  frame_ctx_load(cx, a.plan, tid);
-  bandtab_load(T, a.plan, tid, 256);
-  const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
-  __shared__ long long gq;
-  if (threadIdx.x == 0) gq = take_group(a, kWorkPspec);
-  __syncthreads();
-  long long g = gq;
-  while (g < ngroups) {
-    group_frames<F>(a, g, tid, fidx);
-    __syncthreads();
-    if (tid < F) pit[tid] = fidx[tid] >= 0 ? a.pitch[fidx[tid]] : 0;
-    __syncthreads();
-#pragma unroll
-    for (int fr = 0; fr < F; fr++) {
-      const int f = fidx[fr];
-      if (f < 0) continue;
-      const float *pb = frame_pb(a, f) + (kPitchBuf - kWin - pit[fr]);
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int i = tid + 256 * r;
-        if (i < kWin) {
-          float val = pb[cx.src[r]];
-          val *= cx.wsrc[r];
-          W[fr][i] = make_float2(kScale960 * val, kScale960 * 0.0f);
-        }
-      }
-    }
-    for (int idx = tid; idx < F * kFreq; idx += 256) {
-      const int fr = idx / kFreq, k = idx - fr * kFreq;
-      if (fidx[fr] >= 0) Xl[fr][k] = a.X[(size_t)fidx[fr] * kFreq + k];
-    }
-    __syncthreads();
-    fft960_run<F, kWinP>(cx.tw, W, tid);
-    // P out; Ep (P.P) band terms into the dead upper half of each row, Exp
-    // (X.P) terms over the lower half once every P value has been read
-    {
-      constexpr int NI = (F * kFreq + 255) / 256;
-      float clo[NI], chi[NI];
-#pragma unroll
-      for (int u = 0; u < NI; u++) {
-        const int idx = tid + 256 * u;
-        if (idx < F * kFreq) {
-          const int fr = idx / kFreq, k = idx - fr * kFreq;
-          const float2 pv = W[fr][k];
-          if (fidx[fr] >= 0) a.P[(size_t)fidx[fr] * kFreq + k] = pv;
-          if (k < 400) {
-            float *tr = reinterpret_cast<float *>(W[fr]) + kTermOff;
-            band_terms(pv, pv, T, k, tr[k], tr[400 + k]);
-            band_terms(Xl[fr][k], pv, T, k, clo[u], chi[u]);
-          }
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < NI; u++) {
-        const int idx = tid + 256 * u;
-        if (idx < F * kFreq) {
-          const int fr = idx / kFreq, k = idx - fr * kFreq;
-          float *tr = reinterpret_cast<float *>(W[fr]);
-          if (k < 400) {
-            tr[k] = clo[u];
-            tr[400 + k] = chi[u];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (tid < 2 * F * kBands) {
-      const int h = tid / (F * kBands), r = tid - h * (F * kBands), fr = r / kBands, b = r - fr * kBands;
-      const float *tr = reinterpret_cast<const float *>(W[fr]) + (h == 0 ? kTermOff : 0);
-      const float v = band_chain(tr, tr + 400, T, b);
-      if (h == 0)
-        Ep[fr][b] = v;
-      else
-        Exp[fr][b] = v;
-    }
-    __syncthreads();
-    if (tid < F * kBands) {
-      const int fr = tid / kBands, b = tid - fr * kBands;
-      const int f = fidx[fr];
-      if (f >= 0) {
-        const float ex = a.Ex[(size_t)f * kBands + b];
-        const float e = (float)((double)Exp[fr][b] / sqrt(.001 + (double)(ex * Ep[fr][b])));
-        Exp[fr][b] = e;
-        a.Ep[(size_t)f * kBands + b] = Ep[fr][b];
-        a.Exp[(size_t)f * kBands + b] = e;
-      }
-    }
-    __syncthreads();
-    if (tid < F * 8) {
-      const int fr = tid >> 3, i = tid & 7;
-      const int f = fidx[fr];
-      if (f >= 0 && i < 6) {
-        float sum = 0;
-#pragma unroll
-        for (int j = 0; j < kBands; j++) sum += Exp[fr][j] * T.dct[j * kBands + i];
-        float val = (float)(sum * sqrt(2. / 22));
-        if (i == 0) val = (float)(val - 1.3);
-        if (i == 1) val = (float)(val - 0.9);
-        a.f34[(size_t)f * 8 + i] = val;
-      } else if (f >= 0 && i == 6) {
-        a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pit[fr] - 300));
-      }
-    }
-    if (tid == 0) gq = take_group(a, kWorkPspec);
-    __syncthreads();
-    g = gq;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_rnn: the recurrence.  One workgroup owns S streams and walks their frames
-// in lockstep (frame v of every stream, then v+1 ...).  The whole GRU stack is
-// resident in LDS as an int8 image (rnnimg, 88 KB; int8 -> f32 is exact), so
-// weights never come from L2 per frame.  A matrix column = one neuron's C-order
-// sum: lane (column, stream group) accumulates SL streams of that column with
-// one weight fetch per term; per-stream vectors are stored [j][S] so the SL
-// inputs of a term are one LDS read.  GRU inputs are read in place from their
-// segments (no concatenation copies), GRU states ping-pong between two
-// buffers (no copy-back phase), and the next frame's features are prefetched
-// into registers while the current frame runs.  Per frame and stream:
-// cepstral memory + deltas, spectral variability (distance matrix kept in the
-// state, only the new row recomputed), compute_rnn, and the gain recurrence
-// lastg; the pitch filter and gain application are in k_synth (nothing
-// recurrent is left in them once g and the smoothed gains are known).
-// ---------------------------------------------------------------------------
-constexpr int kRnnS = 8;   // streams per workgroup
-constexpr int kRnnG = 4;   // lanes per column (stream groups of S/G = 2)
-constexpr int kRnnNT = 1024;
 constexpr int kRnnPf = 30; // prefetched words per stream and frame: Lyf[22], f34[7], silence
-
 
 // acc[q] += w[j] * v[j][s0 + q] for the n terms of one segment, C order.  The
 // segment's weights start 8-byte aligned: 8 terms = one 64-bit LDS read plus
@@ -1103,512 +800,13 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
   }
 }
 
-template <int S, int G, int NT>
-__global__ void __launch_bounds__(NT) k_rnn(StagedArgs a) {
-  // One LDS block with a fixed member order: the activation vectors come
-  // first (all below 64 KB, so every read of them uses an immediate offset),
-  // the 90 KB GRU image last.
-  struct Lds {
-    alignas(16) float featT[44 * S];
-    alignas(16) float doutT[24 * S];
-    alignas(16) float gvT[2][24 * S];
-    alignas(16) float gnT[2][48 * S];
-    alignas(16) float gdT[2][96 * S];
-    alignas(16) float zrT[192 * S];
-    float tt[204];
-    float ceps[S][kCeps * kBands];
-    float dist[S][kCeps * kCeps];
-    float lastg[S][kBands];
-    float pf[S][kRnnPf];  // features of the current frame (prefetched)
-    int memid[S], act[S], nfs[S];
-    long long fbase[S];
-    float vad_s[S];
-    alignas(16) int8_t W[rnnimg::kBytes];
-  };
-  __shared__ Lds L;
-  auto &featT = L.featT;
-  auto &doutT = L.doutT;
-  auto &gvT = L.gvT;
-  auto &gnT = L.gnT;
-  auto &gdT = L.gdT;
-  auto &zrT = L.zrT;
-  auto &tt = L.tt;
-  auto &ceps = L.ceps;
-  auto &dist = L.dist;
-  auto &lastg = L.lastg;
-  auto &pf = L.pf;
-  auto &memid = L.memid;
-  auto &act = L.act;
-  auto &nfs = L.nfs;
-  auto &fbase = L.fbase;
-  auto &vad_s = L.vad_s;
-  auto &W = L.W;
-  const int tid = threadIdx.x;
-  const int sb = blockIdx.x * S;
-  {
-    const int4 *src = reinterpret_cast<const int4 *>(a.rnn_img);
-    int4 *dst = reinterpret_cast<int4 *>(W);
-    for (int i = tid; i < rnnimg::kBytes / 16; i += NT) dst[i] = src[i];
-    for (int i = tid; i < 201; i += NT) tt[i] = a.plan->tansig[i];
-  }
-  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
-    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
-    ceps[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] : 0.0f;
-  }
-  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
-    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
-    dist[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] : 0.0f;
-  }
-  for (int idx = tid; idx < S * kBands; idx += NT) {
-    const int s = idx / kBands, i = idx - s * kBands;
-    lastg[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] : 0.0f;
-  }
-  for (int idx = tid; idx < S * 96; idx += NT) {
-    const int s = idx / 96, i = idx - s * 96;
-    const bool ok = sb + s < a.n_streams;
-    const float *stp = a.state + (size_t)(sb + s) * st::kWords;
-    if (i < 24) gvT[0][i * S + s] = ok ? stp[st::kVadGru + i] : 0.0f;
-    if (i < 48) gnT[0][i * S + s] = ok ? stp[st::kNoiseGru + i] : 0.0f;
-    gdT[0][i * S + s] = ok ? stp[st::kDenGru + i] : 0.0f;
-  }
-  if (tid < S) {
-    const int s = sb + tid;
-    const bool ok = s < a.n_streams;
-    memid[tid] = ok ? reinterpret_cast<const int *>(a.state)[(size_t)s * st::kWords + st::kMemId] : 0;
-    nfs[tid] = ok ? ticks_of(a, s) * a.n_channels : 0;
-    fbase[tid] = (long long)s * a.V;
-  }
-  __syncthreads();
-  int maxnf = 0;
-#pragma unroll
-  for (int s = 0; s < S; s++) maxnf = max(maxnf, nfs[s]);
-  // prefetch lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (as 1.0 / 0.0)
-  const int pfs = tid / kRnnPf, pfi = tid - pfs * kRnnPf;
-  const bool pf_lane = tid < S * kRnnPf;
-  auto fetch = [&](int v) -> float {
-    if (!pf_lane || v >= nfs[pfs]) return 1.0f;  // past the end: treated as silent (inactive)
-    const long long f = fbase[pfs] + v;
-    if (pfi < kBands) return a.Lyf[f * kBands + pfi];
-    if (pfi < kBands + 7) return a.f34[f * 8 + (pfi - kBands)];
-    return a.silence[f] ? 1.0f : 0.0f;
-  };
-  // frame 0's silence must be known before its Lyf (which k_fftA leaves unwritten for silent frames) is used
-  if (pf_lane) pf[pfs][pfi] = fetch(0);
-  __syncthreads();
-  if (tid < S) {
-    act[tid] = (0 < nfs[tid]) && pf[tid][kRnnPf - 1] == 0.0f;
-    if (0 < nfs[tid] && !act[tid]) a.vadf[fbase[tid]] = 0;
-  }
-  float pf_next = fetch(1);
-  const int *ra = a.rnn_act;
-  __syncthreads();
-  STAMP_INIT();
-  for (int v = 0; v < maxnf; v++) {
-    const int cur = v & 1, nxt = cur ^ 1;
-    // C: features 0..21 = DCT(Ly) (k_fftA) -> cepstral memory, deltas, the new
-    //    row of the distance matrix, features 34..40 (k_pspec)
-    for (int idx = tid; idx < S * (kBands + 7 + kCeps); idx += NT) {
-      const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
-      if (!act[s]) continue;
-      const int mi = memid[s];
-      const float *c0 = pf[s];  // ceps_0 (the row being written at memid)
-      if (i < kBands) {
-        ceps[s][mi * kBands + i] = c0[i];
-        if (i < 6) {
-          const float *c1 = ceps[s] + ((mi < 1) ? kCeps + mi - 1 : mi - 1) * kBands;
-          const float *c2 = ceps[s] + ((mi < 2) ? kCeps + mi - 2 : mi - 2) * kBands;
-          featT[i * S + s] = c0[i] + c1[i] + c2[i];
-          featT[(kBands + i) * S + s] = c0[i] - c2[i];
-          featT[(kBands + 6 + i) * S + s] = c0[i] - 2 * c1[i] + c2[i];
-        } else {
-          featT[i * S + s] = c0[i];
-        }
-      } else if (i < kBands + 7) {
-        featT[(34 + i - kBands) * S + s] = c0[i];
-      } else {
-        const int j = i - kBands - 7;
-        if (j != mi) {
-          const float *cj = ceps[s] + j * kBands;
-          float d = 0;
-#pragma unroll
-          for (int k = 0; k < kBands; k++) {
-            const float tmp = c0[k] - cj[k];
-            d += tmp * tmp;
-          }
-          dist[s][mi * kCeps + j] = d;
-          dist[s][j * kCeps + mi] = d;
-        }
-      }
-    }
-    __syncthreads();
-    RSTAMP(0);
-    // D: spectral variability
-    if (tid < S && act[tid]) {
-      const int s = tid;
-      float sv = 0;
-      for (int i = 0; i < kCeps; i++) {
-        float mindist = 1e15f;
-        for (int j = 0; j < kCeps; j++)
-          if (j != i) mindist = (mindist < dist[s][i * kCeps + j]) ? mindist : dist[s][i * kCeps + j];
-        sv += mindist;
-      }
-      featT[41 * S + s] = (float)(sv / kCeps - 2.1);
-      int mid = memid[s] + 1;
-      if (mid == kCeps) mid = 0;
-      memid[s] = mid;
-    }
-    __syncthreads();
-    RSTAMP(1);
-    // compute_rnn
-    rnn_gates<0, S, G, NT>(W, RnnIn{featT, nullptr, nullptr}, nullptr, doutT, ra[0], tt, tid);
-    __syncthreads();
-    RSTAMP(2);
-    rnn_gates<1, S, G, NT>(W, RnnIn{doutT, nullptr, nullptr}, gvT[cur], zrT, kActSigmoid, tt, tid);
-    __syncthreads();
-    RSTAMP(3);
-    rnn_cand<2, S, G, NT>(W, RnnIn{doutT, nullptr, nullptr}, gvT[cur], zrT, gvT[nxt], act, ra[2], tt,
-                          tid);
-    __syncthreads();
-    RSTAMP(4);
-    // noise_input = [dense_out, vad_state, features]; vad_output alongside
-    rnn_gates<3, S, G, NT>(W, RnnIn{doutT, gvT[nxt], featT}, gnT[cur], zrT, kActSigmoid, tt, tid);
-    if (tid >= NT - S) {
-      const int s = tid - (NT - S);
-      constexpr int ob = rnnimg::off_b(8), ow = rnnimg::off_w(8);
-      float sum = (float)W[ob];
-      for (int j = 0; j < 24; j++) sum += (float)W[ow + j] * gvT[nxt][j * S + s];
-      vad_s[s] = activate(tt, ra[8], kWs * sum);
-    }
-    __syncthreads();
-    RSTAMP(5);
-    rnn_cand<4, S, G, NT>(W, RnnIn{doutT, gvT[nxt], featT}, gnT[cur], zrT, gnT[nxt], act, ra[4],
-                          tt, tid);
-    __syncthreads();
-    RSTAMP(6);
-    // denoise_input = [vad_state, noise_state, features]
-    rnn_gates<5, S, G, NT>(W, RnnIn{gvT[nxt], gnT[nxt], featT}, gdT[cur], zrT, kActSigmoid, tt,
-                           tid);
-    __syncthreads();
-    RSTAMP(7);
-    rnn_cand<6, S, G, NT>(W, RnnIn{gvT[nxt], gnT[nxt], featT}, gdT[cur], zrT, gdT[nxt], act, ra[6],
-                          tt, tid);
-    __syncthreads();
-    RSTAMP(8);
-    rnn_gates<7, S, G, NT>(W, RnnIn{gdT[nxt], nullptr, nullptr}, nullptr, zrT, ra[7], tt, tid);
-    __syncthreads();
-    RSTAMP(9);
-    // gain smoothing g = max(g, .6*lastg) (denoise.c) and outputs of frame v;
-    // the prefetched features of frame v+1 land in LDS
-    for (int idx = tid; idx < S * kBands; idx += NT) {
-      const int s = idx / kBands, i = idx - s * kBands;
-      if (!act[s]) continue;
-      const long long f = fbase[s] + v;
-      const float gi = zrT[i * S + s];
-      const float al = .6f * lastg[s][i];
-      const float gsm = (gi > al) ? gi : al;
-      lastg[s][i] = gsm;
-      a.gr[f * kBands + i] = gi;
-      a.gs[f * kBands + i] = gsm;
-      if (i == 0) a.vadf[f] = vad_s[s];
-    }
-    if (pf_lane) pf[pfs][pfi] = pf_next;
-    pf_next = fetch(v + 2);
-    __syncthreads();
-    RSTAMP(10);
-    if (tid < S) {
-      const bool valid = v + 1 < nfs[tid];
-      act[tid] = valid && pf[tid][kRnnPf - 1] == 0.0f;
-      if (valid && !act[tid]) a.vadf[fbase[tid] + v + 1] = 0;  // silent: X passes through, state untouched
-    }
-    __syncthreads();
-    RSTAMP(11);
-  }
-  STAMP_FLUSH(0, 12);
-  const int fin = maxnf & 1;  // buffer holding the latest GRU states
-  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
-    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
-    if (sb + s < a.n_streams && nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] = ceps[s][i];
-  }
-  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
-    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
-    if (sb + s < a.n_streams && nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] = dist[s][i];
-  }
-  for (int idx = tid; idx < S * kBands; idx += NT) {
-    const int s = idx / kBands, i = idx - s * kBands;
-    if (sb + s < a.n_streams && nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] = lastg[s][i];
-  }
-  for (int idx = tid; idx < S * 96; idx += NT) {
-    const int s = idx / 96, i = idx - s * 96;
-    if (sb + s >= a.n_streams || nfs[s] <= 0) continue;
-    float *stp = a.state + (size_t)(sb + s) * st::kWords;
-    if (i < 24) stp[st::kVadGru + i] = gvT[fin][i * S + s];
-    if (i < 48) stp[st::kNoiseGru + i] = gnT[fin][i * S + s];
-    stp[st::kDenGru + i] = gdT[fin][i * S + s];
-  }
-  if (tid < S && sb + tid < a.n_streams && nfs[tid] > 0)
-    reinterpret_cast<int *>(a.state)[(size_t)(sb + tid) * st::kWords + st::kMemId] = memid[tid];
-}
-
 // ---------------------------------------------------------------------------
-// k_rnn2: k_rnn's recurrence as a three-stage software pipeline over frames.
-// compute_rnn's GRUs depend on each other only within a frame (vad -> noise ->
-// denoise) and on their own previous state, so step t runs the vad GRU of
-// frame t, the noise GRU of frame t-1 and the denoise GRU of frame t-2 side by
-// side, with the frame features of t+1 and the gain smoothing of t-3:
-//   P1  z|r gates of vad(t), noise(t-1), denoise(t-2); features of t+1
-//       (cepstral memory, deltas, distance row); gains of t-3
-//   P2  candidate gates of the three GRUs; spectral variability of t+1
-//   P3  denoise_output(t-2), dense(t+1), vad_output(t), next features -> LDS
-// Three barriers per step instead of twelve, and every phase has enough
-// independent chains to fill the CU.  Buffers are rings indexed by frame.
-// ---------------------------------------------------------------------------
-template <int S, int G, int NT>
-__global__ void __launch_bounds__(NT) k_rnn2(StagedArgs a) {
-  static_assert(NT == 1024 && S == 8 && G == 4, "k_rnn2 thread plan is for 8 streams x 4 groups x 1024 threads");
-  struct Lds {
-    alignas(16) float featT[4][44 * S];  // frame f in slot f & 3
-    alignas(16) float doutT[4][24 * S];
-    alignas(16) float gvT[4][24 * S];
-    alignas(16) float gnT[2][48 * S];
-    alignas(16) float gdT[2][96 * S];
-    alignas(16) float zrv[48 * S], zrn[96 * S], zrd[192 * S];
-    alignas(16) float gout[22 * S];
-    float tt[204];
-    float ceps[S][kCeps * kBands];
-    float dist[S][kCeps * kCeps];
-    float lastg[S][kBands];
-    float pf[S][kRnnPf];  // features of the frame the next F-C stage reads
-    int act[8][S];        // frame f in slot f & 7: valid and not silent
-    int memid[S], nfs[S];
-    long long fbase[S];
-    alignas(16) int8_t W[rnnimg::kBytes];
-  };
-  __shared__ Lds L;
-  const int tid = threadIdx.x;
-  const int sb = blockIdx.x * S;
-  const int *ra = a.rnn_act;
-  {
-    const int4 *src = reinterpret_cast<const int4 *>(a.rnn_img);
-    int4 *dst = reinterpret_cast<int4 *>(L.W);
-    for (int i = tid; i < rnnimg::kBytes / 16; i += NT) dst[i] = src[i];
-    for (int i = tid; i < 201; i += NT) L.tt[i] = a.plan->tansig[i];
-  }
-  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
-    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
-    L.ceps[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] : 0.0f;
-  }
-  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
-    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
-    L.dist[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] : 0.0f;
-  }
-  for (int idx = tid; idx < S * kBands; idx += NT) {
-    const int s = idx / kBands, i = idx - s * kBands;
-    L.lastg[s][i] = (sb + s < a.n_streams) ? a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] : 0.0f;
-  }
-  // states before frame 0 = "frame -1": gv slot 3, gn / gd slot 1
-  for (int idx = tid; idx < S * 96; idx += NT) {
-    const int s = idx / 96, i = idx - s * 96;
-    const bool ok = sb + s < a.n_streams;
-    const float *stp = a.state + (size_t)(sb + s) * st::kWords;
-    if (i < 24) L.gvT[3][i * S + s] = ok ? stp[st::kVadGru + i] : 0.0f;
-    if (i < 48) L.gnT[1][i * S + s] = ok ? stp[st::kNoiseGru + i] : 0.0f;
-    L.gdT[1][i * S + s] = ok ? stp[st::kDenGru + i] : 0.0f;
-  }
-  if (tid < 8 * S) L.act[tid / S][tid % S] = 0;
-  if (tid < S) {
-    const int s = sb + tid;
-    const bool ok = s < a.n_streams;
-    L.memid[tid] = ok ? reinterpret_cast<const int *>(a.state)[(size_t)s * st::kWords + st::kMemId] : 0;
-    L.nfs[tid] = ok ? ticks_of(a, s) * a.n_channels : 0;
-    L.fbase[tid] = (long long)s * a.V;
-  }
-  __syncthreads();
-  int maxnf = 0;
-#pragma unroll
-  for (int s = 0; s < S; s++) maxnf = max(maxnf, L.nfs[s]);
-  // prefetch lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (as 1.0 / 0.0)
-  const int pfs = tid / kRnnPf, pfi = tid - pfs * kRnnPf;
-  const bool pf_lane = tid < S * kRnnPf;
-  auto fetch = [&](int v) -> float {
-    if (!pf_lane || v >= L.nfs[pfs]) return 1.0f;  // past the end: treated as silent (inactive)
-    const long long f = L.fbase[pfs] + v;
-    if (pfi < kBands) return a.Lyf[f * kBands + pfi];
-    if (pfi < kBands + 7) return a.f34[f * 8 + (pfi - kBands)];
-    return a.silence[f] ? 1.0f : 0.0f;
-  };
-  // F-C: frame f's features from L.pf (cepstral memory, deltas, 34..40, the
-  // new distance row); item (s, i), i < 37; item i == 0 records act(f)
-  auto feat_c = [&](int f, int idx) {
-    const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
-    const bool valid = f < L.nfs[s];
-    const bool on = valid && L.pf[s][kRnnPf - 1] == 0.0f;
-    if (i == 0) {
-      L.act[f & 7][s] = on;
-      if (valid && !on) a.vadf[L.fbase[s] + f] = 0;  // silent: X passes through, state untouched
-    }
-    if (!on) return;
-    float *featT = L.featT[f & 3];
-    const int mi = L.memid[s];
-    const float *c0 = L.pf[s];  // ceps_0 (the row being written at memid)
-    if (i < kBands) {
-      L.ceps[s][mi * kBands + i] = c0[i];
-      if (i < 6) {
-        const float *c1 = L.ceps[s] + ((mi < 1) ? kCeps + mi - 1 : mi - 1) * kBands;
-        const float *c2 = L.ceps[s] + ((mi < 2) ? kCeps + mi - 2 : mi - 2) * kBands;
-        featT[i * S + s] = c0[i] + c1[i] + c2[i];
-        featT[(kBands + i) * S + s] = c0[i] - c2[i];
-        featT[(kBands + 6 + i) * S + s] = c0[i] - 2 * c1[i] + c2[i];
-      } else {
-        featT[i * S + s] = c0[i];
-      }
-    } else if (i < kBands + 7) {
-      featT[(34 + i - kBands) * S + s] = c0[i];
-    } else {
-      const int j = i - kBands - 7;
-      if (j != mi) {
-        const float *cj = L.ceps[s] + j * kBands;
-        float d = 0;
-#pragma unroll
-        for (int k = 0; k < kBands; k++) {
-          const float tmp = c0[k] - cj[k];
-          d += tmp * tmp;
-        }
-        L.dist[s][mi * kCeps + j] = d;
-        L.dist[s][j * kCeps + mi] = d;
-      }
-    }
-  };
-  // F-D: spectral variability of frame f, stream s
-  auto feat_d = [&](int f, int s) {
-    if (!L.act[f & 7][s]) return;
-    float sv = 0;
-    for (int i = 0; i < kCeps; i++) {
-      float mindist = 1e15f;
-      for (int j = 0; j < kCeps; j++)
-        if (j != i) mindist = (mindist < L.dist[s][i * kCeps + j]) ? mindist : L.dist[s][i * kCeps + j];
-      sv += mindist;
-    }
-    L.featT[f & 3][41 * S + s] = (float)(sv / kCeps - 2.1);
-    int mid = L.memid[s] + 1;
-    if (mid == kCeps) mid = 0;
-    L.memid[s] = mid;
-  };
-  // prologue: features and dense layer of frame 0, features of frame 1 staged
-  if (pf_lane) L.pf[pfs][pfi] = fetch(0);
-  __syncthreads();
-  for (int idx = tid; idx < S * (kBands + 7 + kCeps); idx += NT) feat_c(0, idx);
-  __syncthreads();
-  if (tid < S) feat_d(0, tid);
-  __syncthreads();
-  rnn_gates<0, S, G, NT>(L.W, RnnIn{L.featT[0], nullptr, nullptr}, nullptr, L.doutT[0], ra[0], L.tt, tid);
-  if (pf_lane) L.pf[pfs][pfi] = fetch(1);
-  float pf_next = fetch(2);
-  __syncthreads();
-  STAMP_INIT();
-  for (int t = 0; t <= maxnf + 2; t++) {
-    const int fv = t, fn = t - 1, fd = t - 2;
-    // ---- P1: z|r gates; features of t+1; gains of t-3
-    if (fn >= 0 && fn < maxnf) {
-      if (tid < 256)  // noise z|r tasks 0..255
-        rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 3]}, L.gnT[(fn + 1) & 1], L.zrn,
-                              kActSigmoid, L.tt, tid);
-    }
-    if (fd >= 0 && fd < maxnf && tid >= 256)  // denoise z|r tasks 0..767
-      rnn_gates<5, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 3]}, L.gdT[(fd + 1) & 1], L.zrd,
-                            kActSigmoid, L.tt, tid - 256);
-    if (fn >= 0 && fn < maxnf && tid < 128)  // noise z|r tasks 256..383
-      rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 3]}, L.gnT[(fn + 1) & 1], L.zrn,
-                            kActSigmoid, L.tt, 256 + tid);
-    if (fv < maxnf && tid >= 128 && tid < 320)  // vad z|r tasks 0..191
-      rnn_gates<1, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, kActSigmoid,
-                            L.tt, tid - 128);
-    if (t + 1 < maxnf && tid >= 768)
-      for (int idx = tid - 768; idx < S * (kBands + 7 + kCeps); idx += 256) feat_c(t + 1, idx);
-    if (t >= 3 && tid >= 576 && tid < 768) {  // gain smoothing g = max(g, .6*lastg) (denoise.c), frame t-3
-      const int f3 = t - 3;
-      for (int idx = tid - 576; idx < S * kBands; idx += 192) {
-        const int s = idx / kBands, i = idx - s * kBands;
-        if (!L.act[f3 & 7][s]) continue;
-        const long long f = L.fbase[s] + f3;
-        const float gi = L.gout[i * S + s];
-        const float al = .6f * L.lastg[s][i];
-        const float gsm = (gi > al) ? gi : al;
-        L.lastg[s][i] = gsm;
-        a.gr[f * kBands + i] = gi;
-        a.gs[f * kBands + i] = gsm;
-      }
-    }
-    __syncthreads();
-    RSTAMP(0);
-    // ---- P2: candidate gates; spectral variability of t+1
-    if (tid < 384) {
-      if (fd >= 0 && fd < maxnf)
-        rnn_cand<6, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 3]}, L.gdT[(fd + 1) & 1], L.zrd,
-                             L.gdT[fd & 1], L.act[fd & 7], ra[6], L.tt, tid);
-    } else if (tid < 576) {
-      if (fn >= 0 && fn < maxnf)
-        rnn_cand<4, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 3]}, L.gnT[(fn + 1) & 1], L.zrn,
-                             L.gnT[fn & 1], L.act[fn & 7], ra[4], L.tt, tid - 384);
-    } else if (tid < 672) {
-      if (fv < maxnf)
-        rnn_cand<2, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, L.gvT[fv & 3],
-                             L.act[fv & 7], ra[2], L.tt, tid - 576);
-    } else if (tid < 672 + S) {
-      if (t + 1 < maxnf) feat_d(t + 1, tid - 672);
-    }
-    __syncthreads();
-    RSTAMP(1);
-    // ---- P3: denoise_output(t-2), dense(t+1), vad_output(t); features of t+2 -> LDS
-    if (tid < 88) {
-      if (fd >= 0 && fd < maxnf)
-        rnn_gates<7, S, G, 0>(L.W, RnnIn{L.gdT[fd & 1], nullptr, nullptr}, nullptr, L.gout, ra[7], L.tt, tid);
-    } else if (tid < 88 + 96) {
-      if (t + 1 < maxnf)
-        rnn_gates<0, S, G, 0>(L.W, RnnIn{L.featT[(t + 1) & 3], nullptr, nullptr}, nullptr, L.doutT[(t + 1) & 3], ra[0],
-                              L.tt, tid - 88);
-    } else if (tid < 88 + 96 + S) {
-      const int s = tid - 184;
-      if (fv < maxnf && L.act[fv & 7][s]) {
-        constexpr int ob = rnnimg::off_b(8), ow = rnnimg::off_w(8);
-        float sum = (float)L.W[ob];
-        for (int j = 0; j < 24; j++) sum += (float)L.W[ow + j] * L.gvT[fv & 3][j * S + s];
-        a.vadf[L.fbase[s] + fv] = activate(L.tt, ra[8], kWs * sum);
-      }
-    }
-    if (pf_lane) L.pf[pfs][pfi] = pf_next;
-    pf_next = fetch(t + 3);
-    __syncthreads();
-    RSTAMP(2);
-  }
-  STAMP_FLUSH(0, 3);
-  const int fin = maxnf - 1;  // the slots of the latest states ("frame -1" if there were none)
-  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
-    const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
-    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] = L.ceps[s][i];
-  }
-  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
-    const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
-    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] = L.dist[s][i];
-  }
-  for (int idx = tid; idx < S * kBands; idx += NT) {
-    const int s = idx / kBands, i = idx - s * kBands;
-    if (sb + s < a.n_streams && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] = L.lastg[s][i];
-  }
-  for (int idx = tid; idx < S * 96; idx += NT) {
-    const int s = idx / 96, i = idx - s * 96;
-    if (sb + s >= a.n_streams || L.nfs[s] <= 0) continue;
-    float *stp = a.state + (size_t)(sb + s) * st::kWords;
-    if (i < 24) stp[st::kVadGru + i] = L.gvT[fin & 3][i * S + s];
-    if (i < 48) stp[st::kNoiseGru + i] = L.gnT[fin & 1][i * S + s];
-    stp[st::kDenGru + i] = L.gdT[fin & 1][i * S + s];
-  }
-  if (tid < S && sb + tid < a.n_streams && L.nfs[tid] > 0)
-    reinterpret_cast<int *>(a.state)[(size_t)(sb + tid) * st::kWords + st::kMemId] = L.memid[tid];
-}
-
-// ---------------------------------------------------------------------------
-// k_rnn3: k_rnn2's recurrence with 4 streams per lane (G = 2: one column's
-// 8 streams on two lanes) and a two-phase layer pipeline.  A lane's inputs
+// k_rnn3: the recurrence.  One workgroup owns 8 streams and walks their
+// frames in lockstep, 4 streams per lane (G = 2: one column's 8 streams on two
+// lanes), as a two-phase layer pipeline over frames: compute_rnn's GRUs
+// depend on each other only within a frame (vad -> noise -> denoise) and on
+// their own previous state, so one step runs different layers of different
+// frames side by side.  A lane's inputs
 // for one term are one 16-byte LDS read (ds_read_b128, full LDS rate; the
 // float2 reads of G = 4 were paired into half-rate ds_read2_b64) and one
 // int8 -> f32 conversion serves 4 streams.  Step t:
@@ -1923,142 +1121,6 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_synth: pitch_filter + gain application (no recurrence left once g / the
-// smoothed gains are known), then the inverse transform (forward FFT of the
-// Hermitian extension) and the synthesis window
-// ---------------------------------------------------------------------------
-template <int F>
-__global__ void __launch_bounds__(256) k_synth(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[F][kWinP];
-  __shared__ __attribute__((aligned(16))) float2 Xl[F][kFreq + 1];
-  __shared__ BandTab T;
-  __shared__ float rr[F][kBands + 2], nrm[F][kBands + 2], gs[F][kBands + 2], newE[F][kBands + 2];
-  __shared__ int fidx[F], fil[F];
-  const int tid = threadIdx.x;
-  FrameCtx cx;
-  frame_ctx_load(cx, a.plan, tid);
-  bandtab_load(T, a.plan, tid, 256);
-  const long long ngroups = ((long long)a.n_streams * a.V + F - 1) / F;
-  STAMP_INIT();
-  __shared__ long long gq;
-  if (threadIdx.x == 0) gq = take_group(a, kWorkSynth);
-  __syncthreads();
-  long long g = gq;
-  while (g < ngroups) {
-    group_frames<F>(a, g, tid, fidx);
-    __syncthreads();
-    if (tid < F) fil[tid] = fidx[tid] >= 0 && !a.silence[fidx[tid]];  // silent frames: X passes through
-    for (int idx = tid; idx < F * kFreq; idx += 256) {
-      const int fr = idx / kFreq, k = idx - fr * kFreq;
-      if (fidx[fr] >= 0) Xl[fr][k] = a.X[(size_t)fidx[fr] * kFreq + k];
-    }
-    __syncthreads();
-    if (tid < F * kBands) {
-      const int fr = tid / kBands, i = tid - fr * kBands;
-      if (fil[fr]) {
-        const size_t o = (size_t)fidx[fr] * kBands + i;
-        const float Exp = a.Exp[o], gg = a.gr[o], Ex = a.Ex[o], Ep = a.Ep[o];
-        float r;
-        if (Exp > gg)
-          r = 1;
-        else
-          r = (float)((double)((Exp * Exp) * (1 - (gg * gg))) / (.001 + (double)((gg * gg) * (1 - (Exp * Exp)))));
-        float cl = (0 > r) ? 0 : r;
-        cl = (1 < cl) ? 1 : cl;
-        r = (float)sqrt((double)cl);
-        r = (float)((double)r * sqrt((double)Ex / (1e-8 + (double)Ep)));
-        rr[fr][i] = r;
-        gs[fr][i] = a.gs[o];
-      }
-    }
-    __syncthreads();
-    RSTAMP(0);
-    // pitch filter X += r P, and the band terms of the filtered X (into W's
-    // rows: W is free until the synthesis input is staged)
-    for (int idx = tid; idx < F * kFreq; idx += 256) {
-      const int fr = idx / kFreq, k = idx - fr * kFreq;
-      if (fil[fr]) {
-        const float rf = interp_gain_t(rr[fr], T, k);
-        const float2 pk = a.P[(size_t)fidx[fr] * kFreq + k];
-        float2 xv = Xl[fr][k];
-        xv.x += rf * pk.x;
-        xv.y += rf * pk.y;
-        Xl[fr][k] = xv;
-        if (k < 400) {
-          float *tr = reinterpret_cast<float *>(W[fr]);
-          band_terms(xv, xv, T, k, tr[k], tr[400 + k]);
-        }
-      }
-    }
-    __syncthreads();
-    RSTAMP(1);
-    if (tid < F * kBands) {
-      const int fr = tid / kBands, i = tid - fr * kBands;
-      if (fil[fr]) {
-        const float *tr = reinterpret_cast<const float *>(W[fr]);
-        newE[fr][i] = band_chain(tr, tr + 400, T, i);
-        nrm[fr][i] = (float)sqrt((double)a.Ex[(size_t)fidx[fr] * kBands + i] / (1e-8 + (double)newE[fr][i]));
-      }
-    }
-    __syncthreads();
-    for (int idx = tid; idx < F * kFreq; idx += 256) {
-      const int fr = idx / kFreq, k = idx - fr * kFreq;
-      if (fil[fr]) {
-        const float nf = interp_gain_t(nrm[fr], T, k);
-        float2 val = Xl[fr][k];
-        val.x *= nf;
-        val.y *= nf;
-        const float gf = interp_gain_t(gs[fr], T, k);
-        val.x *= gf;
-        val.y *= gf;
-        Xl[fr][k] = val;
-      }
-    }
-    __syncthreads();
-    RSTAMP(2);
-#pragma unroll
-    for (int fr = 0; fr < F; fr++) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int i = tid + 256 * r;
-        if (i < kWin) {
-          float2 val;
-          if (i < kFreq) {
-            val = Xl[fr][i];
-          } else {
-            const float2 c = Xl[fr][kWin - i];
-            val = make_float2(c.x, -c.y);
-          }
-          W[fr][cx.dst[r]] = make_float2(kScale960 * val.x, kScale960 * val.y);
-        }
-      }
-    }
-    __syncthreads();
-    RSTAMP(3);
-    fft960_run<F, kWinP>(cx.tw, W, tid);
-#pragma unroll
-    for (int fr = 0; fr < F; fr++) {
-      const int f = fidx[fr];
-      if (f < 0) continue;
-      float *y = a.ys + (size_t)f * kWin;
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int i = tid + 256 * r;
-        if (i < kWin) {
-          const float yv = (i == 0) ? kWin * W[fr][0].x : kWin * W[fr][kWin - i].x;
-          y[i] = yv * cx.win[r];
-        }
-      }
-    }
-    if (tid == 0) gq = take_group(a, kWorkSynth);
-    __syncthreads();
-    RSTAMP(4);
-    g = gq;
-  }
-  STAMP_FLUSH(40, 5);
-}
-
-// ---------------------------------------------------------------------------
 // k_ola: out = x[0..479] + synthesis_mem; denoised * 1/32767; re-block ring;
 // per-tick vad_low (min over channels in channel order).  Two frames per
 // 256-thread workgroup, a float4 of samples per thread (32-bit frame
@@ -2330,9 +1392,6 @@ __device__ __forceinline__ double ra_push_long(float *buf, size_t bs, int n, uns
   return acc;
 }
 
-constexpr int kVadmS = 8;        // streams per workgroup
-constexpr int kVadmLds = 4225;   // LDS-resident long-term buffer length (odd: no bank conflicts)
-
 // One machine over all completed windows of the push for one stream; `lt`
 // points at entry 0 of the stream's long-term buffer, `lts` is its stride.
 __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t lts) {
@@ -2431,53 +1490,12 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
   a.vadm.st[(size_t)m * B + s] = S;
 }
 
-// One 64-thread workgroup per 8 streams.  Default-length long-term buffers
-// (4218 entries) of the 8 streams live in LDS for the whole push: loaded once
-// with all lanes, walked by the 8 stream lanes window after window, stored
-// back once.  Longer configurations walk them in HBM.  (The engine normally
-// runs k_vadm_hbm instead, on a side stream overlapped with the next push.)
-__global__ void __launch_bounds__(64) k_vadm(StagedArgs a) {
-  __shared__ float ltl[kVadmS][kVadmLds];
-  const int tid = threadIdx.x, sb = blockIdx.x * kVadmS;
-  const int B = a.n_streams, ns = min(kVadmS, B - sb);
-  if (ns <= 0) return;
-  for (int m = 0; m < a.vadm.n; m++) {
-    const VadmConst &K = a.vadm.c[m];
-    if (K.n_lt <= kVadmLds) {
-      for (int idx = tid; idx < ns * K.n_lt; idx += 64) {
-        const int i = idx / ns, j = idx - i * ns;
-        ltl[j][i] = a.vadm.buf[K.lt_off + (size_t)i * B + sb + j];
-      }
-      __syncthreads();
-      if (tid < ns && ticks_of(a, sb + tid) > 0) vadm_stream(a, m, sb + tid, ltl[tid], 1);
-      __syncthreads();
-      for (int idx = tid; idx < ns * K.n_lt; idx += 64) {
-        const int i = idx / ns, j = idx - i * ns;
-        a.vadm.buf[K.lt_off + (size_t)i * B + sb + j] = ltl[j][i];
-      }
-      __syncthreads();
-    } else if (tid < ns && ticks_of(a, sb + tid) > 0) {
-      vadm_stream(a, m, sb + tid, a.vadm.buf + K.lt_off + sb + tid, (size_t)B);
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // launcher
 // ---------------------------------------------------------------------------
 const char *staged_kernel_name(int i) {
-  // the variants launch_staged runs (FVAD_WFFT=0 / FVAD_RNN=2 select the older ones)
-  static const bool wfft = [] {
-    const char *v = getenv("FVAD_WFFT");
-    return !(v && atoi(v) == 0);
-  }();
-  static const bool rnn2 = [] {
-    const char *v = getenv("FVAD_RNN");
-    return v && atoi(v) == 2;
-  }();
-  static const char *const names[kStagedKernels] = {
-      "k_prep3", wfft ? "k_fftAw" : "k_fftA", "k_plpc", "k_pcorr", "k_select", wfft ? "k_pspecw" : "k_pspec",
-      rnn2 ? "k_rnn2" : "k_rnn3", wfft ? "k_synthw" : "k_synth", "k_ola", "k_winmeta", wfft ? "k_fftbw" : "k_fftb"};
+  static const char *const names[kStagedKernels] = {"k_prep3", "k_fftAw",  "k_plpc",  "k_pcorr",   "k_select", "k_pspecw",
+                                                    "k_rnn3",  "k_synthw", "k_ola",   "k_winmeta", "k_fftbw"};
   return (i >= 0 && i < kStagedKernels) ? names[i] : nullptr;
 }
 
@@ -2492,98 +1510,84 @@ int resident_blocks(K kernel, int threads, int n_cu) {
 }
 }  // namespace
 
+// every launch is checked where it is issued: a failed launch in the middle of
+// the pipeline returns its own error instead of surfacing at the end
+#define FVAD_LAUNCH_TRY(x)            \
+  do {                                \
+    const hipError_t e_ = (x);        \
+    if (e_ != hipSuccess) return e_;  \
+  } while (0)
+#define FVAD_KERNEL_TRY(...)                   \
+  do {                                         \
+    hipLaunchKernelGGL(__VA_ARGS__);           \
+    FVAD_LAUNCH_TRY(hipGetLastError());        \
+  } while (0)
+
 hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) {
-  if (ev) (void)hipEventRecord(ev[0], stream);
+  (void)hipGetLastError();
+  if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[0], stream));
   const int S = prep_streams(a.n_channels);
-  hipLaunchKernelGGL(k_prep3, dim3((a.n_streams + S - 1) / S), dim3(64), 0, stream, a);
-  if (ev) (void)hipEventRecord(ev[1], stream);
-  return hipGetLastError();
+  FVAD_KERNEL_TRY(k_prep3, dim3((a.n_streams + S - 1) / S), dim3(64), 0, stream, a);
+  if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[1], stream));
+  return hipSuccess;
 }
 
 hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev) {
   hipStream_t stream = st.main;
-  constexpr int NT = 256;
-  constexpr int FF = kFftFrames;
-  static const int g_fftA = resident_blocks(k_fftA<FF>, 256, n_cu);
-  static const int g_pspec = resident_blocks(k_pspec<FF>, 256, n_cu);
-  static const int g_synth = resident_blocks(k_synth<FF>, 256, n_cu);
   static const int g_plpc = resident_blocks(k_plpc, 256, n_cu);
-  // FVAD_WFFT=0 selects the workgroup-per-4-frames FFT kernels (comparison)
-  static const bool wfft = [] {
-    const char *v = getenv("FVAD_WFFT");
-    return !(v && atoi(v) == 0);
-  }();
   const long long frames = (long long)a.n_streams * a.V;
   auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
   (void)hipGetLastError();
   static_assert(kWorkSlots * kQueues <= kWorkCounters, "work counters");
-  (void)hipMemsetAsync(a.work, 0, kWorkSlots * kQueues * sizeof(unsigned), stream);
-  auto rec = [&](int k) {
-    if (ev) (void)hipEventRecord(ev[k], stream);
-  };
-  auto rec_aux = [&](int k) {
-    if (ev) (void)hipEventRecord(ev[k], st.aux);
-  };
-  // fork: k_fftA (aux) || pitch branch (main); both only read xs and write
-  // disjoint buffers (X, Ex, Lyf, silence | ptile, rec, pitch, pitch state)
-  const long long fgroups = (frames + FF - 1) / FF;
-  // without the fork (the default, aux == main) no fork / join events: a wait
+  FVAD_LAUNCH_TRY(hipMemsetAsync(a.work, 0, kWorkSlots * kQueues * sizeof(unsigned), stream));
+#define REC(k) \
+  if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[k], stream))
+#define REC_AUX(k) \
+  if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[k], st.aux))
+  // fork: k_fftAw (aux) || pitch branch (main); both only read xs and write
+  // disjoint buffers (X, Ex, Lyf, silence | ptile, rec, pitch, pitch state).
+  // Without the fork (the default, aux == main) no fork / join events: a wait
   // on the stream's own event still costs a barrier packet between kernels
   const bool forked = st.aux != stream;
   if (forked) {
-    (void)hipEventRecord(st.fork, stream);
-    (void)hipStreamWaitEvent(st.aux, st.fork, 0);
+    FVAD_LAUNCH_TRY(hipEventRecord(st.fork, stream));
+    FVAD_LAUNCH_TRY(hipStreamWaitEvent(st.aux, st.fork, 0));
   }
-  rec_aux(2);
-  if (wfft)
-    (void)launch_wave(kWaveFftA, a, n_cu, st.aux);
-  else
-    hipLaunchKernelGGL(k_fftA<FF>, grid(fgroups, g_fftA), dim3(NT), 0, st.aux, a);
-  rec_aux(3);
-  if (forked) (void)hipEventRecord(st.join, st.aux);
+  REC_AUX(2);
+  FVAD_LAUNCH_TRY(launch_wave(kWaveFftA, a, n_cu, st.aux));
+  REC_AUX(3);
+  if (forked) FVAD_LAUNCH_TRY(hipEventRecord(st.join, st.aux));
   {
     const long long tiles = (long long)((a.n_streams + 63) / 64) * a.n_ticks * a.n_channels;
-    rec(14);
-    hipLaunchKernelGGL(k_plpc, grid((tiles + 3) / 4, g_plpc), dim3(256), 0, stream, a);
-    rec(4);
-    (void)launch_pcorr(a, tiles, n_cu, stream);
+    REC(14);
+    FVAD_KERNEL_TRY(k_plpc, grid((tiles + 3) / 4, g_plpc), dim3(256), 0, stream, a);
+    REC(4);
+    FVAD_LAUNCH_TRY(launch_pcorr(a, tiles, n_cu, stream));
   }
-  rec(5);
-  hipLaunchKernelGGL(k_select, dim3((a.n_streams + kSelStreams - 1) / kSelStreams), dim3(64), 0, stream, a);
-  rec(6);
-  if (forked) (void)hipStreamWaitEvent(stream, st.join, 0);  // join
-  rec(7);
-  if (wfft)
-    (void)launch_wave(kWavePspec, a, n_cu, stream);
+  REC(5);
+  FVAD_KERNEL_TRY(k_select, dim3((a.n_streams + kSelStreams - 1) / kSelStreams), dim3(64), 0, stream, a);
+  REC(6);
+  if (forked) FVAD_LAUNCH_TRY(hipStreamWaitEvent(stream, st.join, 0));  // join
+  REC(7);
+  FVAD_LAUNCH_TRY(launch_wave(kWavePspec, a, n_cu, stream));
+  REC(8);
+  FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
+  REC(9);
+  FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
+  REC(10);
+  FVAD_KERNEL_TRY(k_ola, dim3((unsigned)((frames + 1) / 2)), dim3(256), 0, stream, a);
+  REC(11);
+  FVAD_KERNEL_TRY(k_winmeta, dim3((a.n_streams + kWmS - 1) / kWmS), dim3(64), 0, stream, a);
+  REC(12);
+  // FFT B: the wave-per-window kernel for 2048 points, the block kernel for 512
+  if (a.nfft_b == 2048)
+    FVAD_LAUNCH_TRY(launch_wave(kWaveFftB, a, n_cu, stream));
   else
-    hipLaunchKernelGGL(k_pspec<FF>, grid(fgroups, g_pspec), dim3(NT), 0, stream, a);
-  rec(8);
-  // FVAD_RNN=2 selects k_rnn2 (three phases, 2 streams per lane; comparison)
-  static const bool rnn2 = [] {
-    const char *v = getenv("FVAD_RNN");
-    return v && atoi(v) == 2;
-  }();
-  if (rnn2)
-  hipLaunchKernelGGL((k_rnn2<kRnnS, kRnnG, kRnnNT>), dim3((a.n_streams + kRnnS - 1) / kRnnS), dim3(kRnnNT), 0,
-                     stream, a);
-  else
-    hipLaunchKernelGGL(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
-  rec(9);
-  if (wfft)
-    (void)launch_wave(kWaveSynth, a, n_cu, stream);
-  else
-    hipLaunchKernelGGL(k_synth<FF>, grid(fgroups, g_synth), dim3(NT), 0, stream, a);
-  rec(10);
-  hipLaunchKernelGGL(k_ola, dim3((unsigned)((frames + 1) / 2)), dim3(256), 0, stream, a);
-  rec(11);
-  hipLaunchKernelGGL(k_winmeta, dim3((a.n_streams + kWmS - 1) / kWmS), dim3(64), 0, stream, a);
-  rec(12);
-  if (wfft && a.nfft_b == 2048)
-    (void)launch_wave(kWaveFftB, a, n_cu, stream);
-  else
-    hipLaunchKernelGGL(k_fftb<NT>, dim3(a.n_streams * a.wmax), dim3(NT), 0, stream, a);
-  rec(13);
-  return hipGetLastError();
+    FVAD_KERNEL_TRY(k_fftb<256>, dim3(a.n_streams * a.wmax), dim3(256), 0, stream, a);
+  REC(13);
+#undef REC
+#undef REC_AUX
+  return hipSuccess;
 }
 
 // k_vadm_hbm: the same machine, long-term buffers walked in HBM, no LDS, 16
@@ -2600,14 +1604,11 @@ __global__ void __launch_bounds__(64) k_vadm_hbm(StagedArgs a) {
     vadm_stream(a, m, s, a.vadm.buf + a.vadm.c[m].lt_off + s, (size_t)a.n_streams);
 }
 
-hipError_t launch_vadm(const StagedArgs &a, bool overlap, hipStream_t stream) {
+hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream) {
   (void)hipGetLastError();
-  if (overlap)
-    hipLaunchKernelGGL(k_vadm_hbm, dim3((a.n_streams + kVadmHbmLanes - 1) / kVadmHbmLanes), dim3(kVadmHbmLanes), 0,
-                       stream, a);
-  else
-    hipLaunchKernelGGL(k_vadm, dim3((a.n_streams + kVadmS - 1) / kVadmS), dim3(64), 0, stream, a);
-  return hipGetLastError();
+  FVAD_KERNEL_TRY(k_vadm_hbm, dim3((a.n_streams + kVadmHbmLanes - 1) / kVadmHbmLanes), dim3(kVadmHbmLanes), 0, stream,
+                  a);
+  return hipSuccess;
 }
 
 }  // namespace fvad

@@ -23,7 +23,7 @@ namespace fvad {
 // with its own LDS region, so a workgroup never waits at a barrier between
 // FFT stages; band terms go to the same region once the transform is done and
 // the 22 band chains run on lanes 0..21 (k_pspecw: Ep on 0..21 beside Exp on
-// 32..53).  Same arithmetic as k_fftA / k_pspec / k_synth.  Frames are taken
+// 32..53).  Same arithmetic as the fused k_frame.  Frames are taken
 // in batches of kWB consecutive frames per wave (dynamic, per-XCD queues as
 // take_group); k_fftAw runs each batch's serial Ly chains lane per frame.
 // ---------------------------------------------------------------------------

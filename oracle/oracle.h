@@ -23,7 +23,7 @@
  * (their sources and the rnnoise weights are absent, the Zig toolchain is absent,
  * there is no network).  The oracle IS pinned against every known-answer vector
  * the reference's own tests hold (SegmentWriter.zig:124-175,
- * MultiRingBuffer.zig:203-249, statistics.zig:472-546) and against derived KATs
+ * MultiRingBuffer.zig:203-249, statistics.zig:286-360) and against derived KATs
  * (FFT.zig normalisation, rnnoise analysis/synthesis perfect reconstruction,
  * silence gate, tansig/DCT tables) — see tests/test_oracle_*.py.
  *

@@ -54,7 +54,7 @@ def test_multi_ring_buffer_reference_vectors(oracle_mod):
 
 @pytest.mark.parametrize("case", REF["calc_false_positive"]["cases"])
 def test_calc_false_positive_reference_vectors(oracle_mod, case):
-    """statistics.zig:472-546 — refs [2,3],[4,5], extrude 2/2, fill gaps 2."""
+    """statistics.zig:286-360 — refs [2,3],[4,5], extrude 2/2, fill gaps 2."""
     v = REF["calc_false_positive"]
     fp = oracle_mod.calc_false_positive_sec(case["vad"][0], case["vad"][1], [tuple(r) for r in v["refs"]],
                                             extrude_start=v["extrude_start"], extrude_end=v["extrude_end"],
