@@ -118,6 +118,29 @@ struct fvad_engine {
   int raw_s16 = 0;  // rnnoise compat mode (s16-scaled I/O)
   unsigned long long *d_stamps = nullptr;
   unsigned *d_work = nullptr;  // staged: persistent-kernel group counters  // diagnostic stamp buffer (FVAD_STAMPS builds)
+  // Device inputs alternate by push (d_pcm aliases the current one): the
+  // input of push k+1 may be copied in while push k's k_prep3 still reads
+  // its own.  ev_in_free[i]: buffer i's last reader (k_prep3 / k_prep) done.
+  // run_resident reads d_pcm_b[0] (fvad_engine_load_synthetic).
+  float *d_pcm_b[2] = {};
+  hipEvent_t ev_in_free[2] = {};
+  bool in_busy[2] = {false, false};
+  int in_next = 0;
+  // Streaming ingest (fvad_engine_submit / collect): pinned host input slots
+  // and output slots per in-flight push, H2D copies on their own stream.
+  // Allocated on first use.
+  hipStream_t cstream = nullptr;
+  struct Slot {
+    float *in = nullptr;                 // pinned [max_ticks][B][C][480]
+    int32_t *ticks = nullptr;            // pinned [B]
+    float *vad = nullptr, *ratio = nullptr, *wratio = nullptr, *wvad = nullptr, *band = nullptr, *den = nullptr;
+    int32_t *wflag = nullptr;            // pinned outputs of the push that used this slot
+    hipEvent_t h2d = nullptr, done = nullptr;
+    bool h2d_busy = false, pending = false;
+    int n_ticks = 0;
+  } slots[2];
+  bool slots_ready = false;
+  int sub_next = 0, col_next = 0;
 };
 
 // Diagnostic builds: per-phase cycle totals of k_frame (thread 0 of every workgroup).
@@ -252,7 +275,7 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
 }
 
 void free_all(fvad_engine *e) {
-  void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm,   e->d_xbuf, e->d_ratio_b[0],
+  void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm_b[0], e->d_pcm_b[1], e->d_xbuf, e->d_ratio_b[0],
                   e->d_ratio_b[1], e->d_ticks_b[0], e->d_ticks_b[1], e->d_xs_b[0], e->d_xs_b[1],
                   e->d_vad,  e->wratio_b[0] ? e->wratio_b[0] : e->d_wratio,  e->wvad_b[0] ? e->wvad_b[0] : e->d_wvad,
                   e->band_b[0] ? e->band_b[0] : e->d_band, e->d_den,   e->wflag_b[0] ? e->wflag_b[0] : e->d_wflag,
@@ -272,6 +295,16 @@ void free_all(fvad_engine *e) {
   if (e->side) (void)hipStreamDestroy(e->side);
   if (e->aux) (void)hipStreamDestroy(e->aux);
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
+  if (e->cstream) (void)hipStreamDestroy(e->cstream);
+  for (auto &sl : e->slots) {
+    void *hp[] = {sl.in, sl.ticks, sl.vad, sl.ratio, sl.wratio, sl.wvad, sl.band, sl.den, sl.wflag};
+    for (void *q : hp)
+      if (q) (void)hipHostFree(q);
+    if (sl.h2d) (void)hipEventDestroy(sl.h2d);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
+  for (auto &ev : e->ev_in_free)
+    if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : e->ev_prep_done)
     if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : e->ev_buf_free)
@@ -288,6 +321,7 @@ int vadm_reset(fvad_engine *e);
 extern "C" int fvad_engine_reset(fvad_engine *e) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (e->cstream) HIP_TRY(hipStreamSynchronize(e->cstream));
   if (e->pstream) HIP_TRY(hipStreamSynchronize(e->pstream));
   if (e->vadm.n > 0) {
     HIP_TRY(hipStreamSynchronize(e->side));
@@ -365,11 +399,16 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t frames = T * B * C * fvad::kFrame;
   if ((rc = dalloc(&e->d_state, B * fvad::st::kWords)) || (rc = dalloc(&e->d_ring, B * C * e->ring_len)) ||
-      (rc = dalloc(&e->d_pcm, frames)) || (rc = dalloc(&e->d_ratio_b[0], T * B)) ||
+      (rc = dalloc(&e->d_pcm_b[0], frames)) || (rc = dalloc(&e->d_pcm_b[1], frames)) ||
+      (rc = dalloc(&e->d_ratio_b[0], T * B)) ||
       (rc = dalloc(&e->d_vad, T * B)) || (rc = dalloc(&e->d_wratio, T * B)) || (rc = dalloc(&e->d_wvad, T * B)) ||
       (rc = dalloc(&e->d_wflag, T * B)) || (rc = dalloc(&e->d_band, T * B * C * c.n_bands)) ||
       (rc = dalloc(&e->d_ticks_b[0], B)) || (c.want_denoised && (rc = dalloc(&e->d_den, frames))))
     return bail(rc);
+  e->d_pcm = e->d_pcm_b[0];
+  if (hipEventCreateWithFlags(&e->ev_in_free[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_in_free[1], hipEventDisableTiming) != hipSuccess)
+    return bail(fail(FVAD_EDEVICE, "hipEventCreate failed"));
   e->d_ratio = e->d_ratio_b[0];
   e->d_ticks = e->d_ticks_b[0];
   e->wflag_b[0] = e->wflag_b[1] = e->d_wflag;
@@ -408,6 +447,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
 extern "C" void fvad_engine_destroy(fvad_engine *e) {
   if (!e) return;
   (void)hipSetDevice(e->cfg.device);
+  if (e->cstream) (void)hipStreamSynchronize(e->cstream);
   if (e->pstream) (void)hipStreamSynchronize(e->pstream);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->side) (void)hipStreamSynchronize(e->side);
@@ -659,19 +699,92 @@ int fetch(fvad_engine *e, int n_ticks, fvad_outputs *o) {
 
 }  // namespace
 
+namespace {
+
+// the input of the push about to launch goes to device buffer in_next; its
+// previous reader (the k_prep3 of the push two before) must be done
+int input_buffer(fvad_engine *e, hipStream_t cs) {
+  const int ib = e->in_next;
+  if (e->in_busy[ib]) HIP_TRY(hipStreamWaitEvent(cs, e->ev_in_free[ib], 0));
+  e->d_pcm = e->d_pcm_b[ib];
+  return FVAD_OK;
+}
+
+// after the launch: the buffer is free again once this push's prep read it
+int release_input(fvad_engine *e) {
+  const int ib = e->in_next;
+  HIP_TRY(hipEventRecord(e->ev_in_free[ib], e->cfg.mode == FVAD_MODE_STAGED ? e->pstream : e->stream));
+  e->in_busy[ib] = true;
+  e->in_next = ib ^ 1;
+  e->resident_ticks = 0;
+  return FVAD_OK;
+}
+
+int check_ticks(const fvad_engine *e, const int32_t *ticks_valid, int n_ticks) {
+  if (ticks_valid)
+    for (int s = 0; s < e->cfg.n_streams; s++)
+      if (ticks_valid[s] < 0 || ticks_valid[s] > n_ticks) return fail(FVAD_EINVAL, "ticks_valid out of range");
+  return FVAD_OK;
+}
+
+// host copy into a pinned slot, split over threads for large inputs
+void par_copy(void *dst, const void *src, size_t bytes) {
+  constexpr size_t kChunk = 8u << 20;
+  unsigned nthr = std::thread::hardware_concurrency();
+  nthr = std::max(1u, std::min(nthr, 16u));
+  const size_t parts = std::min<size_t>(nthr, (bytes + kChunk - 1) / kChunk);
+  if (parts <= 1) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (size_t i = 0; i < parts; i++) {
+    const size_t a = bytes * i / parts, b = bytes * (i + 1) / parts;
+    pool.emplace_back([=]() { std::memcpy((char *)dst + a, (const char *)src + a, b - a); });
+  }
+  for (auto &t : pool) t.join();
+}
+
+int ensure_slots(fvad_engine *e) {
+  if (e->slots_ready) return FVAD_OK;
+  const fvad_engine_config &c = e->cfg;
+  const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
+  const size_t TB = T * B, frames = TB * C * fvad::kFrame;
+  if (!e->cstream && hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) != hipSuccess)
+    return fail(FVAD_EDEVICE, "copy stream creation failed");
+  auto host = [&](auto **p, size_t count) -> int {
+    if (hipHostMalloc(reinterpret_cast<void **>(p), std::max<size_t>(count, 1) * 4, 0) != hipSuccess)
+      return fail(FVAD_ENOMEM, "hipHostMalloc failed (pinned input / output slots)");
+    return FVAD_OK;
+  };
+  for (auto &sl : e->slots) {
+    int rc;
+    if ((rc = host(&sl.in, frames)) || (rc = host(&sl.ticks, B)) || (rc = host(&sl.vad, TB)) ||
+        (rc = host(&sl.ratio, TB)) || (rc = host(&sl.wflag, TB)) || (rc = host(&sl.wratio, TB)) ||
+        (rc = host(&sl.wvad, TB)) || (rc = host(&sl.band, TB * C * c.n_bands)) ||
+        (c.want_denoised && (rc = host(&sl.den, frames))))
+      return rc;
+    if (hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
+      return fail(FVAD_EDEVICE, "hipEventCreate failed");
+  }
+  e->slots_ready = true;
+  return FVAD_OK;
+}
+
+}  // namespace
+
 extern "C" int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
                                 fvad_outputs *out) {
   if (!e || !pcm) return fail(FVAD_EINVAL, "null argument");
   const fvad_engine_config &c = e->cfg;
   if (n_ticks < 0 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range [0, max_ticks]");
   if (n_ticks == 0) return FVAD_OK;
+  int rc = check_ticks(e, ticks_valid, n_ticks);
+  if (rc) return rc;
   HIP_TRY(hipSetDevice(c.device));
   const size_t bytes = (size_t)n_ticks * c.n_streams * c.n_channels * fvad::kFrame * sizeof(float);
-  if (ticks_valid)
-    for (int s = 0; s < c.n_streams; s++)
-      if (ticks_valid[s] < 0 || ticks_valid[s] > n_ticks) return fail(FVAD_EINVAL, "ticks_valid out of range");
-  // staged: the inputs go through the prep stream (the input of push k-1 is
-  // read only by its k_prep3, earlier on that stream; ticks buffer b is free
+  // staged: the inputs go through the prep stream (ticks buffer b is free
   // once push k-2 finished)
   hipStream_t cs = e->stream;
   int *dticks = e->d_ticks;
@@ -681,13 +794,114 @@ extern "C" int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, c
     cs = e->pstream;
     dticks = e->d_ticks_b[b];
   }
+  if ((rc = input_buffer(e, cs))) return rc;
   HIP_TRY(hipMemcpyAsync(e->d_pcm, pcm, bytes, hipMemcpyHostToDevice, cs));
   if (ticks_valid)
     HIP_TRY(hipMemcpyAsync(dticks, ticks_valid, sizeof(int32_t) * c.n_streams, hipMemcpyHostToDevice, cs));
-  e->resident_ticks = 0;
-  int rc = launch(e, n_ticks, ticks_valid != nullptr, false);
-  if (rc) return rc;
+  if ((rc = launch(e, n_ticks, ticks_valid != nullptr, false))) return rc;
+  if ((rc = release_input(e))) return rc;
   return fetch(e, n_ticks, out);
+}
+
+extern "C" float *fvad_engine_input_slot(fvad_engine *e) {
+  if (!e) {
+    fail(FVAD_EINVAL, "null engine");
+    return nullptr;
+  }
+  if (hipSetDevice(e->cfg.device) != hipSuccess || ensure_slots(e)) return nullptr;
+  auto &sl = e->slots[e->sub_next];
+  if (sl.h2d_busy) {
+    if (hipEventSynchronize(sl.h2d) != hipSuccess) {
+      fail(FVAD_EDEVICE, "hipEventSynchronize failed");
+      return nullptr;
+    }
+    sl.h2d_busy = false;
+  }
+  return sl.in;
+}
+
+extern "C" int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid) {
+  if (!e || !pcm) return fail(FVAD_EINVAL, "null argument");
+  const fvad_engine_config &c = e->cfg;
+  if (n_ticks < 1 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range [1, max_ticks]");
+  int rc = check_ticks(e, ticks_valid, n_ticks);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c.device));
+  if ((rc = ensure_slots(e))) return rc;
+  const int si = e->sub_next;
+  auto &sl = e->slots[si];
+  if (sl.pending) return fail(FVAD_EINVAL, "two pushes in flight: collect the older one first");
+  const size_t B = c.n_streams, TB = (size_t)n_ticks * B;
+  const size_t bytes = TB * c.n_channels * fvad::kFrame * sizeof(float);
+  if (pcm != sl.in) {  // otherwise the producer wrote into the slot (fvad_engine_input_slot)
+    if (sl.h2d_busy) HIP_TRY(hipEventSynchronize(sl.h2d));
+    par_copy(sl.in, pcm, bytes);
+  }
+  if (ticks_valid) std::memcpy(sl.ticks, ticks_valid, B * sizeof(int32_t));
+  // staged: copies on the copy stream, overlapping the previous push's
+  // kernels; the prep stream waits for them.  Fused: everything in order on
+  // the engine stream (its kernels read d_ticks in place).
+  const bool staged = c.mode == FVAD_MODE_STAGED;
+  hipStream_t cs = staged ? e->cstream : e->stream;
+  if ((rc = input_buffer(e, cs))) return rc;
+  HIP_TRY(hipMemcpyAsync(e->d_pcm, sl.in, bytes, hipMemcpyHostToDevice, cs));
+  if (ticks_valid) {
+    int *dticks = e->d_ticks;
+    if (staged) {
+      const int b = e->next_buf;
+      if (e->buf_busy[b]) HIP_TRY(hipStreamWaitEvent(cs, e->ev_buf_free[b], 0));
+      dticks = e->d_ticks_b[b];
+    }
+    HIP_TRY(hipMemcpyAsync(dticks, sl.ticks, B * sizeof(int32_t), hipMemcpyHostToDevice, cs));
+  }
+  HIP_TRY(hipEventRecord(sl.h2d, cs));
+  sl.h2d_busy = true;
+  if (staged) HIP_TRY(hipStreamWaitEvent(e->pstream, sl.h2d, 0));
+  if ((rc = launch(e, n_ticks, ticks_valid != nullptr, false))) return rc;
+  if ((rc = release_input(e))) return rc;
+  // outputs into the slot's pinned buffers, after the kernels on the engine
+  // stream (the next push's kernels queue behind these copies)
+  auto d2h = [&](void *dst, const void *src, size_t n) -> int {
+    HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, e->stream));
+    return FVAD_OK;
+  };
+  if ((rc = d2h(sl.vad, e->d_vad, TB * 4)) || (rc = d2h(sl.ratio, e->d_ratio, TB * 4)) ||
+      (rc = d2h(sl.wflag, e->d_wflag, TB * 4)) || (rc = d2h(sl.wratio, e->d_wratio, TB * 4)) ||
+      (rc = d2h(sl.wvad, e->d_wvad, TB * 4)) || (rc = d2h(sl.band, e->d_band, TB * c.n_channels * c.n_bands * 4)) ||
+      (c.want_denoised && (rc = d2h(sl.den, e->d_den, bytes))))
+    return rc;
+  HIP_TRY(hipEventRecord(sl.done, e->stream));
+  sl.pending = true;
+  sl.n_ticks = n_ticks;
+  e->sub_next = si ^ 1;
+  return FVAD_OK;
+}
+
+extern "C" int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_ticks) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  auto &sl = e->slots[e->col_next];
+  if (!e->slots_ready || !sl.pending) return fail(FVAD_EINVAL, "no submitted push to collect");
+  const fvad_engine_config &c = e->cfg;
+  HIP_TRY(hipSetDevice(c.device));
+  HIP_TRY(hipEventSynchronize(sl.done));
+  const size_t TB = (size_t)sl.n_ticks * c.n_streams;
+  if (out) {
+    if (out->denoised && !c.want_denoised) return fail(FVAD_EINVAL, "engine created without want_denoised");
+    auto cp = [](void *dst, const void *src, size_t n) {
+      if (dst) std::memcpy(dst, src, n);
+    };
+    cp(out->vad, sl.vad, TB * 4);
+    cp(out->ratio, sl.ratio, TB * 4);
+    cp(out->win_flag, sl.wflag, TB * 4);
+    cp(out->win_ratio, sl.wratio, TB * 4);
+    cp(out->win_vad, sl.wvad, TB * 4);
+    cp(out->band, sl.band, TB * c.n_channels * c.n_bands * 4);
+    if (out->denoised) par_copy(out->denoised, sl.den, TB * c.n_channels * fvad::kFrame * 4);
+  }
+  if (n_ticks) *n_ticks = sl.n_ticks;
+  sl.pending = false;
+  e->col_next ^= 1;
+  return FVAD_OK;
 }
 
 extern "C" int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t base) {
@@ -715,7 +929,10 @@ extern "C" int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t 
     });
   }
   for (auto &th : pool) th.join();
-  HIP_TRY(hipMemcpy(e->d_pcm, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+  // buffer 0 may still be read by an in-flight push
+  const int rc = fvad_engine_sync(e);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(e->d_pcm_b[0], host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
   e->resident_ticks = n_ticks;
   return FVAD_OK;
 }
@@ -730,17 +947,23 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
   e->ev = e->evs[e->ev_slot];
   int rc = collect_slot(e, e->ev_slot);
   if (rc) return rc;
+  e->d_pcm = e->d_pcm_b[0];
   // FVAD_NO_EVENTS=1: no timing events (diagnostic: their cost on the push)
   static const bool no_events = [] {
     const char *v = getenv("FVAD_NO_EVENTS");
     return v && atoi(v) == 1;
   }();
-  return launch(e, n_ticks, false, !no_events);
+  if ((rc = launch(e, n_ticks, false, !no_events))) return rc;
+  // a later submit / push must not overwrite buffer 0 under this run's prep
+  HIP_TRY(hipEventRecord(e->ev_in_free[0], e->cfg.mode == FVAD_MODE_STAGED ? e->pstream : e->stream));
+  e->in_busy[0] = true;
+  return FVAD_OK;
 }
 
 extern "C" int fvad_engine_sync(fvad_engine *e) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (e->cstream) HIP_TRY(hipStreamSynchronize(e->cstream));
   if (e->pstream) HIP_TRY(hipStreamSynchronize(e->pstream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (e->side) {

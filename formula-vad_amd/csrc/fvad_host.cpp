@@ -533,14 +533,23 @@ extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size
   std::vector<std::thread> th;
   for (size_t pi = 0; pi < m->parts.size(); pi++) {
     th.emplace_back([&, pi]() {
+      // streaming: the next push is gathered straight into the engine's
+      // pinned input slot and submitted while the previous one still runs
+      // (fvad_engine_submit); no per-tick outputs come back, the VADMachines
+      // run on the device (k_vadm_hbm)
       fvad_multi::Part &p = m->parts[pi];
       const int B = p.s1 - p.s0, T = p.ec.max_ticks;
       size_t max_frames = 0;
       for (int s = p.s0; s < p.s1; s++) max_frames = std::max(max_frames, len[s] / fvad::kFrame);
-      std::vector<float> buf((size_t)T * B * C * fvad::kFrame, 0.0f);
       std::vector<int32_t> valid(B);
-      for (size_t f0 = 0; f0 < max_frames; f0 += T) {
+      int in_flight = 0, rc = FVAD_OK;
+      for (size_t f0 = 0; f0 < max_frames && !rc; f0 += T) {
         const int nt = (int)std::min<size_t>(T, max_frames - f0);
+        float *buf = fvad_engine_input_slot(p.engine);
+        if (!buf) {
+          rc = FVAD_EDEVICE;
+          break;
+        }
         for (int b = 0; b < B; b++) {
           const int s = p.s0 + b;
           const size_t frames_s = len[s] / fvad::kFrame;
@@ -550,13 +559,15 @@ extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size
               std::memcpy(&buf[(((size_t)t * B + b) * C + c) * fvad::kFrame],
                           pcm[s] + (size_t)c * len[s] + (f0 + t) * fvad::kFrame, fvad::kFrame * sizeof(float));
         }
-        // VADMachines run on the device (k_vadm); no per-tick outputs come back
-        const int rc = fvad_engine_push(p.engine, buf.data(), nt, valid.data(), nullptr);
-        if (rc) {
-          rcs[pi] = rc;
-          return;
-        }
+        if (in_flight == 2 && !(rc = fvad_engine_collect(p.engine, nullptr, nullptr))) in_flight--;
+        if (!rc && !(rc = fvad_engine_submit(p.engine, buf, nt, valid.data()))) in_flight++;
       }
+      while (in_flight > 0) {
+        const int r2 = fvad_engine_collect(p.engine, nullptr, nullptr);
+        if (!rc) rc = r2;
+        in_flight--;
+      }
+      rcs[pi] = rc;
     });
   }
   for (auto &t : th) t.join();

@@ -117,6 +117,9 @@ SYMBOLS = [
     ("fvad_engine_destroy", None, [C.c_void_p]),
     ("fvad_engine_reset", C.c_int, [C.c_void_p]),
     ("fvad_engine_push", C.c_int, [C.c_void_p, F32P, C.c_int, I32P, C.c_void_p]),
+    ("fvad_engine_input_slot", C.c_void_p, [C.c_void_p]),
+    ("fvad_engine_submit", C.c_int, [C.c_void_p, F32P, C.c_int, I32P]),
+    ("fvad_engine_collect", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]),
     ("fvad_engine_load_synthetic", C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
     ("fvad_engine_run_resident", C.c_int, [C.c_void_p, C.c_int]),
     ("fvad_engine_sync", C.c_int, [C.c_void_p]),
@@ -237,6 +240,7 @@ class Engine:
         _check(lib().fvad_engine_create(C.byref(cfg), model.h, C.byref(h)), "fvad_engine_create")
         self.h = h
         self.B, self.C, self.nb = n_streams, n_channels, len(bands)
+        self.max_ticks = max_ticks
 
     def _alloc_out(self, n_ticks, denoised):
         T, B, Ch, nb = n_ticks, self.B, self.C, self.nb
@@ -261,6 +265,36 @@ class Engine:
         _check(lib().fvad_engine_push(self.h, fptr(pcm), T, tv.ctypes.data_as(I32P) if tv is not None else None,
                                       C.byref(s)), "fvad_engine_push")
         return o
+
+    def input_slot(self):
+        """The engine's pinned input slot for the next submit, as a
+        [max_ticks][streams][channels][480] float32 view (fill it in place
+        and pass it to submit: no host copy)."""
+        p = lib().fvad_engine_input_slot(self.h)
+        if not p:
+            raise FvadError("fvad_engine_input_slot: %s" % last_error())
+        n = self.max_ticks * self.B * self.C * FRAME
+        arr = np.ctypeslib.as_array(C.cast(p, F32P), shape=(n,))
+        return arr.reshape(self.max_ticks, self.B, self.C, FRAME)
+
+    def submit(self, pcm, ticks_valid=None):
+        """Asynchronous push (fvad_engine_submit): returns once queued."""
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        assert pcm.shape[1:] == (self.B, self.C, FRAME), pcm.shape
+        tv = np.ascontiguousarray(ticks_valid, np.int32) if ticks_valid is not None else None
+        self._sub_keep = tv
+        _check(lib().fvad_engine_submit(self.h, fptr(pcm), pcm.shape[0],
+                                        tv.ctypes.data_as(I32P) if tv is not None else None), "fvad_engine_submit")
+
+    def collect(self, denoised=False, want=True):
+        """Outputs of the oldest submitted push (fvad_engine_collect)."""
+        if not want:
+            _check(lib().fvad_engine_collect(self.h, None, None), "fvad_engine_collect")
+            return None
+        o, s = self._alloc_out(self.max_ticks, denoised)
+        n = C.c_int()
+        _check(lib().fvad_engine_collect(self.h, C.byref(s), C.byref(n)), "fvad_engine_collect")
+        return {k: v[: n.value] for k, v in o.items()}
 
     def reset(self):
         _check(lib().fvad_engine_reset(self.h), "fvad_engine_reset")

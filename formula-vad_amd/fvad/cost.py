@@ -3,12 +3,20 @@ rnnoise, plus its share of FFT B) — the unit of the bench metric.
 
 Counts follow the loop trip counts of the restated algorithm (SURVEY.md
 Appendix A / oracle/ora_rnnoise.c): every f32/f64 add, sub, mul, div and sqrt
-is one flop; table lookups, copies, compares and max/min are free.  Pitch
-candidate work uses its upper bound (10 fine-search lags, 14 remove_doubling
-candidates).  The per-phase breakdown is reproduced in DESIGN.md §Roofline.
+is one flop; table lookups, copies, compares and max/min are free.  The
+data-dependent trip counts (fine-search lags, remove_doubling candidates, the
+silence gate) are the instrumented averages of the oracle on the bench's own
+input (MEASURED, from tests/count_ops.py), not upper bounds.  The per-phase
+breakdown is reproduced in DESIGN.md §5.
 """
 
 FRAME = 480
+
+# tests/count_ops.py on the bench workload (256 of the 2048 synthetic streams,
+# 4 pushes of the same 50 resident ticks, as bench.py runs them): per
+# channel-frame averages; tests/test_host_cpu.py recounts them
+MEASURED = {"fine_lags_per_frame": 9.4088, "rd_cands_per_frame": 7.1532, "silent_frac": 0.0,
+            "frames_counted": 102400}
 PTILE_ROWS = 864 + 147 + 294 + 385 + 1  # k_plpc -> k_pcorr rows per frame (fvad_staged.h ptile)
 
 
@@ -47,20 +55,23 @@ def gru_flops(nin, nout):
     return 2 * macs + extra + act
 
 
-def phases(n_channels=2, fft_size=2048):
+def phases(n_channels=2, fft_size=2048, counts=None):
+    m = counts or MEASURED
+    fine, rd, live = m["fine_lags_per_frame"], m["rd_cands_per_frame"], 1.0 - m["silent_frac"]
     p = {}
     p["prep: s16 scale + HP biquad + rms"] = FRAME * (1 + 1 + 3 + 4 + 2) + 2
     p["analysis window + FFT A + scale"] = 960 + 1920 + _fft960()
     p["band energy Ex"] = _band_sum()
     p["pitch downsample + autocorr + LPC + FIR5"] = 864 * 4 + 5 * 864 * 2 + 60 + 864 * 10
     p["coarse xcorr 147x240 + find_best_pitch"] = 147 * 240 * 2 + 240 * 2 + 147 * 8
-    p["fine xcorr <=10x480 + find_best_pitch"] = 10 * 480 * 2 + 480 * 2 + 294 * 8
-    p["remove_doubling"] = 480 * 4 + 480 * 2 + 384 * 4 + 14 * 480 * 4 + 3 * 480 * 2 + 14 * 12
+    p["fine xcorr <=10x480 + find_best_pitch"] = fine * 480 * 2 + 480 * 2 + 294 * 8
+    p["remove_doubling"] = 480 * 4 + 480 * 2 + 384 * 4 + rd * 480 * 4 + 3 * 480 * 2 + rd * 12
     p["pitch window + FFT + Ep + Exp"] = 960 + 1920 + _fft960() + 2 * _band_sum() + 22 * 5
     p["features (log10, DCTs, cepstra, spectral variability)"] = 22 * 3 + 28 * 44 + 18 * 3 + 8 * 8 * 22 * 3 + 16
-    p["GRU stack"] = (2 * 42 * 24 + 24 * 10) + gru_flops(24, 24) + 2 * 24 + gru_flops(90, 48) + \
-        gru_flops(114, 96) + (2 * 96 * 22 + 22 * 12)
-    p["pitch filter + gains"] = 22 * 20 + 481 * 7 + _band_sum() + 22 * 6 + 481 * (2 * 3 + 4)
+    # skipped on frames under the silence gate (denoise.c: if (!silence))
+    p["GRU stack"] = live * ((2 * 42 * 24 + 24 * 10) + gru_flops(24, 24) + 2 * 24 + gru_flops(90, 48) +
+                             gru_flops(114, 96) + (2 * 96 * 22 + 22 * 12))
+    p["pitch filter + gains"] = live * (22 * 20 + 481 * 7 + _band_sum() + 22 * 6 + 481 * (2 * 3 + 4))
     p["synthesis (scale, FFT A, window, OLA, 1/32767)"] = 1920 + _fft960() + 960 + 960 + 480 + 480
     p["re-block + FFT B share"] = _fftb_per_window(fft_size) * FRAME / fft_size + 4
     p["VADMachine share"] = _vadm_per_window() * FRAME / fft_size / n_channels
@@ -76,6 +87,14 @@ def _vadm_per_window(n_lt=4218, n_st=4, n_r=11):
 
 def flops_per_channel_frame(n_channels=2, fft_size=2048):
     return sum(phases(n_channels, fft_size).values())
+
+
+def path_bytes_per_channel_frame(n_channels=2, state_bytes=12236):
+    """SURVEY.md §8(d) B_alg, the real-time tick model: input 1920 B + vad 4 B
+    + band ~1 B + the rnnoise state read and written once per stream-tick
+    (shared by the C channels) + the FFT-B carry of the denoised frame written
+    and read (3840 B)."""
+    return 1920 + 4 + 1 + 2.0 * state_bytes / n_channels + 3840
 
 
 def frame_kernel_bytes(n_streams, n_channels, n_ticks, n_bands=1, state_words=2816, live_state_words=2788,
@@ -105,43 +124,41 @@ def staged_kernels(n_channels=2, fft_size=2048):
     final 3-lag xcorr for every candidate instead of the selected one) is
     counted once, as the reference computes it."""
     p = phases(n_channels, fft_size)
+    rd = MEASURED["rd_cands_per_frame"]
     C = n_channels
     feat = p["features (log10, DCTs, cepstra, spectral variability)"]
     dct_ly = 22 * 44 + 22 * 2
     dct_exp = 6 * 44 + 6 * 2
     spec = 481 * 8  # one complex spectrum
     pitch = (p["pitch downsample + autocorr + LPC + FIR5"] + p["coarse xcorr 147x240 + find_best_pitch"] +
-             p["fine xcorr <=10x480 + find_best_pitch"] + p["remove_doubling"] - 14 * 12)
+             p["fine xcorr <=10x480 + find_best_pitch"] + p["remove_doubling"] - rd * 12)
     # k_plpc: x_lp, autocorr, LPC, FIR and the serial energy recurrences
     # (coarse / fine Syy init + updates, xx, yy_lookup); k_pcorr the rest
     plpc = (p["pitch downsample + autocorr + LPC + FIR5"] + 240 * 2 + 147 * 4 + 480 * 2 + 294 * 4 +
             480 * 2 + 384 * 4)
     k = {
         "k_prep3": (p["prep: s16 scale + HP biquad + rms"], 480 * 4 * 2 + 4.0 / C),
-        "k_fftA": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly,
+        "k_fftAw": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly,
                    960 * 4 + spec + 22 * 4 * 2 + 4),
         "k_plpc": (plpc, 1728 * 4 + PTILE_ROWS * 4),
-        "k_pcorr": (pitch - plpc - 14 * 4, (864 + 147 + 10 + 29 + 1) * 4 + 80 * 4),
-        "k_select": (14 * 4 + 14 * 12, 80 * 4 + 4),
-        "k_pspec": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
-        # k_rnn: cepstral memory, spectral variability, GRU stack, gain
+        "k_pcorr": (pitch - plpc - rd * 4, (864 + 147 + 10 + 29 + 1) * 4 + 80 * 4),
+        "k_select": (rd * 4 + rd * 12, 80 * 4 + 4),
+        "k_pspecw": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
+        # k_rnn3: cepstral memory, spectral variability, GRU stack, gain
         # smoothing; reads DCT(Ly), features 34..40, silence; writes g, smoothed g, vad
-        "k_rnn2": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"],
+        "k_rnn3": (feat - 22 * 3 - dct_ly - dct_exp + p["GRU stack"],
                   (22 + 8 + 1) * 4 + (22 + 22 + 1) * 4),
-        # k_synth: pitch filter (X + r P, band energies, norm), gains, synthesis;
+        # k_synthw: pitch filter (X + r P, band energies, norm), gains, synthesis;
         # reads X, P, Exp, g, Ex, Ep, smoothed g, silence; writes the windowed frame
-        "k_synth": (p["pitch filter + gains"] + p["synthesis (scale, FFT A, window, OLA, 1/32767)"] - 960,
+        "k_synthw": (p["pitch filter + gains"] + p["synthesis (scale, FFT A, window, OLA, 1/32767)"] - 960,
                     2 * spec + 5 * 22 * 4 + 4 + 960 * 4),
         "k_ola": (960, 960 * 4 + 480 * 4 + 4.0 / C),
         "k_winmeta": (0.0, 4 * 4.0 / C),
+        "k_fftbw": (p["re-block + FFT B share"], 480 * 4 + 4),
+        # fft_size 512: the workgroup-per-window kernel, same work
         "k_fftb": (p["re-block + FFT B share"], 480 * 4 + 4),
-        "k_vadm": (p["VADMachine share"], (4218 + 4 + 11 + 2) * 4 * FRAME / fft_size / C + 16),
+        "k_vadm_hbm": (p["VADMachine share"], (4218 + 4 + 11 + 2) * 4 * FRAME / fft_size / C + 16),
     }
-    k["k_vadm_hbm"] = k["k_vadm"]
-    # wave-per-frame / 4-streams-per-lane variants: same algorithmic work
-    for old, new in (("k_fftA", "k_fftAw"), ("k_pspec", "k_pspecw"), ("k_synth", "k_synthw"), ("k_fftb", "k_fftbw"),
-                     ("k_rnn2", "k_rnn3")):
-        k[new] = k[old]
     return {n: {"flops": f, "bytes": b} for n, (f, b) in k.items()}
 
 

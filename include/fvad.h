@@ -143,6 +143,21 @@ typedef struct {
 int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
                      fvad_outputs *out);
 
+/* Streaming ingest (the simulator's read loop, SimulationInstance.zig:194-203,
+ * reads the next chunk while the pipeline works on the last one).  Two pushes
+ * may be in flight: submit copies the input into a pinned slot (or takes it in
+ * place when pcm is the pointer fvad_engine_input_slot returned), queues the
+ * H2D copy on its own stream -- overlapping the previous push's kernels -- then
+ * the kernels and the output copies into pinned memory, and returns without
+ * waiting.  collect returns the outputs of the oldest submitted push (blocking
+ * until they are on the host; out may be NULL, *n_ticks its tick count).
+ * submit fails with FVAD_EINVAL while two pushes are uncollected. */
+/* the pinned [max_ticks][streams][channels][480] slot the next submit reads;
+ * blocks until that slot's previous copy to the device finished; NULL on error */
+float *fvad_engine_input_slot(fvad_engine *e);
+int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid);
+int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_ticks);
+
 /* Device-resident variants for benchmarking / zero-copy producers. */
 /* allocate a device input of n_ticks and fill it with the synthetic generator */
 int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t stream_id_base);

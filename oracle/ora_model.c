@@ -231,3 +231,62 @@ double ora_bench_denoise(const ora_model *m, const float *pcm, int n_streams, in
   clock_gettime(CLOCK_MONOTONIC, &b);
   return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 }
+
+typedef struct {
+  ora_pipeline **pipes;
+  const float *pcm;
+  int s0, s1, n_channels;
+  size_t n_samples, chunk;
+} pipe_job;
+
+static void *pipe_worker(void *arg) {
+  const pipe_job *j = (const pipe_job *)arg;
+  const float *ch[16];
+  size_t off, n;
+  int s, c;
+  for (s = j->s0; s < j->s1; s++) {
+    for (off = 0; off < j->n_samples; off += n) {
+      n = j->n_samples - off < j->chunk ? j->n_samples - off : j->chunk;
+      for (c = 0; c < j->n_channels; c++) ch[c] = j->pcm + ((size_t)s * j->n_channels + c) * j->n_samples + off;
+      ora_pipeline_push(j->pipes[s], ch, n);
+    }
+  }
+  return NULL;
+}
+
+double ora_bench_pipeline(const ora_model *m, const float *pcm, int n_streams, int n_channels,
+                          size_t n_samples, size_t chunk, int n_threads, uint64_t *counts) {
+  pthread_t th[256];
+  pipe_job jobs[256];
+  struct timespec a, b;
+  ora_pipeline **pipes;
+  ora_vadm_config cfg;
+  int i;
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  if (n_threads > n_streams) n_threads = n_streams;
+  if (n_channels < 1 || n_channels > 16 || chunk == 0) return -1.0;
+  ora_tables(NULL, NULL, NULL);
+  ora_vadm_config_default(&cfg);
+  pipes = (ora_pipeline **)calloc((size_t)n_streams, sizeof(*pipes));
+  for (i = 0; i < n_streams; i++) pipes[i] = ora_pipeline_create(n_channels, 48000, 0, 2048, 1, m, &cfg, NULL, 0);
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  for (i = 0; i < n_threads; i++) {
+    jobs[i].pipes = pipes;
+    jobs[i].pcm = pcm;
+    jobs[i].s0 = (int)((long)n_streams * i / n_threads);
+    jobs[i].s1 = (int)((long)n_streams * (i + 1) / n_threads);
+    jobs[i].n_channels = n_channels;
+    jobs[i].n_samples = n_samples;
+    jobs[i].chunk = chunk;
+    pthread_create(&th[i], NULL, pipe_worker, &jobs[i]);
+  }
+  for (i = 0; i < n_threads; i++) pthread_join(th[i], NULL);
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  for (i = 0; i < n_streams; i++) {
+    if (counts && ora_pipeline_denoiser(pipes[i])) ora_rnnoise_counts(ora_pipeline_denoiser(pipes[i]), counts);
+    ora_pipeline_destroy(pipes[i]);
+  }
+  free(pipes);
+  return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}

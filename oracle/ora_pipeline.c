@@ -516,3 +516,5 @@ size_t ora_pipeline_segments(const ora_pipeline *p, int alt_idx, ora_segment *ou
   for (i = 0; i < m->n_segs && i < cap; i++) out[i] = m->segs[i];
   return m->n_segs;
 }
+
+const ora_denoise *ora_pipeline_denoiser(const ora_pipeline *p) { return p->use_denoiser ? p->den : NULL; }

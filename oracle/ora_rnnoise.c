@@ -601,7 +601,7 @@ static void find_best_pitch(const float *xcorr, const float *y, int len, int max
   }
 }
 
-static void pitch_search(const float *x_lp, const float *y, int len, int max_pitch, int *pitch) {
+static void pitch_search(const float *x_lp, const float *y, int len, int max_pitch, int *pitch, int *n_fine) {
   int i, j, lag, offset;
   int best_pitch[2] = {0, 0};
   float x_lp4[PITCH_FRAME_SIZE >> 2];
@@ -617,6 +617,7 @@ static void pitch_search(const float *x_lp, const float *y, int len, int max_pit
     xcorr[i] = 0;
     if (abs(i - 2 * best_pitch[0]) > 2 && abs(i - 2 * best_pitch[1]) > 2) continue;
     sum = inner_prod(x_lp, y + i, len >> 1);
+    (*n_fine)++;
     xcorr[i] = (-1 > sum) ? -1 : sum;
   }
   find_best_pitch(xcorr, y, len >> 1, max_pitch >> 1, best_pitch);
@@ -641,7 +642,7 @@ static float compute_pitch_gain(float xy, float xx, float yy) {
 static const int second_check[16] = {0, 0, 3, 2, 3, 2, 5, 2, 3, 2, 3, 2, 5, 2, 3, 2};
 
 static float remove_doubling(const float *x, int maxperiod, int minperiod, int N, int *T0_,
-                             int prev_period, float prev_gain) {
+                             int prev_period, float prev_gain, int *n_cand) {
   int k, i, T, T0, offset, minperiod0 = minperiod;
   float g, g0, pg, xy, xx, yy, xy2, best_xy, best_yy;
   float xcorr[3];
@@ -670,6 +671,7 @@ static float remove_doubling(const float *x, int maxperiod, int minperiod, int N
     float g1, cont = 0, thresh;
     T1 = (int)((unsigned)(2 * T0 + k) / (unsigned)(2 * k));
     if (T1 < minperiod) break;
+    (*n_cand)++;
     if (k == 2) {
       if (T1 + T0 > maxperiod)
         T1b = T0;
@@ -813,6 +815,8 @@ struct ora_denoise {
   /* debug */
   int dbg_pitch, dbg_silence;
   float dbg_gain, dbg_features[NB_FEATURES];
+  /* work counters (instrumented op count, ora_rnnoise_counts) */
+  uint64_t n_frames, n_silent, n_fine_lags, n_rd_cands;
 };
 
 ora_denoise *ora_rnnoise_create(const ora_model *m) {
@@ -825,6 +829,12 @@ ora_denoise *ora_rnnoise_create(const ora_model *m) {
 void ora_rnnoise_destroy(ora_denoise *st) { free(st); }
 int ora_rnnoise_get_frame_size(void) { return FRAME_SIZE; }
 void ora_rnnoise_set_bypass(ora_denoise *st, int bypass) { st->bypass = bypass; }
+void ora_rnnoise_counts(const ora_denoise *st, uint64_t *counts) {
+  counts[0] += st->n_frames;
+  counts[1] += st->n_silent;
+  counts[2] += st->n_fine_lags;
+  counts[3] += st->n_rd_cands;
+}
 void ora_rnnoise_debug(const ora_denoise *st, int *pitch, float *gain, int *silence, float *f) {
   if (pitch) *pitch = st->dbg_pitch;
   if (gain) *gain = st->dbg_gain;
@@ -860,11 +870,19 @@ static int compute_frame_features(ora_denoise *st, cpx *X, cpx *P, float *Ex, fl
   memmove(st->pitch_buf, &st->pitch_buf[FRAME_SIZE], (PITCH_BUF_SIZE - FRAME_SIZE) * sizeof(float));
   memcpy(&st->pitch_buf[PITCH_BUF_SIZE - FRAME_SIZE], in, FRAME_SIZE * sizeof(float));
   pitch_downsample(st->pitch_buf, pitch_buf, PITCH_BUF_SIZE);
-  pitch_search(pitch_buf + (PITCH_MAX_PERIOD >> 1), pitch_buf, PITCH_FRAME_SIZE,
-               PITCH_MAX_PERIOD - 3 * PITCH_MIN_PERIOD, &pitch_index);
+  {
+    int n_fine = 0;
+    pitch_search(pitch_buf + (PITCH_MAX_PERIOD >> 1), pitch_buf, PITCH_FRAME_SIZE,
+                 PITCH_MAX_PERIOD - 3 * PITCH_MIN_PERIOD, &pitch_index, &n_fine);
+    st->n_fine_lags += (uint64_t)n_fine;
+  }
   pitch_index = PITCH_MAX_PERIOD - pitch_index;
-  gain = remove_doubling(pitch_buf, PITCH_MAX_PERIOD, PITCH_MIN_PERIOD, PITCH_FRAME_SIZE,
-                         &pitch_index, st->last_period, st->last_gain);
+  {
+    int n_cand = 0;
+    gain = remove_doubling(pitch_buf, PITCH_MAX_PERIOD, PITCH_MIN_PERIOD, PITCH_FRAME_SIZE,
+                           &pitch_index, st->last_period, st->last_gain, &n_cand);
+    st->n_rd_cands += (uint64_t)n_cand;
+  }
   st->last_period = pitch_index;
   st->last_gain = gain;
   st->dbg_pitch = pitch_index;
@@ -1019,6 +1037,8 @@ float ora_rnnoise_process_frame(ora_denoise *st, float *out, const float *in) {
   biquad(x, st->mem_hp_x, in, b_hp, a_hp, FRAME_SIZE);
   silence = compute_frame_features(st, X, P, Ex, Ep, Exp, features, x);
   st->dbg_silence = silence;
+  st->n_frames++;
+  st->n_silent += (uint64_t)silence;
   memcpy(st->dbg_features, features, sizeof(features));
   if (st->bypass) {
     /* weight-free KAT hook: unit gains, no pitch filter */

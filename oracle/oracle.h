@@ -78,6 +78,10 @@ int ora_rnnoise_get_frame_size(void);
 float ora_rnnoise_process_frame(ora_denoise *st, float *out, const float *in);
 /* test hook: 1 = force gains to 1 and skip the RNN / pitch filter (weight-free KAT) */
 void ora_rnnoise_set_bypass(ora_denoise *st, int bypass);
+/* instrumented work counts, added into counts[4]: frames, silent frames (E < 0.04:
+ * no GRU, pitch filter or gains), fine-search lags computed, remove_doubling
+ * candidates evaluated (the loop's break at T1 < minperiod) */
+void ora_rnnoise_counts(const ora_denoise *st, uint64_t *counts);
 /* debug: last frame's pitch index and gain, silence flag, features */
 void ora_rnnoise_debug(const ora_denoise *st, int *pitch, float *gain, int *silence, float *features);
 
@@ -192,6 +196,18 @@ long ora_parse_audacity(const char *txt, size_t len, float *from_to, size_t cap)
  * Returns seconds elapsed. */
 double ora_bench_denoise(const ora_model *m, const float *pcm, int n_streams, int n_channels,
                          int n_frames, int n_threads, float *vad_out);
+/* The whole per-stream path the GPU bench times: AudioPipeline.pushSamples ->
+ * VAD (rnnoise, re-block, FFT B band sums) -> VADMachine (default config), one
+ * pipeline per stream, pushed in chunks of `chunk` samples per channel.
+ * pcm: planar [stream][ch][n_samples] in [-1, 1].  Pipelines are created
+ * before and destroyed after the timed region; n_threads workers take
+ * contiguous stream ranges (simulator.zig:217-228 runs a thread per
+ * instance).  Returns seconds of the timed region; counts (nullable, [4]) as
+ * ora_rnnoise_counts summed over the streams. */
+double ora_bench_pipeline(const ora_model *m, const float *pcm, int n_streams, int n_channels,
+                          size_t n_samples, size_t chunk, int n_threads, uint64_t *counts);
+/* the rnnoise state of a pipeline (NULL without the denoiser) */
+const ora_denoise *ora_pipeline_denoiser(const ora_pipeline *p);
 
 #ifdef __cplusplus
 }

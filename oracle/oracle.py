@@ -367,3 +367,48 @@ def bench_denoise(model, pcm, n_threads=1, want_vad=False):
     secs = lib().ora_bench_denoise(model.h, fptr(pcm), S, Ch, T, n_threads,
                                    fptr(vad) if want_vad else None)
     return secs, vad
+
+
+def _bench_lib(path):
+    L = C.CDLL(path)
+    L.ora_bench_pipeline.restype = C.c_double
+    L.ora_bench_pipeline.argtypes = [C.c_void_p, F32P, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_int,
+                                     C.POINTER(C.c_uint64)]
+    L.ora_model_synthetic.restype = C.c_void_p
+    L.ora_model_synthetic.argtypes = [C.c_uint64]
+    L.ora_model_free.argtypes = [C.c_void_p]
+    return L
+
+
+def native_lib():
+    """The -O3 -march=native flavour of the restatement for the CPU baseline,
+    built on the host that runs it (tag = this host's CPU model)."""
+    import hashlib
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    tag = hashlib.sha1(model.encode()).hexdigest()[:10]
+    out = os.path.join(_HERE, "_build", "liboracle_native_%s.so" % tag)
+    subprocess.check_call(["make", "-s", "-C", _HERE, "native", "NATIVE_OUT=_build/" + os.path.basename(out)])
+    return _bench_lib(out), model
+
+
+def bench_pipeline(pcm, chunk=24000, n_threads=1, seed=1, L=None):
+    """pcm: [streams][ch][n] float32 in [-1, 1].  Runs the whole per-stream path
+    (ora_bench_pipeline).  Returns (seconds, counts{frames, silent, fine_lags,
+    rd_cands})."""
+    L = L or _bench_lib(_LIB_PATH)
+    pcm = np.ascontiguousarray(pcm, np.float32)
+    S, Ch, n = pcm.shape
+    m = L.ora_model_synthetic(seed)
+    cnt = (C.c_uint64 * 4)()
+    try:
+        secs = L.ora_bench_pipeline(m, fptr(pcm), S, Ch, n, chunk, n_threads, cnt)
+    finally:
+        L.ora_model_free(m)
+    if secs < 0:
+        raise ValueError("ora_bench_pipeline: bad arguments")
+    return secs, dict(zip(("frames", "silent", "fine_lags", "rd_cands"), [int(c) for c in cnt]))

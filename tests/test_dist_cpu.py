@@ -52,3 +52,23 @@ def test_two_rank_partition_and_timing():
         assert w == 2 and mx == 2.0
         assert parts == [[0, 2048], [2048, 4096]]  # disjoint, contiguous stream ids
         assert rate == pytest.approx(2048 * 2 * 50 * 2 * 10 / 2.0)
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` outside torch.distributed.run re-launches itself as
+    two ranks (child torch.distributed.run on 127.0.0.1); --cpu-stub swaps the
+    engine for a CPU stub so the launcher, partition, barrier and max-reduce
+    run here on gloo.  Rank 1 sleeps longer: the reported time is the max."""
+    import json
+    import subprocess
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-stub",
+                          "--steps", "4", "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # one JSON line, from rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert d["ms_per_step"] >= 20.0  # rank 1's 20 ms per step, not rank 0's 10
+    assert d["value"] == pytest.approx(2048 * 2 * 50 * 2 / (d["ms_per_step"] / 1000.0), rel=1e-6)

@@ -123,3 +123,24 @@ def test_engine_fails_loudly_without_gpu(fvad_mod):
         pytest.skip("GPU present")
     with pytest.raises(fvad_mod.FvadError):
         fvad_mod.Engine(fvad_mod.Model(seed=1), 2)
+
+
+def test_instrumented_counts_match_cost_model(fvad_mod, oracle_mod):
+    """fvad/cost.py MEASURED is what tests/count_ops.py counts on the bench
+    input (fine-search lags, remove_doubling candidates, silent frames)."""
+    import count_ops
+    from fvad import cost
+    got = count_ops.count(threads=8)
+    for k, v in cost.MEASURED.items():
+        assert got[k] == pytest.approx(v, abs=1e-4), k
+
+
+def test_cpu_baseline_native_build_same_work(oracle_mod, fvad_mod):
+    """The -O3 -march=native CPU-baseline flavour runs the same algorithm:
+    identical work counts on the same input."""
+    import numpy as np
+    L, _ = oracle_mod.native_lib()
+    pcm = np.stack([fvad_mod.synth_stream(s, 48000, 2)[0] for s in (0, 19)])
+    _, a = oracle_mod.bench_pipeline(pcm, chunk=24000, n_threads=2)
+    _, b = oracle_mod.bench_pipeline(pcm, chunk=24000, n_threads=2, L=L)
+    assert a == b and a["frames"] == 2 * 100 * 2
