@@ -142,8 +142,9 @@ def test_full_size_bench_config_parity(fvad_mod, oracle_mod, models):
     late = np.zeros((2, T, B, 2, FRAME), np.float32)
     xs = []
     for s in range(B):
+        x0 = fvad_mod.synth_stream(s, n, 2)[0]  # what load_synthetic generated (the generator depends on the length)
         x = fvad_mod.synth_stream(s, 6 * 48000, 2)[0]
-        xs.append(np.concatenate([x[:, :n], x[:, :n], x[:, 5 * 48000:6 * 48000]], axis=1))
+        xs.append(np.concatenate([x0, x0, x[:, 5 * 48000:6 * 48000]], axis=1))
         late[:, :, s] = x[:, 5 * 48000:6 * 48000].reshape(2, 2, T, FRAME).transpose(1, 2, 0, 3)
     eng.submit(late[0])
     eng.submit(late[1])
