@@ -51,14 +51,16 @@ def parse():
     ap.add_argument("--streams-per-gpu", type=int, default=2048)
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--ticks", type=int, default=50)
-    ap.add_argument("--mode", choices=("staged", "fused"), default="staged")
+    ap.add_argument("--mode", choices=("staged", "fused", "fp16"), default="staged",
+                    help="staged (bit-exact, default), fused (bit-exact), fp16 (configs[4]: GRU on MFMA, tolerance)")
     ap.add_argument("--no-vadm", action="store_true", help="staged: do not run the device VADMachine (k_vadm)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on this host (rank 0)")
     ap.add_argument("--cpu-streams", type=int, default=64)
     ap.add_argument("--cpu-ticks", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="measure each CPU sample (single-core, all-core) for about this long")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-json", default=None,
+                    help="PMC byte counts (tools/profile.sh); default profiles/pmc_traffic[_<mode>].json")
     ap.add_argument("--host-rate", type=int, default=1,
                     help="also time pushes from host buffers (PCIe-inclusive; reported as host_buffers, never value)")
     ap.add_argument("--cpu-stub", action="store_true",
@@ -273,6 +275,9 @@ def host_rate(eng, args, rank, dist, torch):
 
 def main():
     args = parse()
+    if args.pmc_json is None:
+        args.pmc_json = os.path.join(ROOT, "profiles", "pmc_traffic%s.json" % ("" if args.mode == "staged" else
+                                                                             "_" + args.mode))
     maybe_spawn(args)
     if args.cpu_stub:
         return stub_main(args)
@@ -283,7 +288,7 @@ def main():
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     model = fvad.Model(seed=1)
     eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=args.mode)
-    if args.mode == "staged" and not args.no_vadm:
+    if args.mode != "fused" and not args.no_vadm:
         eng.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
     base, _ = stream_partition(rank, B)
     eng.load_synthetic(T, base=base)
@@ -401,13 +406,16 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f32" if args.mode != "fp16" else "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
+        "data": "synthetic",
         "config": {"workload": "configs[4] per-GPU partition: %d synthetic 48 kHz streams x %d ch per GPU "
-                               "(%d at %d GPU), %d ticks (480 samples/ch) per step, fp32 weights, bit-exact path"
-                               % (B, Ch, B * world, world, T),
+                               "(%d at %d GPU), %d ticks (480 samples/ch) per step, %s"
+                               % (B, Ch, B * world, world, T,
+                                  "fp16 GRU weights on MFMA (configs[4] variant, tolerance parity)" if args.mode == "fp16"
+                                  else "fp32 weights, bit-exact path"),
                    "streams_per_gpu": B, "channels": Ch, "ticks_per_step": T, "fft_size": 2048,
                    "parallelism": "stream-partition x%d (no collectives)" % world, "mode": args.mode,
-                   "vad_machine": "device" if (args.mode == "staged" and not args.no_vadm) else "none"},
+                   "vad_machine": "device" if (args.mode != "fused" and not args.no_vadm) else "none"},
         "realtime_streams": round(value / (100.0 * Ch), 1),
         "roofline": roofline,
         "cpu_baseline": cpu,

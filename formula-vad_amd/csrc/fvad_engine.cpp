@@ -68,6 +68,8 @@ struct fvad_engine {
   int *d_sil = nullptr, *d_pitch = nullptr, *d_wtick = nullptr;
   float *d_gr = nullptr, *d_gs = nullptr;
   int8_t *d_rnn_img = nullptr;
+  uint16_t *d_gru16 = nullptr;  // FVAD_MODE_FP16: MFMA weight fragments (f16 bits)
+  float *d_gru16_bias = nullptr;
   // device VADMachines (fvad_engine_attach_vadm)
   fvad::VadmArgs vadm{};
   // k_vadm_hbm runs on a side stream over copies of one push's window outputs,
@@ -261,6 +263,14 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
     rc = dalloc(&e->d_rnn_img, img.size());
     if (rc) return rc;
     HIP_TRY(hipMemcpy(e->d_rnn_img, img.data(), img.size(), hipMemcpyHostToDevice));
+    if (e->cfg.mode == FVAD_MODE_FP16) {  // MFMA fragments of the same image (fvad_gru16.hip)
+      std::vector<uint16_t> frags((size_t)fvad::gru16_frag_count() * 64 * 8);
+      std::vector<float> bias(fvad::gru16_bias_rows());
+      fvad::gru16_build(img.data(), frags.data(), bias.data());
+      if ((rc = dalloc(&e->d_gru16, frags.size())) || (rc = dalloc(&e->d_gru16_bias, bias.size()))) return rc;
+      HIP_TRY(hipMemcpy(e->d_gru16, frags.data(), frags.size() * 2, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(e->d_gru16_bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
+    }
   }
   e->dmodel.in_dense = dense(0);
   e->dmodel.vad = gru(1);
@@ -281,7 +291,7 @@ void free_all(fvad_engine *e) {
                   e->band_b[0] ? e->band_b[0] : e->d_band, e->d_den,   e->wflag_b[0] ? e->wflag_b[0] : e->d_wflag,
                   e->d_model, e->d_stamps, e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
-                  e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->vadm.st, e->vadm.buf,
+                  e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->d_gru16, e->d_gru16_bias, e->vadm.st, e->vadm.buf,
                   e->vadm.seg, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -353,7 +363,8 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     hi = std::max(hi, c.band_hi[b]);
   }
   if (hi - lo + 1 > 256) return fail(FVAD_EINVAL, "reported bins must span <= 256");
-  if (c.mode != FVAD_MODE_STAGED && c.mode != FVAD_MODE_FUSED) return fail(FVAD_EINVAL, "unknown engine mode");
+  if (c.mode != FVAD_MODE_STAGED && c.mode != FVAD_MODE_FUSED && c.mode != FVAD_MODE_FP16)
+    return fail(FVAD_EINVAL, "unknown engine mode");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FVAD_EDEVICE, "no HIP device available");
   if (c.device < 0 || c.device >= ndev) return fail(FVAD_EDEVICE, "device ordinal out of range");
@@ -363,9 +374,9 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   // the staged path writes every tick of a push before FFT B reads its
   // windows, so the ring holds one window plus a whole push
   e->ring_len = c.fft_size + c.max_ticks * fvad::kFrame;
-  e->n_kernels = c.mode == FVAD_MODE_STAGED ? fvad::kStagedKernels : 2;
-  e->n_events = c.mode == FVAD_MODE_STAGED ? fvad::kStagedEvents : 3;
-  e->last_event = c.mode == FVAD_MODE_STAGED ? fvad::kStagedLast : 2;
+  e->n_kernels = c.mode != FVAD_MODE_FUSED ? fvad::kStagedKernels : 2;
+  e->n_events = c.mode != FVAD_MODE_FUSED ? fvad::kStagedEvents : 3;
+  e->last_event = c.mode != FVAD_MODE_FUSED ? fvad::kStagedLast : 2;
   static_assert(fvad::kStagedEvents <= FVAD_MAX_TIMES, "timing events");
   auto bail = [&](int rc) {
     free_all(e);
@@ -375,7 +386,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   if (hipSetDevice(c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipSetDevice failed"));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
-  if (c.mode == FVAD_MODE_STAGED &&
+  if (c.mode != FVAD_MODE_FUSED &&
       (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -553,6 +564,8 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.gr = e->d_gr;
   a.gs = e->d_gs;
   a.rnn_img = e->d_rnn_img;
+  a.gru16_frags = e->d_gru16;
+  a.gru16_bias = e->d_gru16_bias;
   for (int m = 0; m < fvad::rnnimg::kMats; m++) a.rnn_act[m] = e->rnn_act[m];
   a.ys = e->d_ys;
   a.ring = e->d_ring;
@@ -640,7 +653,7 @@ int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
 int collect_slot(fvad_engine *e, int slot) {
   if (!e->slot_pending[slot]) return FVAD_OK;
   hipEvent_t *ev = e->evs[slot];
-  const bool staged = e->cfg.mode == FVAD_MODE_STAGED;
+  const bool staged = e->cfg.mode != FVAD_MODE_FUSED;
   HIP_TRY(hipEventSynchronize(ev[e->last_event]));
   for (int i = 0; i < e->n_kernels; i++) {
     float ms = 0;
@@ -713,7 +726,7 @@ int input_buffer(fvad_engine *e, hipStream_t cs) {
 // after the launch: the buffer is free again once this push's prep read it
 int release_input(fvad_engine *e) {
   const int ib = e->in_next;
-  HIP_TRY(hipEventRecord(e->ev_in_free[ib], e->cfg.mode == FVAD_MODE_STAGED ? e->pstream : e->stream));
+  HIP_TRY(hipEventRecord(e->ev_in_free[ib], e->cfg.mode != FVAD_MODE_FUSED ? e->pstream : e->stream));
   e->in_busy[ib] = true;
   e->in_next = ib ^ 1;
   e->resident_ticks = 0;
@@ -788,7 +801,7 @@ extern "C" int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, c
   // once push k-2 finished)
   hipStream_t cs = e->stream;
   int *dticks = e->d_ticks;
-  if (e->cfg.mode == FVAD_MODE_STAGED) {
+  if (e->cfg.mode != FVAD_MODE_FUSED) {
     const int b = e->next_buf;
     if (e->buf_busy[b]) HIP_TRY(hipStreamWaitEvent(e->pstream, e->ev_buf_free[b], 0));
     cs = e->pstream;
@@ -841,7 +854,7 @@ extern "C" int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks,
   // staged: copies on the copy stream, overlapping the previous push's
   // kernels; the prep stream waits for them.  Fused: everything in order on
   // the engine stream (its kernels read d_ticks in place).
-  const bool staged = c.mode == FVAD_MODE_STAGED;
+  const bool staged = c.mode != FVAD_MODE_FUSED;
   hipStream_t cs = staged ? e->cstream : e->stream;
   if ((rc = input_buffer(e, cs))) return rc;
   HIP_TRY(hipMemcpyAsync(e->d_pcm, sl.in, bytes, hipMemcpyHostToDevice, cs));
@@ -955,7 +968,7 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
   }();
   if ((rc = launch(e, n_ticks, false, !no_events))) return rc;
   // a later submit / push must not overwrite buffer 0 under this run's prep
-  HIP_TRY(hipEventRecord(e->ev_in_free[0], e->cfg.mode == FVAD_MODE_STAGED ? e->pstream : e->stream));
+  HIP_TRY(hipEventRecord(e->ev_in_free[0], e->cfg.mode != FVAD_MODE_FUSED ? e->pstream : e->stream));
   e->in_busy[0] = true;
   return FVAD_OK;
 }
@@ -1010,6 +1023,7 @@ extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
   if (e && i == e->n_kernels && e->vadm.n > 0) return "k_vadm_hbm";
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
   if (e->cfg.mode == FVAD_MODE_FUSED) return i == 0 ? "k_prep" : "k_frame";
+  if (e->cfg.mode == FVAD_MODE_FP16 && i == 6) return "k_gru16";
   return fvad::staged_kernel_name(i);
 }
 
@@ -1036,7 +1050,7 @@ int vadm_reset(fvad_engine *e) {
 
 extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *cfgs, int n, int seg_capacity) {
   if (!e || !cfgs || n < 1 || n > FVAD_MAX_BANDS || seg_capacity < 1) return fail(FVAD_EINVAL, "invalid argument");
-  if (e->cfg.mode != FVAD_MODE_STAGED) return fail(FVAD_EINVAL, "device VADMachines need the staged engine");
+  if (e->cfg.mode == FVAD_MODE_FUSED) return fail(FVAD_EINVAL, "device VADMachines need the staged engine");
   if (e->vadm.n > 0) return fail(FVAD_EINVAL, "VADMachines already attached");
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int B = e->cfg.n_streams;

@@ -77,6 +77,8 @@ struct StagedArgs {
   float *vadf;             // [f] per-frame vad probability
   float *gr, *gs;          // [f][22] GRU gains g and smoothed gains max(g, .6*lastg)
   const int8_t *rnn_img;   // rnnimg image (fvad_internal.h), device
+  const void *gru16_frags;   // FVAD_MODE_FP16: MFMA A fragments (fvad_gru16.hip), null otherwise
+  const float *gru16_bias;   //   and the gate biases per tile row
   int rnn_act[rnnimg::kMats];  // activation of each image matrix
   float *ys;               // [f][960] windowed synthesis output
   float *ring;             // [s][c][ring_len]
@@ -128,5 +130,10 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
 // Device VADMachines over the window outputs a.out_* of one push: overlap =
 // the light HBM variant meant to co-run with the next push on a side stream.
 hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream);
+// fp16 / MFMA recurrence (fvad_gru16.hip), run in k_rnn3's place when a.gru16_frags is set
+hipError_t launch_gru16(const StagedArgs &a, hipStream_t stream);
+int gru16_frag_count();   // A fragments of 64 lanes x 8 f16
+int gru16_bias_rows();
+void gru16_build(const int8_t *rnn_img, uint16_t *frags, float *bias);
 
 }  // namespace fvad

@@ -1571,7 +1571,10 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   REC(7);
   FVAD_LAUNCH_TRY(launch_wave(kWavePspec, a, n_cu, stream));
   REC(8);
-  FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
+  if (a.gru16_frags)  // FVAD_MODE_FP16: the GRU stack on the matrix cores (configs[4])
+    FVAD_LAUNCH_TRY(launch_gru16(a, stream));
+  else
+    FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
   REC(9);
   FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
   REC(10);

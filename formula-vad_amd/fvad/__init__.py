@@ -38,7 +38,7 @@ class EngineConfig(C.Structure):
                 ("mode", C.c_int)]
 
 
-MODE_STAGED, MODE_FUSED = 0, 1
+MODE_STAGED, MODE_FUSED, MODE_FP16 = 0, 1, 2
 MAX_TIMES = 16
 
 
@@ -233,7 +233,7 @@ class Engine:
             cfg.band_lo[i] = lo
             cfg.band_hi[i] = hi
         cfg.want_denoised = int(want_denoised)
-        cfg.mode = {"staged": MODE_STAGED, "fused": MODE_FUSED}[mode]
+        cfg.mode = {"staged": MODE_STAGED, "fused": MODE_FUSED, "fp16": MODE_FP16}[mode]
         self.cfg = cfg
         self.model = model
         h = C.c_void_p()

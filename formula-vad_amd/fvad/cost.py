@@ -159,6 +159,7 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_fftb": (p["re-block + FFT B share"], 480 * 4 + 4),
         "k_vadm_hbm": (p["VADMachine share"], (4218 + 4 + 11 + 2) * 4 * FRAME / fft_size / C + 16),
     }
+    k["k_gru16"] = k["k_rnn3"]  # FVAD_MODE_FP16: the same recurrence, gate sums on MFMA
     return {n: {"flops": f, "bytes": b} for n, (f, b) in k.items()}
 
 

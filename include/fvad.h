@@ -109,13 +109,18 @@ typedef struct {
   int band_lo[FVAD_MAX_BANDS]; /* inclusive FFT-B bin ranges (FFT.freqToBin) */
   int band_hi[FVAD_MAX_BANDS];
   int want_denoised;    /* keep denoised PCM (VAD.zig temp_denoiser_segment) */
-  int mode;             /* FVAD_MODE_STAGED (default) or FVAD_MODE_FUSED; identical results */
+  int mode;             /* FVAD_MODE_STAGED (default), FVAD_MODE_FUSED or FVAD_MODE_FP16 */
 } fvad_engine_config;
 
 /* staged: time-parallel frame kernels + a thin per-stream recurrence kernel;
- * fused: one workgroup runs every frame of a stream (lower memory). */
+ * fused: one workgroup runs every frame of a stream (lower memory); staged
+ * and fused give identical results (bit-exact with the CPU reference).
+ * fp16: BASELINE configs[4] -- the staged pipeline with the GRU stack on the
+ * matrix cores (int8 weights as f16, f16 inputs, f32 accumulation): within
+ * the stated tolerance (vad |d| <= 2e-2), not bit-exact. */
 #define FVAD_MODE_STAGED 0
 #define FVAD_MODE_FUSED 1
+#define FVAD_MODE_FP16 2
 #define FVAD_MAX_TIMES 16
 
 void fvad_engine_config_default(fvad_engine_config *cfg, int n_streams, int n_channels);

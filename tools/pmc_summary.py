@@ -2,7 +2,7 @@
 """Summarise a tools/profile.sh run into profiles/.
 
 - profiles/<tag>_kernel_stats.csv : rocprofv3 --stats summary (trace pass)
-- profiles/pmc_traffic.json       : per-kernel HBM bytes per launch from the
+- profiles/pmc_traffic[_<mode>].json : per-kernel HBM bytes per launch from the
   FETCH_SIZE and WRITE_SIZE passes (kilobytes in rocprofv3), corrected as
   MI355X_MICROARCH.md prescribes for gfx950: FETCH_SIZE counts 128-B memory
   requests at 64 B, so it is doubled; WRITE_SIZE is taken as is.
@@ -90,7 +90,8 @@ def main():
         res["fetch_kb_raw"][k] = fa
         res["write_kb_raw"][k] = wa
         res["bytes_per_launch"][k] = (2 * fa + wa) * 1024.0
-    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
+    name = "pmc_traffic.json" if cfg["mode"] == "staged" else "pmc_traffic_%s.json" % cfg["mode"]
+    with open(os.path.join(ROOT, "profiles", name), "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
 
