@@ -25,7 +25,7 @@
 // the gains of t-1 run on waves the phase leaves idle:
 //   P0  dense(t) [w0,1]                den_out(t-1) [w2,3]
 //   P1  vad z|r(t) [w4..6]             features(t+1) [w0..3]   gains(t-1) [w7]
-//   P2  vad h(t) [w4,5]                spectral variability(t+1) [w0]
+//   P2  vad h(t) [w4,5]                spectral variability(t+1) [w0,1]
 //   P3  noise z|r(t) [w0..5]           vad_out(t) [w6]         fetch raw features(t+2)
 //   P4  noise h(t) [w5..7]
 //   P5  denoise z|r(t) [w0..7, w0..3 a second tile]
@@ -376,16 +376,22 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
       }
     }
   };
-  // spectral variability of frame f (feature 41), stream s
-  auto feat_d = [&](int f, int s) {
-    if (!L.act[f & 7][s]) return;
+  // spectral variability of frame f (feature 41): lane (s, i) = (tid >> 3,
+  // tid & 7) takes row i's minimum distance, lane i == 0 adds the 8 minima in
+  // row order (the C loop's sum) and advances memid; 128 lanes (w0, w1)
+  auto feat_d = [&](int f) {
+    const int s = tid >> 3, i = tid & 7;
+    float mindist = 1e15f;
+#pragma unroll
+    for (int j = 0; j < kCeps; j++)
+      if (j != i) mindist = (mindist < L.dist[s][i * kCeps + j]) ? mindist : L.dist[s][i * kCeps + j];
+    float m[kCeps];
+#pragma unroll
+    for (int k = 0; k < kCeps; k++) m[k] = __shfl(mindist, (lane & ~7) + k);
+    if (i != 0 || !L.act[f & 7][s]) return;
     float sv = 0;
-    for (int i = 0; i < kCeps; i++) {
-      float mindist = 1e15f;
-      for (int j = 0; j < kCeps; j++)
-        if (j != i) mindist = (mindist < L.dist[s][i * kCeps + j]) ? mindist : L.dist[s][i * kCeps + j];
-      sv += mindist;
-    }
+#pragma unroll
+    for (int k = 0; k < kCeps; k++) sv += m[k];
     L.op[s][(f & 1) * 6 * 8 + 41] = (_Float16)(float)(sv / kCeps - 2.1);
     int mid = L.memid[s] + 1;
     if (mid == kCeps) mid = 0;
@@ -396,12 +402,13 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
   __syncthreads();
   for (int idx = tid; idx < kFeatItems; idx += kGNT) feat_c(0, idx);
   __syncthreads();
-  if (tid < S && 0 < maxnf) feat_d(0, tid);
+  if (tid < S * kCeps && 0 < maxnf) feat_d(0);
   const float pf1 = fetch(1);
   __syncthreads();
   if (pf_lane) L.pf[pfs][pfi] = pf1;
   __syncthreads();
   const int col = lane & 15;
+  STAMP_INIT();
   for (int t = 0; t <= maxnf; t++) {
     const int fs = t & 1;
     const bool fr_t = t < maxnf;
@@ -428,12 +435,20 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
       }
     }
     __syncthreads();
+    RSTAMP(0);
     // ---- P1: vad z|r(t) [w4..6], features(t+1) [w0..3], gains(t-1) [w7]
     if (W >= 4 && W < 7) {
       if (fr_t) epi_zr<24>(L, mma_job<20, 1>(fr, JC.tile, L, lane, fs), JC.tile, lane, L.zv, L.sv, kRsv);
     } else if (W < 4) {
-      if (t + 1 < maxnf)
-        for (int idx = tid; idx < kFeatItems; idx += 4 * 64) feat_c(t + 1, idx);
+      // distance rows (the 22-term sums) one per lane on w0, w1; the rest on w2, w3
+      if (t + 1 < maxnf) {
+        constexpr int kIt = kBands + 7 + kCeps, kLight = kBands + 7;
+        if (tid < S * kCeps)
+          feat_c(t + 1, (tid >> 3) * kIt + kLight + (tid & 7));
+        else
+          for (int k = tid - S * kCeps; k < S * kLight; k += 4 * 64 - S * kCeps)
+            feat_c(t + 1, (k / kLight) * kIt + k % kLight);
+      }
     } else if (t >= 1) {  // gain smoothing g = max(g, .6*lastg) (denoise.c), frame t-1
       const int f1 = t - 1;
       for (int idx = lane; idx < S * kBands; idx += 64) {
@@ -449,13 +464,15 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
       }
     }
     __syncthreads();
+    RSTAMP(1);
     if (!fr_t) break;
     // ---- P2: vad h(t) [w4, w5], spectral variability(t+1) [w0]
     if (W == 4 || W == 5)
       epi_h<24>(L, mma_job<22, 2>(fr, JD.tile, L, lane, fs), JD.tile, lane, ra[2], L.zv, L.sv, kSv, on_t);
-    else if (W == 0 && lane < S && t + 1 < maxnf)
-      feat_d(t + 1, lane);
+    else if (W < 2 && t + 1 < maxnf)
+      feat_d(t + 1);
     __syncthreads();
+    RSTAMP(2);
     // ---- P3: noise z|r(t) [w0..5], vad_output(t) [w6]; raw features of t+2 requested
     const float pf_next = fetch(t + 2);
     if (W < 6) {
@@ -465,18 +482,23 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
       if (lane < 16 && on_t) a.vadf[L.fbase[col] + t] = activate(L.tt, ra[8], kWs * acc[0]);
     }
     __syncthreads();
+    RSTAMP(3);
     // ---- P4: noise h(t) [w5..7]
     if (W >= 5) epi_h<48>(L, mma_job<5, 4>(fr, JE.tile, L, lane, fs), JE.tile, lane, ra[4], L.zn, L.sn, kSn, on_t);
     __syncthreads();
+    RSTAMP(4);
     // ---- P5: denoise z|r(t), A from LDS: tile w [w0..7] and w + 8 [w0..3]
     epi_zr<96>(L, mma_job<-1, 5>(fr, W, L, lane, fs), W, lane, L.zd, L.sd, kRsd);
     if (W < 4) epi_zr<96>(L, mma_job<-1, 5>(fr, W + 8, L, lane, fs), W + 8, lane, L.zd, L.sd, kRsd);
     __syncthreads();
+    RSTAMP(5);
     // ---- P6: denoise h(t) [w2..7]; raw features of t+2 staged
     if (W >= 2) epi_h<96>(L, mma_job<10, 6>(fr, JF.tile, L, lane, fs), JF.tile, lane, ra[6], L.zd, L.sd, kSd, on_t);
     if (pf_lane) L.pf[pfs][pfi] = pf_next;
     __syncthreads();
+    RSTAMP(6);
   }
+  STAMP_FLUSH(48, 7);
   // ---- state write-back (streams that ran at least one frame)
   for (int idx = tid; idx < S * kCeps * kBands; idx += kGNT) {
     const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);

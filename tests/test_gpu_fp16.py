@@ -22,9 +22,13 @@ import parity_util as pu
 
 pytestmark = pytest.mark.gpu
 
-VAD_ABS = 2e-2
-DEN_RELRMS = 2e-2
-BAND_REL = 2e-2
+# SURVEY.md 8(c) states vad |d| <= 2e-2 for this config; measured on the
+# synthetic set (tools/fp16_diag.py): max |dvad| 6.6e-5, denoised rel-RMS
+# 1.7e-4, band rel 3.0e-4 -- the tests hold the tighter bounds below so a
+# regression shows long before the stated tolerance is reached
+VAD_ABS = 1e-3
+DEN_RELRMS = 2e-3
+BAND_REL = 2e-3
 
 
 @pytest.fixture(scope="module")
@@ -107,7 +111,7 @@ def test_fp16_twenty_streams_evaluator(fvad_mod, oracle_mod, models):
     """configs[2]'s labelled set (20 stereo streams x 120 s) through the fp16
     engine with device VADMachines: segment lists are compared with the oracle's
     and every difference is reported; Evaluator TP/FP/FN (simulator.zig:123-128
-    settings) agree within 1 % of the labelled speech time."""
+    settings).  Measured: identical segment lists and TP/FP/FN."""
     m, _ = models
     secs, ids, T = 120.0, list(range(20)), 100
     streams = [fvad_mod.synth_stream(i, int(48000 * secs), 2)[0] for i in ids]
@@ -140,9 +144,9 @@ def test_fp16_twenty_streams_evaluator(fvad_mod, oracle_mod, models):
         tot["pos"] += so["total_positives_sec"]
     print("fp16 20 x 120 s: %d/20 streams with identical segment bounds; differing bounds: %s" % (same, diffs))
     print("fp16 TP/FP/FN s: %s vs oracle %s (labelled %.1f s)" % (tot["g"], tot["o"], tot["pos"]))
-    assert same >= 18
-    for i in range(3):
-        assert abs(tot["g"][i] - tot["o"][i]) <= 0.01 * tot["pos"], (i, tot)
+    # measured: all 20 segment lists identical and TP/FP/FN equal to the oracle's
+    assert same == 20, diffs
+    assert tot["g"] == tot["o"], tot
 
 
 def test_fp16_resident_bench_shape(fvad_mod, oracle_mod, models):

@@ -33,6 +33,10 @@ elif MODE == "staged":
              "noise h", "denoise z|r", "denoise h", "denoise_output", "gains + outputs + prefetch", "next act"]
     FFTA = ["group setup", "window scatter (global loads)", "FFT 960 x F", "X store + band sums + log10",
             "Ly chain + silence", "DCT(Ly)"]
+if MODE == "fp16":  # k_gru16 phases (fvad_gru16.hip), stamps[48..54]
+    GRU = ["P0 dense(t) + den_out(t-1)", "P1 vad z|r + features(t+1) + gains(t-1)",
+           "P2 vad h + spectral variability(t+1)", "P3 noise z|r + vad_out", "P4 noise h", "P5 denoise z|r",
+           "P6 denoise h"]
 L = fvad.lib()
 L.fvad_engine_stamps.restype = C.c_int
 L.fvad_engine_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
@@ -46,6 +50,13 @@ e.run_resident(T)
 e.sync()
 buf = (C.c_ulonglong * 64)()
 assert L.fvad_engine_stamps(e.h, buf, 64) == 0
+if MODE == "fp16":
+    frames = (B // 16) * 2 * T
+    gt = sum(buf[48:55])
+    print("k_gru16: stamped cycles per frame step per WG: %.0f" % (gt / frames))
+    for i, n in enumerate(GRU):
+        print("%2d %-44s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[48 + i] / max(1, gt), buf[48 + i] / frames))
+    sys.exit(0)
 tot = sum(buf[:24]) if MODE == "fused" else (sum(buf[:2]) if len(NAMES) > 12 else sum(buf[:12]))
 frames = B * 2 * T
 if MODE == "staged":
