@@ -84,25 +84,47 @@ extern "C" float rnnoise_process_frame(DenoiseState *st, float *out, const float
 // Layout: header | twiddles[ncfft] | super[ncfft/2] | perm[ncfft].
 // ---------------------------------------------------------------------------
 struct kiss_fftr_state {
-  int nfft, ncfft, stages, inverse;
+  int nfft, ncfft, nf, inverse;
   uint64_t magic;
+  int fac[2 * fvad::kMaxFactors];  // kf_factor(ncfft): (p, m) pairs
 };
 
 namespace {
 constexpr uint64_t kMagic = 0x4656414446465452ull;  // "FVADFFTR"
 
-size_t cfg_bytes(int ncfft) {
-  return sizeof(kiss_fftr_state) + sizeof(float) * 2 * ncfft + sizeof(float) * 2 * (ncfft / 2) +
-         sizeof(int) * ncfft;
+// cfg memory: header, twiddles [ncfft], super twiddles [ncfft/2], leaf
+// permutation [ncfft] -- the device tables are uploaded from it per call
+size_t tab_floats(int ncfft) { return 2 * (size_t)ncfft + 2 * (size_t)(ncfft / 2) + (size_t)ncfft; }
+size_t cfg_bytes(int ncfft) { return sizeof(kiss_fftr_state) + sizeof(float) * tab_floats(ncfft); }
+
+// kf_factor (kissfft): powers of 4, then 2, then odd primes
+int factor(int n, int *fac) {
+  int p = 4, k = 0;
+  const double floor_sqrt = std::floor(std::sqrt((double)n));
+  do {
+    while (n % p) {
+      switch (p) {
+        case 4: p = 2; break;
+        case 2: p = 3; break;
+        default: p += 2; break;
+      }
+      if (p > floor_sqrt) p = n;
+    }
+    n /= p;
+    fac[2 * k] = p;
+    fac[2 * k + 1] = n;
+    k++;
+  } while (n > 1);
+  return k;
 }
 
-void leaf_perm(int *perm, int out_base, int in_base, int fstride, int n) {
-  // kf_work leaf placement for radix-4-only factorisations
-  const int m = n / 4;
+// kf_work's leaf placement: Fout position -> input index
+void leaf_perm(int *perm, int out_base, int in_base, int fstride, const int *fac) {
+  const int p = fac[0], m = fac[1];
   if (m == 1) {
-    for (int j = 0; j < 4; j++) perm[out_base + j] = in_base + j * fstride;
+    for (int j = 0; j < p; j++) perm[out_base + j] = in_base + j * fstride;
   } else {
-    for (int j = 0; j < 4; j++) leaf_perm(perm, out_base + j * m, in_base + j * fstride, fstride * 4, m);
+    for (int j = 0; j < p; j++) leaf_perm(perm, out_base + j * m, in_base + j * fstride, fstride * p, fac + 2);
   }
 }
 
@@ -115,32 +137,27 @@ struct DevScratch {
 
 }  // namespace
 
+// Same protocol as mborgerding kiss_fftr_alloc (FFT.zig:179-208): with
+// lenmem != NULL the required size is written to *lenmem and the cfg is built
+// in mem only when *lenmem was large enough (mem = NULL, *lenmem = 1 is the
+// size probe: returns NULL).  Any even nfft; forward transforms only.
 extern "C" kiss_fftr_cfg kiss_fftr_alloc(int nfft, int inverse_fft, void *mem, size_t *lenmem) {
   if (nfft <= 0 || (nfft & 1)) return nullptr;
   const int ncfft = nfft / 2;
-  int stages = 0, n = ncfft;
-  while (n > 1 && n % 4 == 0) {
-    n /= 4;
-    stages++;
-  }
-  if (n != 1 || stages < 1 || ncfft > 4096) {  // LDS holds ncfft complex (<= 32 KiB)
-    if (lenmem) *lenmem = 0;
-    return nullptr;  // device path: nfft/2 must be a power of 4
-  }
   const size_t need = cfg_bytes(ncfft);
   kiss_fftr_state *st = nullptr;
   if (lenmem == nullptr) {
     st = (kiss_fftr_state *)std::malloc(need);
   } else {
-    if (*lenmem >= need) st = (kiss_fftr_state *)mem;
+    if (mem != nullptr && *lenmem >= need) st = (kiss_fftr_state *)mem;
     *lenmem = need;
   }
   if (!st) return nullptr;
   st->nfft = nfft;
   st->ncfft = ncfft;
-  st->stages = stages;
   st->inverse = inverse_fft;
   st->magic = kMagic;
+  st->nf = factor(ncfft, st->fac);
   float *tw = reinterpret_cast<float *>(st + 1);
   float *sup = tw + 2 * ncfft;
   int *perm = reinterpret_cast<int *>(sup + 2 * (ncfft / 2));
@@ -157,7 +174,7 @@ extern "C" kiss_fftr_cfg kiss_fftr_alloc(int nfft, int inverse_fft, void *mem, s
     sup[2 * i] = (float)std::cos(phase);
     sup[2 * i + 1] = (float)std::sin(phase);
   }
-  leaf_perm(perm, 0, 0, 1, ncfft);
+  leaf_perm(perm, 0, 0, 1, st->fac);
   return st;
 }
 
@@ -168,8 +185,11 @@ extern "C" void kiss_fftr(kiss_fftr_cfg cfg, const float *timedata, kiss_fft_cpx
   }
   const int nc = cfg->ncfft;
   const float *tw = reinterpret_cast<const float *>(cfg + 1);
-  const size_t tab_floats = 2 * (size_t)nc + 2 * (size_t)(nc / 2) + (size_t)nc;
-  const size_t need = tab_floats + 2 * (size_t)nc + 2 * (size_t)(nc + 1);
+  const size_t tf = tab_floats(nc);
+  // device: tables, factors, input, output, work arrays W + S (used when
+  // they do not fit the kernel's LDS)
+  const size_t fac_floats = 2 * fvad::kMaxFactors;
+  const size_t need = tf + fac_floats + 2 * (size_t)nc + 2 * (size_t)(nc + 1) + 4 * (size_t)nc;
   std::lock_guard<std::mutex> lk(g_mu);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
@@ -187,13 +207,16 @@ extern "C" void kiss_fftr(kiss_fftr_cfg cfg, const float *timedata, kiss_fft_cpx
     g_fft.dev = dev;
   }
   float *d_tab = g_fft.buf;
-  float *d_in = d_tab + tab_floats;
+  int *d_fac = reinterpret_cast<int *>(d_tab + tf);
+  float *d_in = d_tab + tf + fac_floats;
   float *d_out = d_in + 2 * (size_t)nc;
+  float *d_work = d_out + 2 * (size_t)(nc + 1);
   hipStream_t s = g_fft.stream;
-  bool ok = hipMemcpyAsync(d_tab, tw, tab_floats * sizeof(float), hipMemcpyHostToDevice, s) == hipSuccess &&
+  bool ok = hipMemcpyAsync(d_tab, tw, tf * sizeof(float), hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(d_fac, cfg->fac, sizeof(cfg->fac), hipMemcpyHostToDevice, s) == hipSuccess &&
             hipMemcpyAsync(d_in, timedata, 2 * (size_t)nc * sizeof(float), hipMemcpyHostToDevice, s) == hipSuccess &&
-            fvad::launch_kiss_fftr(nc, cfg->stages, d_tab, d_tab + 2 * nc,
-                                   reinterpret_cast<const int *>(d_tab + 2 * nc + 2 * (nc / 2)), d_in, d_out,
+            fvad::launch_kiss_fftr(nc, d_fac, cfg->nf, d_tab, d_tab + 2 * nc,
+                                   reinterpret_cast<const int *>(d_tab + 2 * nc + 2 * (nc / 2)), d_in, d_out, d_work,
                                    s) == hipSuccess &&
             hipMemcpyAsync(freqdata, d_out, 2 * (size_t)(nc + 1) * sizeof(float), hipMemcpyDeviceToHost, s) ==
                 hipSuccess &&

@@ -78,6 +78,88 @@ __device__ __forceinline__ void bfly3(float2 *F, int m, float2 tw1, float2 tw2, 
   F[m] = make_float2(b1.x - s0.y, b1.y + s0.x);
 }
 
+// --- mborgerding kissfft (FFT B: kiss_fftr at FFT.zig:90), forward, any size.
+// kf_work's recursion in iterative form: W holds the leaf-permuted input
+// (Plan::permb / the compat cfg), then stage k = nf-1 .. 0 runs fstride_k =
+// nc / (p_k m_k) groups of radix-p_k butterflies over m_k, each butterfly the
+// expression of kf_bfly{2,3,4,5,generic} (oracle/ora_kissfft.c) on its own
+// elements.  Generic radices (p > 5, kf_factor's remaining primes) are computed
+// out of place into S (nc complex) and copied back, the order of every
+// output's sum as in kf_bfly_generic.
+__device__ __forceinline__ void kbfly5(float2 *F, int m, float2 t1, float2 t2, float2 t3, float2 t4, float2 ya,
+                                       float2 yb) {
+  const float2 s0 = F[0];
+  const float2 s1 = cmul(F[m], t1), s2 = cmul(F[2 * m], t2), s3 = cmul(F[3 * m], t3), s4 = cmul(F[4 * m], t4);
+  const float2 s7 = cadd(s1, s4), s10 = csub(s1, s4), s8 = cadd(s2, s3), s9 = csub(s2, s3);
+  F[0] = make_float2(s0.x + (s7.x + s8.x), s0.y + (s7.y + s8.y));
+  const float2 s5 = make_float2(s0.x + s7.x * ya.x + s8.x * yb.x, s0.y + s7.y * ya.x + s8.y * yb.x);
+  const float2 s6 = make_float2(s10.y * ya.y + s9.y * yb.y, -(s10.x * ya.y) - s9.x * yb.y);
+  F[m] = csub(s5, s6);
+  F[4 * m] = cadd(s5, s6);
+  const float2 s11 = make_float2(s0.x + s7.x * yb.x + s8.x * ya.x, s0.y + s7.y * yb.x + s8.y * ya.x);
+  const float2 s12 = make_float2(-(s10.y * yb.y) + s9.y * ya.y, s10.x * yb.y - s9.x * ya.y);
+  F[2 * m] = cadd(s11, s12);
+  F[3 * m] = csub(s11, s12);
+}
+
+// one stage: (p, m), fstride = nc / (p m); threads tid, tid + nt, ... take
+// butterflies (group g, u); returns after its own writes (the caller syncs)
+__device__ __forceinline__ void kiss_stage(float2 *W, float2 *S, int p, int m, int nc,
+                                           const float2 *__restrict__ tw, int tid, int nt) {
+  if (p == 1) return;  // nc = 1 (fft_size 2): kf_bfly_generic with p = 1 copies in place
+  const int fstride = nc / (p * m);
+  if (p <= 5) {
+    const int nb = fstride * m;
+    for (int idx = tid; idx < nb; idx += nt) {
+      const int g = idx / m, u = idx - g * m;
+      float2 *F = W + g * p * m + u;
+      if (p == 4) {
+        bfly4(F, m, tw[u * fstride], tw[2 * u * fstride], tw[3 * u * fstride]);
+      } else if (p == 2) {
+        const float2 t = cmul(F[m], tw[u * fstride]);
+        F[m] = csub(F[0], t);
+        F[0] = cadd(F[0], t);
+      } else if (p == 3) {
+        bfly3(F, m, tw[u * fstride], tw[2 * u * fstride], tw[fstride * m]);
+      } else {
+        kbfly5(F, m, tw[u * fstride], tw[2 * u * fstride], tw[3 * u * fstride], tw[4 * u * fstride],
+               tw[fstride * m], tw[fstride * 2 * m]);
+      }
+    }
+    return;
+  }
+  // generic: output (g, u, q1) = scratch[0] + sum_q scratch[q] * tw[q * fstride * k mod nc], k = u + q1 m
+  const int no = fstride * m * p;
+  for (int idx = tid; idx < no; idx += nt) {
+    const int g = idx / (p * m), r = idx - g * (p * m), q1 = r / m, u = r - q1 * m;
+    const float2 *F = W + g * p * m + u;
+    const int k = u + q1 * m;
+    float2 acc = F[0];
+    int twidx = 0;
+    for (int q = 1; q < p; q++) {
+      twidx += fstride * k;
+      if (twidx >= nc) twidx -= nc;
+      acc = cadd(acc, cmul(F[q * m], tw[twidx]));
+    }
+    S[g * p * m + k] = acc;
+  }
+}
+
+// all stages of one transform; fac = kf_factor's (p, m) pairs, nf of them
+__device__ __forceinline__ void kiss_stages(float2 *W, float2 *S, const int *__restrict__ fac, int nf, int nc,
+                                            const float2 *__restrict__ tw, int tid, int nt) {
+  for (int k = nf - 1; k >= 0; k--) {
+    const int p = fac[2 * k], m = fac[2 * k + 1];
+    kiss_stage(W, S, p, m, nc, tw, tid, nt);
+    __syncthreads();
+    if (p > 5) {
+      for (int i = tid; i < nc; i += nt) W[i] = S[i];
+      __syncthreads();
+    }
+  }
+}
+
+
 __device__ __forceinline__ void bfly5(float2 *F, int m, float2 t1, float2 t2, float2 t3, float2 t4, float2 ya,
                                       float2 yb) {
   const float2 s0 = F[0];

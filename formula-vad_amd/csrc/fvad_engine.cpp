@@ -173,6 +173,7 @@ extern "C" void fvad_engine_config_default(fvad_engine_config *c, int n_streams,
   c->band_lo[0] = 4;
   c->band_hi[0] = 64;
   c->want_denoised = 0;
+  c->use_denoiser = 1;
 }
 
 namespace {
@@ -351,8 +352,20 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   if (c.sample_rate != 48000) return fail(FVAD_ERATE, "only 48 kHz is supported (VAD.zig:101-104)");
   if (c.n_streams < 1 || c.n_channels < 1 || c.n_channels > FVAD_MAX_CHANNELS)
     return fail(FVAD_EINVAL, "n_streams >= 1 and 1 <= n_channels <= 8 required");
-  if (c.fft_size != 2048 && c.fft_size != 512)
-    return fail(FVAD_EINVAL, "fft_size must be 2048 or 512 on the device path");
+  // FFT.zig:29-31 needs an even size; the engine's per-tick window outputs
+  // hold at most one window per 480-sample tick (fft_size >= 480), and one
+  // transform's work arrays stay in LDS (<= kMaxFftB)
+  if (c.fft_size < fvad::kFrame || (c.fft_size & 1) || c.fft_size > fvad::kMaxFftB)
+    return fail(FVAD_EINVAL, "fft_size must be even, 480 <= fft_size <= 16384");
+  if (c.mode == FVAD_MODE_FUSED) {
+    int n = c.fft_size / 2;
+    for (int p : {4, 2, 3, 5})
+      while (n % p == 0) n /= p;
+    if (n != 1 || c.fft_size > 2048)
+      return fail(FVAD_EINVAL, "fused mode: fft_size <= 2048 with radices 2, 3, 4, 5 (use the staged mode)");
+  }
+  if (!c.use_denoiser && c.mode == FVAD_MODE_FUSED)
+    return fail(FVAD_EINVAL, "use_denoiser = 0 runs on the staged engine");
   if (c.max_ticks < 1) return fail(FVAD_EINVAL, "max_ticks must be >= 1");
   if (c.n_bands < 1 || c.n_bands > FVAD_MAX_BANDS) return fail(FVAD_EINVAL, "1 <= n_bands <= 4");
   int lo = 1 << 30, hi = -1;
@@ -362,7 +375,8 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     lo = std::min(lo, c.band_lo[b]);
     hi = std::max(hi, c.band_hi[b]);
   }
-  if (hi - lo + 1 > 256) return fail(FVAD_EINVAL, "reported bins must span <= 256");
+  if (hi - lo + 1 > 256 && (c.mode == FVAD_MODE_FUSED || c.fft_size == 2048))
+    return fail(FVAD_EINVAL, "reported bins must span <= 256");
   if (c.mode != FVAD_MODE_STAGED && c.mode != FVAD_MODE_FUSED && c.mode != FVAD_MODE_FP16)
     return fail(FVAD_EINVAL, "unknown engine mode");
   int ndev = 0;
@@ -578,6 +592,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.n_bands = c.n_bands;
   fill_bands(c, a.band_lo, a.band_hi, &a.bin_lo_all, &a.bin_hi_all);
   a.nfft_b = c.fft_size;
+  a.use_denoiser = c.use_denoiser;
   // wave kernels with static batch striding (bit 1 << fvad::WaveKernel):
   // k_pspecw and k_synthw by default; FVAD_WSTATIC=<mask> overrides
   static const int wstatic = [] {
@@ -602,12 +617,21 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
     return v && atoi(v) == 1;
   }();
   const fvad::StagedStreams st{e->stream, fork ? e->aux : e->stream, e->ev_fork, e->ev_join};
-  HIP_TRY(fvad::launch_prep(a, e->pstream, timed ? e->ev : nullptr));
-  HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
-  HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
-  // window output set b is free once push k-2's k_vadm_hbm has read it
-  if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
-  HIP_TRY(fvad::launch_staged(a, e->grid_frames, st, timed ? e->ev : nullptr));
+  if (c.use_denoiser) {
+    HIP_TRY(fvad::launch_prep(a, e->pstream, timed ? e->ev : nullptr));
+    HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
+    // window output set b is free once push k-2's k_vadm_hbm has read it
+    if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
+    HIP_TRY(fvad::launch_staged(a, e->grid_frames, st, timed ? e->ev : nullptr));
+  } else {
+    // no denoiser: raw input frames to the ring, windows, FFT B, all on the
+    // engine stream after the input copy (queued on the prep stream)
+    HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
+    if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
+    HIP_TRY(fvad::launch_nodenoise(a, e->grid_frames, e->stream));
+  }
   if (e->vadm.n > 0) {
     const fvad_engine_config &c = e->cfg;
     const size_t TB = (size_t)n_ticks * c.n_streams;
@@ -644,6 +668,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
 }
 
 int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
+  if (!e->cfg.use_denoiser) timed = false;  // the no-denoiser pipeline records no kernel events
   const int rc = e->cfg.mode == FVAD_MODE_FUSED ? launch_fused(e, n_ticks, use_ticks, timed)
                                                  : launch_staged(e, n_ticks, use_ticks, timed);
   if (!rc && timed) e->slot_pending[e->ev_slot] = true;
@@ -714,6 +739,12 @@ int fetch(fvad_engine *e, int n_ticks, fvad_outputs *o) {
 
 namespace {
 
+// the stream whose kernel reads the device input: k_prep3 on the prep stream
+// (staged), k_prep / k_ndring on the engine stream (fused, no denoiser)
+hipStream_t input_reader(const fvad_engine *e) {
+  return (e->cfg.mode != FVAD_MODE_FUSED && e->cfg.use_denoiser) ? e->pstream : e->stream;
+}
+
 // the input of the push about to launch goes to device buffer in_next; its
 // previous reader (the k_prep3 of the push two before) must be done
 int input_buffer(fvad_engine *e, hipStream_t cs) {
@@ -726,7 +757,7 @@ int input_buffer(fvad_engine *e, hipStream_t cs) {
 // after the launch: the buffer is free again once this push's prep read it
 int release_input(fvad_engine *e) {
   const int ib = e->in_next;
-  HIP_TRY(hipEventRecord(e->ev_in_free[ib], e->cfg.mode != FVAD_MODE_FUSED ? e->pstream : e->stream));
+  HIP_TRY(hipEventRecord(e->ev_in_free[ib], input_reader(e)));
   e->in_busy[ib] = true;
   e->in_next = ib ^ 1;
   e->resident_ticks = 0;
@@ -968,7 +999,7 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
   }();
   if ((rc = launch(e, n_ticks, false, !no_events))) return rc;
   // a later submit / push must not overwrite buffer 0 under this run's prep
-  HIP_TRY(hipEventRecord(e->ev_in_free[0], e->cfg.mode != FVAD_MODE_FUSED ? e->pstream : e->stream));
+  HIP_TRY(hipEventRecord(e->ev_in_free[0], input_reader(e)));
   e->in_busy[0] = true;
   return FVAD_OK;
 }

@@ -22,9 +22,11 @@ constexpr int kMaxNeurons = 128;
 constexpr int kMaxCh = 8;
 constexpr int kMaxBandCfg = 4;
 
-// FFT B (FFT.zig) is a real FFT of fft_size; the device path supports
-// fft_size/2 = 4^k (kissfft then factors into radix-4 only), fft_size <= 4096.
-constexpr int kMaxFftB = 4096;
+// FFT B (FFT.zig) is a real FFT of fft_size: any even fft_size up to
+// kMaxFftB on the device (kissfft's mixed-radix factorisation; one transform's
+// work array, twice that with a radix > 5, stays in LDS).
+constexpr int kMaxFftB = 16384;
+constexpr int kMaxFactors = 32;
 
 // ---------------------------------------------------------------------------
 // Per-stream persistent state, one contiguous record per stream (the kernels
@@ -101,7 +103,10 @@ struct Plan {
   // FFT B (kissfft real FFT of size nfft_b)
   int nfft_b;                    // real size (2048)
   int ncfft_b;                   // nfft_b / 2
-  int stages_b;                  // log4(ncfft_b)
+  int stages_b;                  // log4(ncfft_b) when ncfft_b = 4^k (k_fftbw), else 0
+  int nfac_b;                    // kf_factor(ncfft_b): (p, m) pairs
+  int fac_b[2 * kMaxFactors];
+  int generic_b;                 // a radix > 5 occurs (out-of-place stage scratch needed)
   float norm_b;                  // windowNormFactor / (nfft/2)
   float twb[2 * kMaxFftB / 2];   // kissfft substate twiddles (r,i)
   float superb[2 * kMaxFftB / 4];  // super twiddles (r,i)

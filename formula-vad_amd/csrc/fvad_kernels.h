@@ -38,7 +38,7 @@ struct FrameArgs {
 size_t frame_lds_bytes();
 hipError_t launch_prep(const PrepArgs &a, hipStream_t stream);
 hipError_t launch_frame(const FrameArgs &a, hipStream_t stream);
-hipError_t launch_kiss_fftr(int ncfft, int stages, const float *twb, const float *sup, const int *perm,
-                            const float *in, float *out, hipStream_t stream);
+hipError_t launch_kiss_fftr(int ncfft, const int *fac, int nf, const float *twb, const float *sup, const int *perm,
+                            const float *in, float *out, float *work, hipStream_t stream);
 
 }  // namespace fvad

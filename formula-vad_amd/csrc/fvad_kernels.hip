@@ -804,7 +804,7 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
       }
       if (!complete && tid < C * a.n_bands) a.out_band[o * C * a.n_bands + tid] = 0.0f;  // defined: no window
       if (complete) {
-        // FFT B per channel: window, kissfft (radix-4 DIT), kiss_fftr post-pass, |X|*norm, band sums
+        // FFT B per channel: window, kissfft (mixed radix), kiss_fftr post-pass, |X|*norm, band sums
         const int nc = P->ncfft_b;
         const float2 *__restrict__ twb = reinterpret_cast<const float2 *>(P->twb);
         const float2 *__restrict__ sup = reinterpret_cast<const float2 *>(P->superb);
@@ -818,14 +818,8 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
             W[k] = make_float2(t0, t1);
           }
           __syncthreads();
-          for (int stg = 0, m = 1; stg < P->stages_b; stg++, m *= 4) {
-            const int fstride = nc / (4 * m);
-            for (int q = tid; q < nc / 4; q += NT) {
-              const int blk = q / m, u = q - blk * m;
-              bfly4(W + blk * 4 * m + u, m, twb[u * fstride], twb[2 * u * fstride], twb[3 * u * fstride]);
-            }
-            __syncthreads();
-          }
+          // fused mode: fft_size <= 2048 and radices 2..5 (no out-of-place stage)
+          kiss_stages(W, nullptr, P->fac_b, P->nfac_b, nc, twb, tid, NT);
           // magnitudes of the union of reported bins
           const int lo = a.bin_lo_all, hi = a.bin_hi_all;
           for (int k = lo + tid; k <= hi; k += NT) {
@@ -837,12 +831,12 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
               re = W[0].x - W[0].y;
               imv = 0;
             } else {
-              const int kk = (k < nc / 2) ? k : nc - k;
+              const int kk = (2 * k < nc) ? k : nc - k;
               const float2 fpk = W[kk];
               const float2 fpnk = make_float2(W[nc - kk].x, -W[nc - kk].y);
               const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
               const float2 tw2 = cmul(f2k, sup[kk - 1]);
-              if (k < nc / 2) {
+              if (2 * k < nc) {
                 re = (f1k.x + tw2.x) * ((float).5);
                 imv = (f1k.y + tw2.y) * ((float).5);
               } else {
@@ -894,27 +888,24 @@ __global__ void __launch_bounds__(NT) k_frame(FrameArgs a) {
 
 // ---------------------------------------------------------------------------
 // k_kiss_fftr: one workgroup computes the complete kissfft real FFT of one
-// nfft-point frame (kiss_fftr, FFT.zig:90) — used by the kiss_fftr compat shim.
-// Tables (twiddles, super twiddles, leaf permutation) come from the caller's
-// cfg memory (kiss_fftr_alloc lenmem protocol).
+// nfft-point frame (kiss_fftr, FFT.zig:90) -- used by the kiss_fftr compat
+// shim, any even nfft.  Tables (twiddles, super twiddles, factors, leaf
+// permutation) come from the caller's cfg memory (kiss_fftr_alloc lenmem
+// protocol).  The work arrays W / S are in LDS when they fit, else in the
+// shim's device scratch (work).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_kiss_fftr(int ncfft, int stages, const float2 *__restrict__ twb,
-                                                   const float2 *__restrict__ sup, const int *__restrict__ perm,
-                                                   const float *__restrict__ in, float2 *__restrict__ out) {
+__global__ void __launch_bounds__(256) k_kiss_fftr(int ncfft, const int *__restrict__ fac, int nf,
+                                                   const float2 *__restrict__ twb, const float2 *__restrict__ sup,
+                                                   const int *__restrict__ perm, const float *__restrict__ in,
+                                                   float2 *__restrict__ out, float2 *work, int in_lds) {
   extern __shared__ __attribute__((aligned(16))) float L[];
-  float2 *W = reinterpret_cast<float2 *>(L);
+  float2 *W = in_lds ? reinterpret_cast<float2 *>(L) : work;
+  float2 *S = W + ncfft;
   const int tid = threadIdx.x;
   const float2 *in2 = reinterpret_cast<const float2 *>(in);
   for (int k = tid; k < ncfft; k += 256) W[k] = in2[perm[k]];
   __syncthreads();
-  for (int stg = 0, m = 1; stg < stages; stg++, m *= 4) {
-    const int fstride = ncfft / (4 * m);
-    for (int q = tid; q < ncfft / 4; q += 256) {
-      const int blk = q / m, u = q - blk * m;
-      bfly4(W + blk * 4 * m + u, m, twb[u * fstride], twb[2 * u * fstride], twb[3 * u * fstride]);
-    }
-    __syncthreads();
-  }
+  kiss_stages(W, S, fac, nf, ncfft, twb, tid, 256);
   for (int k = tid; k <= ncfft; k += 256) {
     float2 r;
     if (k == 0) {
@@ -922,12 +913,15 @@ __global__ void __launch_bounds__(256) k_kiss_fftr(int ncfft, int stages, const 
     } else if (k == ncfft) {
       r = make_float2(W[0].x - W[0].y, 0.0f);
     } else {
-      const int kk = (k < ncfft / 2) ? k : ncfft - k;
+      // kiss_fftr's loop kk = 1 .. ncfft/2 writes bin kk, then bin ncfft - kk
+      // (the later write wins at kk = ncfft/2)
+      const bool lower = 2 * k < ncfft;
+      const int kk = lower ? k : ncfft - k;
       const float2 fpk = W[kk];
       const float2 fpnk = make_float2(W[ncfft - kk].x, -W[ncfft - kk].y);
       const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
       const float2 tw2 = cmul(f2k, sup[kk - 1]);
-      if (k < ncfft / 2)
+      if (lower)
         r = make_float2((f1k.x + tw2.x) * ((float).5), (f1k.y + tw2.y) * ((float).5));
       else
         r = make_float2((f1k.x - tw2.x) * ((float).5), (tw2.y - f1k.y) * ((float).5));
@@ -950,11 +944,13 @@ hipError_t launch_prep(const PrepArgs &a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_kiss_fftr(int ncfft, int stages, const float *twb, const float *sup, const int *perm,
-                            const float *in, float *out, hipStream_t stream) {
-  hipLaunchKernelGGL(k_kiss_fftr, dim3(1), dim3(256), sizeof(float) * 2 * ncfft, stream, ncfft, stages,
+hipError_t launch_kiss_fftr(int ncfft, const int *fac, int nf, const float *twb, const float *sup, const int *perm,
+                            const float *in, float *out, float *work, hipStream_t stream) {
+  const size_t lds = sizeof(float) * 4 * (size_t)ncfft;  // W + S
+  const bool in_lds = lds <= 64 * 1024;
+  hipLaunchKernelGGL(k_kiss_fftr, dim3(1), dim3(256), in_lds ? lds : 0, stream, ncfft, fac, nf,
                      reinterpret_cast<const float2 *>(twb), reinterpret_cast<const float2 *>(sup), perm, in,
-                     reinterpret_cast<float2 *>(out));
+                     reinterpret_cast<float2 *>(out), reinterpret_cast<float2 *>(work), in_lds ? 1 : 0);
   return hipGetLastError();
 }
 

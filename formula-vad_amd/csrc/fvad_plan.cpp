@@ -41,6 +41,28 @@ void celt_digit_reverse(int fout, int *f, int fstride, const int *factors) {
 }
 
 // kissfft kf_work leaf placement: Fout[k] = fin[perm[k]].
+// kf_factor (kissfft): powers of 4 first, then 2, then odd primes; one (p, m)
+// pair per stage with m = the remaining length
+void kiss_factor(int n, int *fac, int *nf) {
+  int p = 4, k = 0;
+  const double floor_sqrt = std::floor(std::sqrt((double)n));
+  do {
+    while (n % p) {
+      switch (p) {
+        case 4: p = 2; break;
+        case 2: p = 3; break;
+        default: p += 2; break;
+      }
+      if (p > floor_sqrt) p = n;
+    }
+    n /= p;
+    fac[2 * k] = p;
+    fac[2 * k + 1] = n;
+    k++;
+  } while (n > 1);
+  *nf = k;
+}
+
 void kiss_leaf_perm(int *perm, int out_base, int in_base, int fstride, const int *factors) {
   const int p = factors[0], m = factors[1];
   if (m == 1) {
@@ -91,10 +113,14 @@ void build_plan(Plan *p, int nfft_b) {
   // kissfft real FFT B
   p->nfft_b = nfft_b;
   p->ncfft_b = nfft_b / 2;
-  int st = 0;
-  for (int n = p->ncfft_b; n > 1; n /= 4) st++;
-  p->stages_b = st;
   const int nc = p->ncfft_b;
+  kiss_factor(nc, p->fac_b, &p->nfac_b);
+  int st = 0;
+  for (int i = 0; i < p->nfac_b; i++) {
+    st = (p->fac_b[2 * i] == 4 && st == i) ? st + 1 : st;
+    if (p->fac_b[2 * i] > 5) p->generic_b = 1;
+  }
+  p->stages_b = st == p->nfac_b ? st : 0;
   for (int i = 0; i < nc; i++) {
     const double kpi = 3.141592653589793238462643383279502884197169399375105820974944;
     const double phase = -2 * kpi * i / nc;
@@ -106,17 +132,7 @@ void build_plan(Plan *p, int nfft_b) {
     p->superb[2 * i] = (float)std::cos(phase);
     p->superb[2 * i + 1] = (float)std::sin(phase);
   }
-  int kf[2 * 16];
-  {
-    int n = nc, k = 0;
-    while (n > 1) {
-      n /= 4;
-      kf[2 * k] = 4;
-      kf[2 * k + 1] = n;
-      k++;
-    }
-  }
-  kiss_leaf_perm(p->permb, 0, 0, 1, kf);
+  kiss_leaf_perm(p->permb, 0, 0, 1, p->fac_b);
   // hannWindowPeriodic in f32 (2*pi coerced to f32, (2*pi*k*n)/N in f32, f32 cos)
   const float N = (float)nfft_b;
   const float two_pi = (float)(2.0 * pi);

@@ -90,6 +90,7 @@ struct StagedArgs {
   const DevModel *model;
   int n_bands;
   int nfft_b;                  // FFT B size (fft_size)
+  int use_denoiser;            // 0: raw fft_size frames straight to FFT B (launch_nodenoise)
   int wave_static;             // wave kernels with static batch striding: bit 1 << WaveKernel
   int band_lo[kMaxBandCfg], band_hi[kMaxBandCfg];
   int bin_lo_all, bin_hi_all;
@@ -130,6 +131,8 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
 // Device VADMachines over the window outputs a.out_* of one push: overlap =
 // the light HBM variant meant to co-run with the next push on a side stream.
 hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream);
+// use_denoiser = 0 (VAD.zig:206-212,239-249): k_ndring, k_ndmeta, FFT B
+hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream);
 // fp16 / MFMA recurrence (fvad_gru16.hip), run in k_rnn3's place when a.gru16_frags is set
 hipError_t launch_gru16(const StagedArgs &a, hipStream_t stream);
 int gru16_frag_count();   // A fragments of 64 lanes x 8 f16

@@ -1231,16 +1231,19 @@ __global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
 // ---------------------------------------------------------------------------
 template <int NT>
 __global__ void __launch_bounds__(NT) k_fftb(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 W[kMaxFftB / 2];
-  __shared__ float mag[256];
+  // dynamic LDS: W[nc] (+ S[nc] with a radix > 5), then the magnitudes of
+  // the reported bins
+  extern __shared__ __attribute__((aligned(16))) float2 W[];
+  const Plan *__restrict__ P = a.plan;
+  const int nc = P->ncfft_b, C = a.n_channels;
+  float2 *S = W + nc;
+  float *mag = reinterpret_cast<float *>(W + (P->generic_b ? 2 * nc : nc));
   const int tid = threadIdx.x;
   const int s = blockIdx.x / a.wmax, j = blockIdx.x - s * a.wmax;
   if (s >= a.n_streams) return;
   const int t = a.win_tick[(size_t)s * a.wmax + j];
   if (t < 0) return;
   const long long wstart = a.win_start[(size_t)s * a.wmax + j];
-  const Plan *__restrict__ P = a.plan;
-  const int nc = P->ncfft_b, C = a.n_channels;
   const float2 *__restrict__ twb = reinterpret_cast<const float2 *>(P->twb);
   const float2 *__restrict__ sup = reinterpret_cast<const float2 *>(P->superb);
   const size_t o = (size_t)t * a.n_streams + s;
@@ -1253,14 +1256,7 @@ __global__ void __launch_bounds__(NT) k_fftb(StagedArgs a) {
       W[k] = make_float2(t0, t1);
     }
     __syncthreads();
-    for (int stg = 0, m = 1; stg < P->stages_b; stg++, m *= 4) {
-      const int fstride = nc / (4 * m);
-      for (int q = tid; q < nc / 4; q += NT) {
-        const int blk = q / m, u = q - blk * m;
-        bfly4(W + blk * 4 * m + u, m, twb[u * fstride], twb[2 * u * fstride], twb[3 * u * fstride]);
-      }
-      __syncthreads();
-    }
+    kiss_stages(W, S, P->fac_b, P->nfac_b, nc, twb, tid, NT);
     const int lo = a.bin_lo_all, hi = a.bin_hi_all;
     for (int k = lo + tid; k <= hi; k += NT) {
       float re, imv;
@@ -1271,12 +1267,12 @@ __global__ void __launch_bounds__(NT) k_fftb(StagedArgs a) {
         re = W[0].x - W[0].y;
         imv = 0;
       } else {
-        const int kk = (k < nc / 2) ? k : nc - k;
+        const int kk = (2 * k < nc) ? k : nc - k;
         const float2 fpk = W[kk];
         const float2 fpnk = make_float2(W[nc - kk].x, -W[nc - kk].y);
         const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
         const float2 tw2 = cmul(f2k, sup[kk - 1]);
-        if (k < nc / 2) {
+        if (2 * k < nc) {
           re = (f1k.x + tw2.x) * ((float).5);
           imv = (f1k.y + tw2.y) * ((float).5);
         } else {
@@ -1414,7 +1410,8 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
       if (v < min_v) min_v = v;
       if (v > max_v) max_v = v;
     }
-    const float vad = a.out_win_vad[o], vr = a.out_win_ratio[o];
+    // fft_input.vad orelse 0 (VADMachine.zig:240-246): no vad without the denoiser
+    const float vad = a.use_denoiser ? a.out_win_vad[o] : 0.0f, vr = a.out_win_ratio[o];
     const double st_avg = ra_push(st, B, K.n_st, S.st_widx, S.st_count, S.st_last, S.st_has, min_v);
     const double r_avg = ra_push(rb, B, K.n_r, S.r_widx, S.r_count, S.r_last, S.r_has, vr);
     double base;
@@ -1510,6 +1507,90 @@ int resident_blocks(K kernel, int threads, int n_cu) {
 }
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// use_denoiser = false (VAD.zig:206-212,239-249): the pipeline reads fft_size
+// frames of raw input straight into FFT B; no rnnoise, no per-frame vad.
+// k_ndring: input ticks -> the stream's re-block ring (k_ola's float4 layout),
+// per-tick vad / ratio set to -1 (not produced by the reference on this path),
+// the raw input as the "denoised" output.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_ndring(StagedArgs a) {
+  const int C = a.n_channels, V = a.V;
+  const int q = threadIdx.x & 127;
+  const long long fl = (long long)blockIdx.x * 2 + (threadIdx.x >> 7);
+  if (fl >= (long long)a.n_streams * V || q >= kFrame / 4) return;
+  const int s = (int)(fl / V), v = (int)(fl - (long long)s * V);
+  const int nt = ticks_of(a, s);
+  if (v >= nt * C) return;
+  const int t = v / C, c = v - t * C, i = 4 * q;
+  const float *stp = a.state + (size_t)s * st::kWords;
+  const size_t o = (size_t)t * a.n_streams + s;
+  const float4 x = *reinterpret_cast<const float4 *>(a.pcm + (o * C + c) * kFrame + i);
+  const int frames_done = reinterpret_cast<const int *>(stp)[st::kFramesDone];
+  long long ri = (long long)(frames_done + t) * kFrame % a.ring_len + i;
+  if (ri >= a.ring_len) ri -= a.ring_len;
+  *reinterpret_cast<float4 *>(a.ring + ((size_t)s * C + c) * a.ring_len + ri) = x;
+  if (a.out_den) *reinterpret_cast<float4 *>(a.out_den + (o * C + c) * kFrame + i) = x;
+  if (i == 0 && c == 0) {
+    a.out_vad[o] = -1.0f;
+    a.ratio[o] = -1.0f;
+  }
+}
+
+// k_ndmeta: window completion per tick (the k_winmeta rule); a completed
+// window's volume ratio is preAnalyzeSegment over its fft_size input samples
+// (VAD.zig:253-272: rmsVolume per channel = sqrt(sum x^2 / n), the sum in
+// sample order; min / max over channels); lane per stream.
+__global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= a.n_streams) return;
+  const int nt = ticks_of(a, s), C = a.n_channels, FB = a.nfft_b;
+  int *wt = a.win_tick + (size_t)s * a.wmax;
+  long long *wsx = a.win_start + (size_t)s * a.wmax;
+  int j = 0;
+  if (nt > 0) {
+    int *istp = reinterpret_cast<int *>(a.state + (size_t)s * st::kWords);
+    int fd = istp[st::kFramesDone];
+    for (int t = 0; t < nt; t++) {
+      const size_t o = (size_t)t * a.n_streams + s;
+      const long long a0 = (long long)fd * kFrame;
+      const long long wdone = a0 / FB;
+      const long long next_end = (wdone + 1) * FB;
+      const bool complete = a0 + kFrame >= next_end;
+      if (complete) {
+        const long long ws = wdone * FB;
+        float vol_min = 1, vol_max = 0;
+        for (int c = 0; c < C; c++) {
+          const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
+          long long ri = ws % a.ring_len;
+          float sum = 0.0f;
+          for (int n = 0; n < FB; n++) {
+            const float x = ring[ri];
+            sum += x * x;
+            if (++ri == a.ring_len) ri = 0;
+          }
+          const float vol = sqrtf(sum / (float)FB);
+          if (vol < vol_min) vol_min = vol;
+          if (vol > vol_max) vol_max = vol;
+        }
+        a.out_win_ratio[o] = vol_max == 0 ? 0.0f : vol_min / vol_max;
+        a.out_win_vad[o] = -1.0f;
+        wt[j] = t;
+        wsx[j] = ws;
+        j++;
+      } else {
+        a.out_win_ratio[o] = 0.0f;
+        a.out_win_vad[o] = 0.0f;
+        for (int i = 0; i < C * a.n_bands; i++) a.out_band[o * C * a.n_bands + i] = 0.0f;
+      }
+      a.out_win_flag[o] = complete ? 1 : 0;
+      fd++;
+    }
+    istp[st::kFramesDone] = fd;
+  }
+  for (; j < a.wmax; j++) wt[j] = -1;
+}
+
 // every launch is checked where it is issued: a failed launch in the middle of
 // the pipeline returns its own error instead of surfacing at the end
 #define FVAD_LAUNCH_TRY(x)            \
@@ -1522,6 +1603,32 @@ int resident_blocks(K kernel, int threads, int n_cu) {
     hipLaunchKernelGGL(__VA_ARGS__);           \
     FVAD_LAUNCH_TRY(hipGetLastError());        \
   } while (0)
+
+// k_fftb's dynamic LDS: the transform (twice with a radix > 5) + reported bins
+size_t fftb_lds_bytes(const StagedArgs &a) {
+  const int nc = a.nfft_b / 2;
+  int n = nc, generic = 0;
+  for (int p = 2; p * p <= n; p++)
+    while (n % p == 0) {
+      generic |= p > 5;
+      n /= p;
+    }
+  generic |= n > 5;
+  return sizeof(float2) * (size_t)nc * (generic ? 2 : 1) + sizeof(float) * (a.bin_hi_all - a.bin_lo_all + 1);
+}
+
+// FFT B: the wave-per-window kernel for 2048 points, the block kernel
+// (mixed radix, dynamic LDS) for every other size
+hipError_t launch_fftb(const StagedArgs &a, int n_cu, hipStream_t stream) {
+  if (a.nfft_b == 2048) return launch_wave(kWaveFftB, a, n_cu, stream);
+  static const bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fftb<256>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
+  FVAD_KERNEL_TRY(k_fftb<256>, dim3(a.n_streams * a.wmax), dim3(256), fftb_lds_bytes(a), stream, a);
+  return hipSuccess;
+}
 
 hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) {
   (void)hipGetLastError();
@@ -1582,11 +1689,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   REC(11);
   FVAD_KERNEL_TRY(k_winmeta, dim3((a.n_streams + kWmS - 1) / kWmS), dim3(64), 0, stream, a);
   REC(12);
-  // FFT B: the wave-per-window kernel for 2048 points, the block kernel for 512
-  if (a.nfft_b == 2048)
-    FVAD_LAUNCH_TRY(launch_wave(kWaveFftB, a, n_cu, stream));
-  else
-    FVAD_KERNEL_TRY(k_fftb<256>, dim3(a.n_streams * a.wmax), dim3(256), 0, stream, a);
+  FVAD_LAUNCH_TRY(launch_fftb(a, n_cu, stream));
   REC(13);
 #undef REC
 #undef REC_AUX
@@ -1605,6 +1708,14 @@ __global__ void __launch_bounds__(64) k_vadm_hbm(StagedArgs a) {
   if (s >= a.n_streams || ticks_of(a, s) <= 0) return;
   for (int m = 0; m < a.vadm.n; m++)
     vadm_stream(a, m, s, a.vadm.buf + a.vadm.c[m].lt_off + s, (size_t)a.n_streams);
+}
+
+hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream) {
+  (void)hipGetLastError();
+  const long long frames = (long long)a.n_streams * a.V;
+  FVAD_KERNEL_TRY(k_ndring, dim3((unsigned)((frames + 1) / 2)), dim3(256), 0, stream, a);
+  FVAD_KERNEL_TRY(k_ndmeta, dim3((a.n_streams + 63) / 64), dim3(64), 0, stream, a);
+  return launch_fftb(a, n_cu, stream);
 }
 
 hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream) {

@@ -103,13 +103,16 @@ typedef struct {
   int n_channels;       /* channels per stream (2 = onboard stereo) */
   int device;           /* HIP device ordinal */
   int sample_rate;      /* must be 48000 */
-  int fft_size;         /* VAD.Config.fft_size: 2048 (or 512) */
+  int fft_size;         /* VAD.Config.fft_size: even, 480..16384 (fused mode: radices 2..5, <= 2048) */
   int max_ticks;        /* largest n_ticks per push */
   int n_bands;          /* band sums to report per window, 1..4 */
   int band_lo[FVAD_MAX_BANDS]; /* inclusive FFT-B bin ranges (FFT.freqToBin) */
   int band_hi[FVAD_MAX_BANDS];
   int want_denoised;    /* keep denoised PCM (VAD.zig temp_denoiser_segment) */
   int mode;             /* FVAD_MODE_STAGED (default), FVAD_MODE_FUSED or FVAD_MODE_FP16 */
+  int use_denoiser;     /* VAD.Config.use_denoiser (default 1).  0: fft_size frames of raw input go
+                         * straight to FFT B (VAD.zig:206-212,239-249); per-tick vad / ratio are -1,
+                         * the window ratio is preAnalyzeSegment's over the frame, window vad -1 */
 } fvad_engine_config;
 
 /* staged: time-parallel frame kernels + a thin per-stream recurrence kernel;

@@ -144,3 +144,21 @@ def test_cpu_baseline_native_build_same_work(oracle_mod, fvad_mod):
     _, a = oracle_mod.bench_pipeline(pcm, chunk=24000, n_threads=2)
     _, b = oracle_mod.bench_pipeline(pcm, chunk=24000, n_threads=2, L=L)
     assert a == b and a["frames"] == 2 * 100 * 2
+
+
+@pytest.mark.parametrize("n", [2, 6, 1000, 1024, 2048, 2 * 1009, 40000])
+def test_kiss_fftr_alloc_lenmem_protocol(fvad_mod, n):
+    """FFT.zig:193-208 probes kiss_fftr_alloc(n, 0, NULL, &lenmem = 1): it must
+    fail and write the size; FFT.zig:179-191 then builds the cfg in caller
+    memory.  Host-only (no device call)."""
+    import ctypes as C
+    L = fvad_mod.lib()
+    lenmem = C.c_size_t(1)
+    assert L.kiss_fftr_alloc(n, 0, None, C.byref(lenmem)) is None
+    assert lenmem.value > 0
+    small = C.c_size_t(lenmem.value - 1)
+    mem = C.create_string_buffer(lenmem.value)
+    assert L.kiss_fftr_alloc(n, 0, mem, C.byref(small)) is None and small.value == lenmem.value
+    got = C.c_size_t(lenmem.value)
+    assert L.kiss_fftr_alloc(n, 0, mem, C.byref(got)) == C.addressof(mem)
+    assert L.kiss_fftr_alloc(n + 1, 0, None, C.byref(C.c_size_t(1))) is None  # odd sizes refused
