@@ -387,7 +387,9 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   e->cfg = c;
   // the staged path writes every tick of a push before FFT B reads its
   // windows, so the ring holds one window plus a whole push
-  e->ring_len = c.fft_size + c.max_ticks * fvad::kFrame;
+  // the re-block ring holds a window plus a push; a multiple of 4 so a
+  // frame's float4 writes never straddle its end (k_ola, k_ndring)
+  e->ring_len = (c.fft_size + c.max_ticks * fvad::kFrame + 3) & ~3;
   e->n_kernels = c.mode != FVAD_MODE_FUSED ? fvad::kStagedKernels : 2;
   e->n_events = c.mode != FVAD_MODE_FUSED ? fvad::kStagedEvents : 3;
   e->last_event = c.mode != FVAD_MODE_FUSED ? fvad::kStagedLast : 2;

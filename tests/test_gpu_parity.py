@@ -250,7 +250,7 @@ def test_full_size_determinism_and_spot_parity(fvad_mod, oracle_mod, models):
 def test_engine_argument_errors(fvad_mod, models):
     m, _ = models
     with pytest.raises(fvad_mod.FvadError):
-        fvad_mod.Engine(m, 1, 2, fft_size=1000)
+        fvad_mod.Engine(m, 1, 2, fft_size=1001)  # odd: FFT.zig:29-31
     e = fvad_mod.Engine(m, 2, 2, max_ticks=4)
     with pytest.raises(fvad_mod.FvadError):
         e.push(np.zeros((5, 2, 2, 480), np.float32))
