@@ -345,24 +345,32 @@ extern "C" int fvad_recording_channel(const float *const *pcm, int n_channels, s
   return best;
 }
 
-extern "C" int fvad_pipeline_create(int sample_rate, int n_channels, const fvad_model *model, int device,
-                                    const fvad_vadm_config *main_cfg, const fvad_vadm_config *alt_cfgs, int n_alt,
-                                    fvad_pipeline **out) {
-  if (!model || !out || n_channels < 1 || n_channels > FVAD_MAX_CHANNELS || n_alt < 0) return FVAD_EINVAL;
+extern "C" void fvad_vad_config_default(fvad_vad_config *c) {
+  std::memset(c, 0, sizeof(*c));
+  c->fft_size = 2048;
+  c->use_denoiser = 1;
+  fvad_vadm_config_default(&c->vad_machine_config);
+}
+
+extern "C" int fvad_pipeline_create_ex(int sample_rate, int n_channels, const fvad_model *model, int device,
+                                       const fvad_vad_config *vc, fvad_pipeline **out) {
+  if (!model || !out || !vc || n_channels < 1 || n_channels > FVAD_MAX_CHANNELS || vc->n_alt < 0 ||
+      (vc->n_alt > 0 && !vc->alt_vad_machine_configs))
+    return FVAD_EINVAL;
   if (sample_rate != 48000) return FVAD_ERATE;
   fvad_pipeline *p = new fvad_pipeline();
   p->n_channels = n_channels;
-  fvad_vadm_config def;
-  fvad_vadm_config_default(&def);
-  p->sm.machines.emplace_back(main_cfg ? *main_cfg : def, sample_rate, 2048);
-  for (int i = 0; i < n_alt; i++) p->sm.machines.emplace_back(alt_cfgs[i], sample_rate, 2048);
+  p->sm.machines.emplace_back(vc->vad_machine_config, sample_rate, vc->fft_size);
+  for (int i = 0; i < vc->n_alt; i++) p->sm.machines.emplace_back(vc->alt_vad_machine_configs[i], sample_rate, vc->fft_size);
   fvad_engine_config_default(&p->ec, 1, n_channels);
   p->ec.device = device;
   p->ec.max_ticks = 100;
+  p->ec.fft_size = vc->fft_size;
+  p->ec.use_denoiser = vc->use_denoiser;
   int rc = assign_bands(p->sm.machines, p->ec);
   if (!rc) rc = fvad_engine_create(&p->ec, model, &p->engine);
   if (!rc) {
-    // the machines run on the device after every push (k_vadm)
+    // the machines run on the device after every push (k_vadm_hbm)
     std::vector<fvad_vadm_config> cfgs;
     for (auto &m : p->sm.machines) cfgs.push_back(m.cfg);
     rc = fvad_engine_attach_vadm(p->engine, cfgs.data(), (int)cfgs.size(), kPipelineSegCap);
@@ -377,6 +385,17 @@ extern "C" int fvad_pipeline_create(int sample_rate, int n_channels, const fvad_
   p->pcm.resize((size_t)p->ec.max_ticks * n_channels * fvad::kFrame);
   *out = p;
   return FVAD_OK;
+}
+
+extern "C" int fvad_pipeline_create(int sample_rate, int n_channels, const fvad_model *model, int device,
+                                    const fvad_vadm_config *main_cfg, const fvad_vadm_config *alt_cfgs, int n_alt,
+                                    fvad_pipeline **out) {
+  fvad_vad_config vc;
+  fvad_vad_config_default(&vc);
+  if (main_cfg) vc.vad_machine_config = *main_cfg;
+  vc.alt_vad_machine_configs = alt_cfgs;
+  vc.n_alt = n_alt;
+  return fvad_pipeline_create_ex(sample_rate, n_channels, model, device, &vc, out);
 }
 
 extern "C" void fvad_pipeline_destroy(fvad_pipeline *p) {
@@ -464,60 +483,88 @@ extern "C" size_t fvad_pipeline_segments(const fvad_pipeline *p, int alt, fvad_s
 }
 
 // ---------------------------------------------------------------------------
-// Multi-stream simulator core: streams partitioned contiguously over devices,
-// one host thread and one engine per device, lock-step ticks (no collectives).
+// Multi-stream simulator core (simulator.zig:217-228 runs a thread per
+// instance): streams grouped by channel count, each group partitioned
+// contiguously over the devices; one engine and one host thread per (group,
+// device) part, lock-step pushes, no collectives.  Input is pulled from a
+// reader per push (the simulator's 48 000-frame read loop,
+// SimulationInstance.zig:171-203) straight into the engine's pinned slot,
+// with two pushes in flight.
 // ---------------------------------------------------------------------------
 struct fvad_multi {
-  int n_streams, n_channels, ticks_per_push;
+  int n_streams, ticks_per_push, n_machines;
+  std::vector<int> channels;  // [stream]
   struct Part {
-    int device, s0, s1;
+    int device, n_channels;
+    std::vector<int> streams;  // global stream ids, in order
     fvad_engine *engine = nullptr;
     fvad_engine_config ec;
   };
   std::vector<Part> parts;
-  std::vector<StreamMachines> sm;
-  fvad_vadm_config cfg;
+  std::vector<std::pair<int, int>> where;  // stream -> (part, index in part)
 };
 
-extern "C" int fvad_multi_create(int n_streams, int n_channels, const fvad_model *model, const int *devices,
-                                 int n_devices, const fvad_vadm_config *cfg, int ticks_per_push, fvad_multi **out) {
-  if (!model || !out || n_streams < 1 || n_devices < 1 || !devices || ticks_per_push < 1) return FVAD_EINVAL;
+extern "C" int fvad_multi_create_ex(int n_streams, const int *n_channels, const fvad_model *model, const int *devices,
+                                    int n_devices, const fvad_vad_config *vc, int ticks_per_push, fvad_multi **out) {
+  if (!model || !out || !vc || n_streams < 1 || n_devices < 1 || !devices || !n_channels || ticks_per_push < 1 ||
+      vc->n_alt < 0 || (vc->n_alt > 0 && !vc->alt_vad_machine_configs))
+    return FVAD_EINVAL;
+  for (int s = 0; s < n_streams; s++)
+    if (n_channels[s] < 1 || n_channels[s] > FVAD_MAX_CHANNELS) return FVAD_EINVAL;
   fvad_multi *m = new fvad_multi();
   m->n_streams = n_streams;
-  m->n_channels = n_channels;
   m->ticks_per_push = ticks_per_push;
-  if (cfg)
-    m->cfg = *cfg;
-  else
-    fvad_vadm_config_default(&m->cfg);
-  for (int s = 0; s < n_streams; s++) {
-    StreamMachines x;
-    x.machines.emplace_back(m->cfg, 48000, 2048);
-    m->sm.push_back(std::move(x));
-  }
-  const int nd = std::min(n_devices, n_streams);
-  for (int d = 0; d < nd; d++) {
-    fvad_multi::Part p;
-    p.device = devices[d];
-    p.s0 = (int)((long)n_streams * d / nd);
-    p.s1 = (int)((long)n_streams * (d + 1) / nd);
-    fvad_engine_config_default(&p.ec, p.s1 - p.s0, n_channels);
-    p.ec.device = p.device;
-    p.ec.max_ticks = ticks_per_push;
-    std::vector<VADMachine> tmp{m->sm[p.s0].machines[0]};
-    assign_bands(tmp, p.ec);
-    for (int s = p.s0; s < p.s1; s++) m->sm[s].machines[0].band_slot = tmp[0].band_slot;
-    int rc = fvad_engine_create(&p.ec, model, &p.engine);
-    if (!rc) rc = fvad_engine_attach_vadm(p.engine, &m->cfg, 1, kMultiSegCap);
-    if (rc) {
-      if (p.engine) fvad_engine_destroy(p.engine);
-      fvad_multi_destroy(m);
-      return rc;
+  m->n_machines = 1 + vc->n_alt;
+  m->channels.assign(n_channels, n_channels + n_streams);
+  m->where.assign(n_streams, {-1, -1});
+  std::vector<VADMachine> ms;
+  ms.emplace_back(vc->vad_machine_config, 48000, vc->fft_size);
+  for (int i = 0; i < vc->n_alt; i++) ms.emplace_back(vc->alt_vad_machine_configs[i], 48000, vc->fft_size);
+  std::vector<fvad_vadm_config> cfgs;
+  for (auto &x : ms) cfgs.push_back(x.cfg);
+  std::vector<int> groups(m->channels);
+  std::sort(groups.begin(), groups.end());
+  groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
+  for (int C : groups) {
+    std::vector<int> ids;
+    for (int s = 0; s < n_streams; s++)
+      if (m->channels[s] == C) ids.push_back(s);
+    const int nd = std::min<int>(n_devices, (int)ids.size());
+    for (int d = 0; d < nd; d++) {
+      fvad_multi::Part p;
+      p.device = devices[d];
+      p.n_channels = C;
+      const size_t i0 = ids.size() * d / nd, i1 = ids.size() * (d + 1) / nd;
+      p.streams.assign(ids.begin() + i0, ids.begin() + i1);
+      fvad_engine_config_default(&p.ec, (int)p.streams.size(), C);
+      p.ec.device = p.device;
+      p.ec.max_ticks = ticks_per_push;
+      p.ec.fft_size = vc->fft_size;
+      p.ec.use_denoiser = vc->use_denoiser;
+      int rc = assign_bands(ms, p.ec);
+      if (!rc) rc = fvad_engine_create(&p.ec, model, &p.engine);
+      if (!rc) rc = fvad_engine_attach_vadm(p.engine, cfgs.data(), (int)cfgs.size(), kMultiSegCap);
+      if (rc) {
+        if (p.engine) fvad_engine_destroy(p.engine);
+        fvad_multi_destroy(m);
+        return rc;
+      }
+      for (size_t k = 0; k < p.streams.size(); k++) m->where[p.streams[k]] = {(int)m->parts.size(), (int)k};
+      m->parts.push_back(std::move(p));
     }
-    m->parts.push_back(p);
   }
   *out = m;
   return FVAD_OK;
+}
+
+extern "C" int fvad_multi_create(int n_streams, int n_channels, const fvad_model *model, const int *devices,
+                                 int n_devices, const fvad_vadm_config *cfg, int ticks_per_push, fvad_multi **out) {
+  if (n_streams < 1) return FVAD_EINVAL;
+  fvad_vad_config vc;
+  fvad_vad_config_default(&vc);
+  if (cfg) vc.vad_machine_config = *cfg;
+  std::vector<int> ch(n_streams, n_channels);
+  return fvad_multi_create_ex(n_streams, ch.data(), model, devices, n_devices, &vc, ticks_per_push, out);
 }
 
 extern "C" void fvad_multi_destroy(fvad_multi *m) {
@@ -526,39 +573,53 @@ extern "C" void fvad_multi_destroy(fvad_multi *m) {
   delete m;
 }
 
-extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size_t *len) {
-  if (!m || !pcm || !len) return FVAD_EINVAL;
-  const int C = m->n_channels;
+extern "C" int fvad_multi_run_stream(fvad_multi *m, fvad_read_fn read, void *ctx) {
+  if (!m || !read) return FVAD_EINVAL;
   std::vector<int> rcs(m->parts.size(), FVAD_OK);
   std::vector<std::thread> th;
   for (size_t pi = 0; pi < m->parts.size(); pi++) {
     th.emplace_back([&, pi]() {
-      // streaming: the next push is gathered straight into the engine's
-      // pinned input slot and submitted while the previous one still runs
-      // (fvad_engine_submit); no per-tick outputs come back, the VADMachines
-      // run on the device (k_vadm_hbm)
       fvad_multi::Part &p = m->parts[pi];
-      const int B = p.s1 - p.s0, T = p.ec.max_ticks;
-      size_t max_frames = 0;
-      for (int s = p.s0; s < p.s1; s++) max_frames = std::max(max_frames, len[s] / fvad::kFrame);
+      const int B = (int)p.streams.size(), T = p.ec.max_ticks, C = p.n_channels;
+      const size_t cap = (size_t)T * fvad::kFrame;
+      std::vector<float> tmp((size_t)C * cap);
+      std::vector<float *> dst(C);
+      for (int c = 0; c < C; c++) dst[c] = tmp.data() + (size_t)c * cap;
       std::vector<int32_t> valid(B);
-      int in_flight = 0, rc = FVAD_OK;
-      for (size_t f0 = 0; f0 < max_frames && !rc; f0 += T) {
-        const int nt = (int)std::min<size_t>(T, max_frames - f0);
+      std::vector<char> done(B, 0);
+      int in_flight = 0, rc = FVAD_OK, live = B;
+      while (live > 0 && !rc) {
         float *buf = fvad_engine_input_slot(p.engine);
         if (!buf) {
           rc = FVAD_EDEVICE;
           break;
         }
+        int nt = 0;
         for (int b = 0; b < B; b++) {
-          const int s = p.s0 + b;
-          const size_t frames_s = len[s] / fvad::kFrame;
-          valid[b] = (int)(frames_s > f0 ? std::min<size_t>(nt, frames_s - f0) : 0);
+          valid[b] = 0;
+          if (done[b]) continue;
+          // whole ticks only; a tail shorter than a frame is never processed
+          // (VAD.zig:219: the loop needs frame_size unread samples)
+          size_t got = 0;
+          while (got < cap) {
+            std::vector<float *> d(C);
+            for (int c = 0; c < C; c++) d[c] = dst[c] + got;
+            const size_t r = read(ctx, p.streams[b], d.data(), cap - got);
+            if (r == 0) break;
+            got += r;
+          }
+          if (got < cap) {
+            done[b] = 1;
+            live--;
+          }
+          valid[b] = (int)(got / fvad::kFrame);
+          nt = std::max(nt, valid[b]);
           for (int t = 0; t < valid[b]; t++)
             for (int c = 0; c < C; c++)
-              std::memcpy(&buf[(((size_t)t * B + b) * C + c) * fvad::kFrame],
-                          pcm[s] + (size_t)c * len[s] + (f0 + t) * fvad::kFrame, fvad::kFrame * sizeof(float));
+              std::memcpy(&buf[(((size_t)t * B + b) * C + c) * fvad::kFrame], dst[c] + (size_t)t * fvad::kFrame,
+                          fvad::kFrame * sizeof(float));
         }
+        if (nt == 0) break;
         if (in_flight == 2 && !(rc = fvad_engine_collect(p.engine, nullptr, nullptr))) in_flight--;
         if (!rc && !(rc = fvad_engine_submit(p.engine, buf, nt, valid.data()))) in_flight++;
       }
@@ -576,11 +637,38 @@ extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size
   return FVAD_OK;
 }
 
+namespace {
+struct MemReader {
+  const float *const *pcm;
+  const size_t *len;
+  const std::vector<int> *channels;
+  std::vector<size_t> pos;
+};
+size_t mem_read(void *ctx, int s, float *const *dst, size_t max_frames) {
+  MemReader *r = static_cast<MemReader *>(ctx);
+  const size_t n = std::min(max_frames, r->len[s] - r->pos[s]);
+  for (int c = 0; c < (*r->channels)[s]; c++)
+    std::memcpy(dst[c], r->pcm[s] + (size_t)c * r->len[s] + r->pos[s], n * sizeof(float));
+  r->pos[s] += n;
+  return n;
+}
+}  // namespace
+
+extern "C" int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size_t *len) {
+  if (!m || !pcm || !len) return FVAD_EINVAL;
+  MemReader r{pcm, len, &m->channels, std::vector<size_t>(m->n_streams, 0)};
+  return fvad_multi_run_stream(m, mem_read, &r);
+}
+
+extern "C" size_t fvad_multi_segments_alt(const fvad_multi *m, int stream, int machine, fvad_segment *out,
+                                          size_t cap) {
+  if (!m || stream < 0 || stream >= m->n_streams || machine < 0 || machine >= m->n_machines) return 0;
+  const auto &w = m->where[stream];
+  return fvad_engine_segments(m->parts[w.first].engine, w.second, machine, out, cap);
+}
+
 extern "C" size_t fvad_multi_segments(const fvad_multi *m, int stream, fvad_segment *out, size_t cap) {
-  if (!m || stream < 0 || stream >= m->n_streams) return 0;
-  for (const auto &p : m->parts)
-    if (stream >= p.s0 && stream < p.s1) return fvad_engine_segments(p.engine, stream - p.s0, 0, out, cap);
-  return 0;
+  return fvad_multi_segments_alt(m, stream, 0, out, cap);
 }
 
 // ---------------------------------------------------------------------------

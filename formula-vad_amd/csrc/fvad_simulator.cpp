@@ -10,7 +10,12 @@
 //   SimulationInstance.zig:91-95).  Audio: WAV (PCM 16/24/32-bit or float32,
 //   48 kHz) — libsndfile/ogg are not available, see DESIGN.md.
 //   Instances run in lock-step on the GPU(s) (simulator.zig:217-228 spawns one
-//   thread per instance instead).  Statistics use
+//   thread per instance instead), streamed from their files push by push
+//   (preload_audio: read whole first); any even fft_size >= 480,
+//   use_denoiser, alternative machines (run on the device; like the
+//   reference, only the main machine's segments are reported); instances may
+//   differ in channel count.  audio_read_frame_count does not change results
+//   (the pipeline is chunking-invariant) and is not used.  Statistics use
 //   {ignore_shorter_than = min_vad_duration_sec, extrude 5/10, fill gaps 5}
 //   (simulator.zig:123-128); the report follows report_generator.zig:29-116.
 #include <algorithm>
@@ -218,71 +223,112 @@ bool write_wav_f32(const std::string &path, const float *x, size_t n, int sample
 }
 
 // ---------------- WAV ingest (AudioFileStream replacement) ----------------
-struct Audio {
-  int channels = 0, sample_rate = 0;
-  std::vector<float> planar;  // [ch][n]
-  size_t n = 0;
-};
+// Streams frames from the file (AudioFileStream.zig:56-98 over libsndfile):
+// the header is parsed once, read() converts the next frames to planar f32,
+// read_at() re-reads a range (the Recorder's capture of a segment).
+// preload_audio (simulator.zig:41-42) reads the whole file into memory first.
+struct WavStream {
+  FILE *f = nullptr;
+  int channels = 0, sample_rate = 0, fmt = 0, bits = 0, bps = 0;
+  long long data_off = 0;
+  size_t n = 0, pos = 0;        // frames in the file, next frame to read
+  std::vector<float> pre;       // preloaded planar [ch][n] (preload_audio)
+  std::vector<unsigned char> raw;
 
-bool read_wav(const std::string &path, Audio &au, std::string &err) {
-  std::string d;
-  if (!read_file(path, d)) {
-    err = "cannot open " + path;
-    return false;
+  ~WavStream() {
+    if (f) std::fclose(f);
   }
-  auto u32 = [&](size_t o) { return (uint32_t)(uint8_t)d[o] | (uint32_t)(uint8_t)d[o + 1] << 8 |
-                                    (uint32_t)(uint8_t)d[o + 2] << 16 | (uint32_t)(uint8_t)d[o + 3] << 24; };
-  auto u16 = [&](size_t o) { return (uint32_t)(uint8_t)d[o] | (uint32_t)(uint8_t)d[o + 1] << 8; };
-  if (d.size() < 12 || d.compare(0, 4, "RIFF") != 0 || d.compare(8, 4, "WAVE") != 0) {
-    err = path + ": not a RIFF/WAVE file (only WAV is supported without libsndfile)";
-    return false;
-  }
-  int fmt = 0, bits = 0;
-  size_t pos = 12, data_off = 0, data_len = 0;
-  while (pos + 8 <= d.size()) {
-    const uint32_t len = u32(pos + 4);
-    if (d.compare(pos, 4, "fmt ") == 0) {
-      fmt = (int)u16(pos + 8);
-      au.channels = (int)u16(pos + 10);
-      au.sample_rate = (int)u32(pos + 12);
-      bits = (int)u16(pos + 22);
-      if (fmt == 0xFFFE && len >= 40) fmt = (int)u16(pos + 32);  // WAVE_FORMAT_EXTENSIBLE subformat
-    } else if (d.compare(pos, 4, "data") == 0) {
-      data_off = pos + 8;
-      data_len = std::min<size_t>(len, d.size() - data_off);
+  bool open(const std::string &path, std::string &err) {
+    f = std::fopen(path.c_str(), "rb");
+    if (!f) {
+      err = "cannot open " + path;
+      return false;
     }
-    pos += 8 + len + (len & 1);
-  }
-  if (!data_off || au.channels < 1) {
-    err = path + ": missing fmt/data chunk";
-    return false;
-  }
-  const int bps = bits / 8;
-  if (!((fmt == 1 && (bits == 16 || bits == 24 || bits == 32)) || (fmt == 3 && bits == 32))) {
-    err = path + ": unsupported WAV encoding";
-    return false;
-  }
-  au.n = data_len / ((size_t)bps * au.channels);
-  au.planar.assign((size_t)au.channels * au.n, 0.0f);
-  for (size_t i = 0; i < au.n; i++)
-    for (int c = 0; c < au.channels; c++) {
-      const size_t o = data_off + (i * au.channels + c) * bps;
-      float v;
-      if (fmt == 3) {
-        uint32_t u = u32(o);
-        std::memcpy(&v, &u, 4);
-      } else if (bits == 16) {
-        v = (float)(int16_t)u16(o) / 32768.0f;  // libsndfile short->float normalisation
-      } else if (bits == 24) {
-        int32_t x = (int32_t)(u16(o) | ((uint32_t)(uint8_t)d[o + 2] << 16)) << 8;
-        v = (float)((double)x / 2147483648.0);
-      } else {
-        v = (float)((double)(int32_t)u32(o) / 2147483648.0);
+    unsigned char h[12];
+    if (std::fread(h, 1, 12, f) != 12 || std::memcmp(h, "RIFF", 4) || std::memcmp(h + 8, "WAVE", 4)) {
+      err = path + ": not a RIFF/WAVE file (only WAV is supported without libsndfile)";
+      return false;
+    }
+    long long data_len = -1;
+    unsigned char ck[8];
+    while (std::fread(ck, 1, 8, f) == 8) {
+      const uint32_t len = le32(ck + 4);
+      const long long body = std::ftell(f);
+      if (!std::memcmp(ck, "fmt ", 4)) {
+        unsigned char fm[40] = {};
+        if (std::fread(fm, 1, std::min<uint32_t>(len, 40), f) < 16) break;
+        fmt = (int)le16(fm);
+        channels = (int)le16(fm + 2);
+        sample_rate = (int)le32(fm + 4);
+        bits = (int)le16(fm + 14);
+        if (fmt == 0xFFFE && len >= 40) fmt = (int)le16(fm + 24);  // WAVE_FORMAT_EXTENSIBLE subformat
+      } else if (!std::memcmp(ck, "data", 4)) {
+        data_off = body;
+        data_len = len;
+        break;
       }
-      au.planar[(size_t)c * au.n + i] = v;
+      std::fseek(f, body + len + (len & 1), SEEK_SET);
     }
-  return true;
-}
+    if (data_len < 0 || channels < 1) {
+      err = path + ": missing fmt/data chunk";
+      return false;
+    }
+    if (!((fmt == 1 && (bits == 16 || bits == 24 || bits == 32)) || (fmt == 3 && bits == 32))) {
+      err = path + ": unsupported WAV encoding";
+      return false;
+    }
+    bps = bits / 8;
+    std::fseek(f, 0, SEEK_END);
+    const long long avail = std::ftell(f) - data_off;
+    n = (size_t)(std::min(data_len, avail) / ((long long)bps * channels));
+    std::fseek(f, data_off, SEEK_SET);
+    return true;
+  }
+  static uint32_t le16(const unsigned char *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
+  static uint32_t le32(const unsigned char *p) { return le16(p) | le16(p + 2) << 16; }
+  float sample(const unsigned char *o) const {
+    float v;
+    if (fmt == 3) {
+      uint32_t u = le32(o);
+      std::memcpy(&v, &u, 4);
+    } else if (bits == 16) {
+      v = (float)(int16_t)le16(o) / 32768.0f;  // libsndfile short->float normalisation
+    } else if (bits == 24) {
+      const int32_t x = (int32_t)(le16(o) | (uint32_t)o[2] << 16) << 8;
+      v = (float)((double)x / 2147483648.0);
+    } else {
+      v = (float)((double)(int32_t)le32(o) / 2147483648.0);
+    }
+    return v;
+  }
+  // frames [from, from + k) into dst[c][0..k)
+  size_t read_at(size_t from, float *const *dst, size_t k) {
+    if (from >= n) return 0;
+    k = std::min(k, n - from);
+    if (!pre.empty()) {
+      for (int c = 0; c < channels; c++) std::memcpy(dst[c], pre.data() + (size_t)c * n + from, k * sizeof(float));
+      return k;
+    }
+    raw.resize(k * bps * channels);
+    std::fseek(f, data_off + (long long)from * bps * channels, SEEK_SET);
+    k = std::fread(raw.data(), (size_t)bps * channels, k, f);
+    for (size_t i = 0; i < k; i++)
+      for (int c = 0; c < channels; c++) dst[c][i] = sample(raw.data() + (i * channels + c) * bps);
+    return k;
+  }
+  size_t read(float *const *dst, size_t k) {
+    const size_t r = read_at(pos, dst, k);
+    pos += r;
+    return r;
+  }
+  void preload() {
+    std::vector<float> buf((size_t)channels * n, 0.0f);
+    std::vector<float *> d(channels);
+    for (int c = 0; c < channels; c++) d[c] = buf.data() + (size_t)c * n;
+    (void)read_at(0, d.data(), n);  // from the file (pre is still empty)
+    pre.swap(buf);
+  }
+};
 
 float num(const Json *j, float def) { return (j && j->kind == Json::Num) ? (float)j->n : def; }
 
@@ -386,15 +432,31 @@ extern "C" int fvad_simulator_main(int argc, char **argv) {
   const std::string base = dirname_of(plan_path);
   const Json *cfg = plan.get("config");
   const Json *vcfg = cfg ? cfg->get("vad_config") : nullptr;
-  fvad_vadm_config mcfg;
+  // VAD.Config (VAD.zig:17-23) and the simulator's own options (simulator.zig:37-45)
+  fvad_vad_config vc;
+  fvad_vad_config_default(&vc);
+  fvad_vadm_config &mcfg = vc.vad_machine_config;
   vadm_from_json(vcfg ? vcfg->get("vad_machine_config") : nullptr, mcfg);
+  std::vector<fvad_vadm_config> alts;
+  bool preload = false;
   if (vcfg) {
     const Json *fs = vcfg->get("fft_size");
     const Json *ud = vcfg->get("use_denoiser");
-    if ((fs && fs->kind == Json::Num && fs->n != 2048) || (ud && ud->kind == Json::Bool && !ud->b)) {
-      std::printf("Failed to initialize simulation: only fft_size=2048 with the denoiser is supported on the GPU path\n");
-      return 1;
-    }
+    const Json *al = vcfg->get("alt_vad_machine_configs");
+    if (fs && fs->kind == Json::Num) vc.fft_size = (int)fs->n;
+    if (ud && ud->kind == Json::Bool) vc.use_denoiser = ud->b ? 1 : 0;
+    if (al && al->kind == Json::Arr)
+      for (const Json &aj : al->a) {
+        fvad_vadm_config c;
+        vadm_from_json(&aj, c);
+        alts.push_back(c);
+      }
+  }
+  vc.alt_vad_machine_configs = alts.empty() ? nullptr : alts.data();
+  vc.n_alt = (int)alts.size();
+  if (cfg) {
+    const Json *pl = cfg->get("preload_audio");
+    if (pl && pl->kind == Json::Bool) preload = pl->b;
   }
   // output directory <base>/<output_dir>/<unix ts>/ (simulator.zig:153-172)
   std::string out_dir;
@@ -408,12 +470,11 @@ extern "C" int fvad_simulator_main(int argc, char **argv) {
   }
   struct Inst {
     std::string name;
-    Audio audio;
+    WavStream audio;
     std::vector<float> refs;
     std::vector<fvad_segment> segs;
   };
   std::vector<Inst> inst(insts->a.size());
-  int channels = -1;
   for (size_t k = 0; k < insts->a.size(); k++) {
     const Json &ij = insts->a[k];
     const Json *nm = ij.get("name"), *ap = ij.get("audio_path"), *rp = ij.get("ref_path");
@@ -423,7 +484,7 @@ extern "C" int fvad_simulator_main(int argc, char **argv) {
     }
     inst[k].name = nm->s;
     std::string err;
-    if (!read_wav(join(base, ap->s), inst[k].audio, err)) {
+    if (!inst[k].audio.open(join(base, ap->s), err)) {
       std::printf("Failed to initialize simulation: %s\n", err.c_str());
       return 1;
     }
@@ -431,11 +492,7 @@ extern "C" int fvad_simulator_main(int argc, char **argv) {
       std::printf("Failed to initialize simulation: error.InvalidSampleRate\n");
       return 1;
     }
-    if (channels < 0) channels = inst[k].audio.channels;
-    if (channels != inst[k].audio.channels) {
-      std::printf("Failed to initialize simulation: all instances must have the same channel count\n");
-      return 1;
-    }
+    if (preload) inst[k].audio.preload();
     std::string ref_txt;
     if (!read_file(join(base, rp->s), ref_txt)) {
       std::printf("Failed to initialize simulation: error.FileNotFound (%s)\n", rp->s.c_str());
@@ -457,22 +514,23 @@ extern "C" int fvad_simulator_main(int argc, char **argv) {
   }
   if (!inst.empty()) {
     fvad_multi *multi = nullptr;
-    rc = fvad_multi_create((int)inst.size(), channels, model, devices.data(), (int)devices.size(), &mcfg, 100,
-                           &multi);
+    std::vector<int> chans(inst.size());
+    for (size_t k = 0; k < inst.size(); k++) chans[k] = inst[k].audio.channels;
+    rc = fvad_multi_create_ex((int)inst.size(), chans.data(), model, devices.data(), (int)devices.size(), &vc, 100,
+                              &multi);
     if (rc) {
       std::printf("simulation failed: %s\n", fvad_last_error());
       fvad_model_free(model);
       return 1;
     }
-    std::vector<const float *> pcm(inst.size());
-    std::vector<size_t> len(inst.size());
-    for (size_t k = 0; k < inst.size(); k++) {
-      pcm[k] = inst[k].audio.planar.data();
-      len[k] = inst[k].audio.n;
-      std::fprintf(stderr, "info(sim_instance): %s: Streaming %.2fs from audio file. Running...\n",
-                   inst[k].name.c_str(), (double)inst[k].audio.n / 48000.0);
-    }
-    rc = fvad_multi_run(multi, pcm.data(), len.data());
+    for (auto &I : inst)
+      std::fprintf(stderr, "info(sim_instance): %s: Streaming %.2fs from audio file. Running...\n", I.name.c_str(),
+                   (double)I.audio.n / 48000.0);
+    // the read loop: each part thread pulls its instances' next frames
+    auto reader = [](void *ctx, int s, float *const *dst, size_t max_frames) -> size_t {
+      return (*static_cast<std::vector<Inst> *>(ctx))[s].audio.read(dst, max_frames);
+    };
+    rc = fvad_multi_run_stream(multi, reader, &inst);
     if (rc) {
       std::printf("simulation failed: %s\n", fvad_last_error());
       fvad_multi_destroy(multi);
@@ -491,11 +549,16 @@ extern "C" int fvad_simulator_main(int argc, char **argv) {
     if (!out_dir.empty()) {
       for (auto &I : inst) {
         size_t count = 0;
+        const int channels = I.audio.channels;
+        std::vector<float> buf;
+        std::vector<float *> dst(channels);
         std::vector<const float *> ch(channels);
         for (auto &sg : I.segs) {
           if (sg.sample_to > I.audio.n || sg.sample_to <= sg.sample_from) continue;
           const size_t len = (size_t)(sg.sample_to - sg.sample_from);
-          for (int c = 0; c < channels; c++) ch[c] = I.audio.planar.data() + (size_t)c * I.audio.n + sg.sample_from;
+          buf.assign((size_t)channels * len, 0.0f);
+          for (int c = 0; c < channels; c++) ch[c] = dst[c] = buf.data() + (size_t)c * len;
+          if (I.audio.read_at(sg.sample_from, dst.data(), len) != len) continue;
           const int best = fvad_recording_channel(ch.data(), channels, len);
           char nm[32];
           std::snprintf(nm, sizeof nm, "%03zu-", count++);

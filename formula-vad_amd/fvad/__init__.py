@@ -62,6 +62,29 @@ class VadmConfig(C.Structure):
         return c
 
 
+class VadConfig(C.Structure):
+    """VAD.Config (VAD.zig:17-23)."""
+    _fields_ = [("fft_size", C.c_int), ("use_denoiser", C.c_int), ("vad_machine_config", VadmConfig),
+                ("alt_vad_machine_configs", C.c_void_p), ("n_alt", C.c_int)]
+
+    @classmethod
+    def make(cls, fft_size=2048, use_denoiser=True, main_cfg=None, alt_cfgs=()):
+        c = cls()
+        lib().fvad_vad_config_default(C.byref(c))
+        c.fft_size = fft_size
+        c.use_denoiser = int(use_denoiser)
+        if main_cfg is not None:
+            c.vad_machine_config = main_cfg
+        arr = (VadmConfig * max(1, len(alt_cfgs)))(*alt_cfgs)
+        c._alts = arr
+        c.alt_vad_machine_configs = C.cast(arr, C.c_void_p) if alt_cfgs else None
+        c.n_alt = len(alt_cfgs)
+        return c
+
+
+READ_FN = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.c_int, C.POINTER(F32P), C.c_size_t)
+
+
 class Segment(C.Structure):
     _fields_ = [("sample_from", C.c_uint64), ("sample_to", C.c_uint64), ("debug_rnn_vad", C.c_float),
                 ("debug_avg_speech_vol_ratio", C.c_float)]
@@ -147,6 +170,12 @@ SYMBOLS = [
     ("fvad_pipeline_set_recorder", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fvad_multi_create", C.c_int, [C.c_int, C.c_int, C.c_void_p, I32P, C.c_int, C.c_void_p, C.c_int,
                                     C.POINTER(C.c_void_p)]),
+    ("fvad_multi_create_ex", C.c_int, [C.c_int, I32P, C.c_void_p, I32P, C.c_int, C.c_void_p, C.c_int,
+                                       C.POINTER(C.c_void_p)]),
+    ("fvad_multi_run_stream", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fvad_multi_segments_alt", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
+    ("fvad_vad_config_default", None, [C.c_void_p]),
+    ("fvad_pipeline_create_ex", C.c_int, [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("fvad_multi_destroy", None, [C.c_void_p]),
     ("fvad_multi_run", C.c_int, [C.c_void_p, C.POINTER(F32P), C.POINTER(C.c_size_t)]),
     ("fvad_multi_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
@@ -496,18 +525,38 @@ class AudioPipeline:
 
 
 class Multi:
-    """Multi-stream simulator core: lock-step ticks, streams partitioned over devices."""
+    """Multi-stream simulator core: lock-step ticks, streams grouped by channel
+    count and partitioned over devices (fvad_multi_create_ex)."""
 
-    def __init__(self, model, n_streams, n_channels=2, devices=(0,), cfg=None, ticks_per_push=50):
+    def __init__(self, model, n_streams, n_channels=2, devices=(0,), cfg=None, ticks_per_push=50, fft_size=2048,
+                 use_denoiser=True, alt_cfgs=()):
         self.model = model
         self.n = n_streams
         d = np.ascontiguousarray(devices, np.int32)
-        c = cfg if cfg is not None else VadmConfig.default()
-        self._keep = (d, c)
+        ch = np.ascontiguousarray([n_channels] * n_streams if np.isscalar(n_channels) else n_channels, np.int32)
+        vc = VadConfig.make(fft_size, use_denoiser, cfg, tuple(alt_cfgs))
+        self._keep = (d, ch, vc)
         h = C.c_void_p()
-        _check(lib().fvad_multi_create(n_streams, n_channels, model.h, d.ctypes.data_as(I32P), len(d), C.byref(c),
-                                       ticks_per_push, C.byref(h)), "fvad_multi_create")
+        _check(lib().fvad_multi_create_ex(n_streams, ch.ctypes.data_as(I32P), model.h, d.ctypes.data_as(I32P), len(d),
+                                          C.byref(vc), ticks_per_push, C.byref(h)), "fvad_multi_create_ex")
         self.h = h
+
+    def run_stream(self, streams, chunk=48000):
+        """Pull each stream through fvad_multi_run_stream in reads of at most
+        `chunk` frames (the simulator's streaming read loop)."""
+        arrs = [np.ascontiguousarray(s, np.float32) for s in streams]
+        pos = [0] * len(arrs)
+
+        def read(ctx, s, dst, max_frames):
+            a = arrs[s]
+            k = min(max_frames, chunk, a.shape[1] - pos[s])
+            for c in range(a.shape[0]):
+                C.memmove(dst[c], a[c, pos[s]:].ctypes.data, k * 4)
+            pos[s] += k
+            return k
+
+        cb = READ_FN(read)
+        _check(lib().fvad_multi_run_stream(self.h, C.cast(cb, C.c_void_p), None), "fvad_multi_run_stream")
 
     def run(self, streams):
         """streams: list of planar float32 arrays [ch][len]."""
@@ -516,10 +565,10 @@ class Multi:
         lens = (C.c_size_t * len(arrs))(*[a.shape[1] for a in arrs])
         _check(lib().fvad_multi_run(self.h, ptrs, lens), "fvad_multi_run")
 
-    def segments(self, stream):
-        n = lib().fvad_multi_segments(self.h, stream, None, 0)
+    def segments(self, stream, machine=0):
+        n = lib().fvad_multi_segments_alt(self.h, stream, machine, None, 0)
         buf = (Segment * max(1, n))()
-        lib().fvad_multi_segments(self.h, stream, buf, n)
+        lib().fvad_multi_segments_alt(self.h, stream, machine, buf, n)
         return [(s.sample_from, s.sample_to, s.debug_rnn_vad, s.debug_avg_speech_vol_ratio) for s in buf[:n]]
 
     def __del__(self):

@@ -235,12 +235,25 @@ size_t fvad_engine_segments_range(fvad_engine *e, int stream, int machine, size_
 int fvad_engine_vadm_state(fvad_engine *e, int stream, int machine, int *speech_state, uint64_t *speech_start,
                            uint64_t *speech_end);
 
+/* VAD.Config (VAD.zig:17-23) */
+typedef struct {
+  int fft_size;                                     /* even, 480..16384 (FFT.zig:28-31) */
+  int use_denoiser;                                 /* 0: fft_size frames of raw input to FFT B */
+  fvad_vadm_config vad_machine_config;              /* main machine */
+  const fvad_vadm_config *alt_vad_machine_configs;  /* alternative machines (training), nullable */
+  int n_alt;                                        /* <= FVAD_MAX_BANDS - 1 */
+} fvad_vad_config;
+void fvad_vad_config_default(fvad_vad_config *c);
+
 /* AudioPipeline (AudioPipeline.zig:20-26,39-120) for one stream, backed by a
  * 1-stream engine.  n_alt alternative VADMachine configs (VAD.zig:20-23). */
 typedef struct fvad_pipeline fvad_pipeline;
 int fvad_pipeline_create(int sample_rate, int n_channels, const fvad_model *model, int device,
                          const fvad_vadm_config *main_cfg, const fvad_vadm_config *alt_cfgs, int n_alt,
                          fvad_pipeline **out);
+/* the same with a whole VAD.Config (fft_size, use_denoiser, machines) */
+int fvad_pipeline_create_ex(int sample_rate, int n_channels, const fvad_model *model, int device,
+                            const fvad_vad_config *vad_config, fvad_pipeline **out);
 void fvad_pipeline_destroy(fvad_pipeline *p);
 /* pushSamples: planar channel pointers, n samples each; *first_index receives
  * the absolute index of the first pushed sample (AudioPipeline.zig:86-120) */
@@ -259,14 +272,28 @@ int fvad_recording_channel(const float *const *channel_pcm, int n_channels, size
 typedef void (*fvad_recording_fn)(void *ctx, const float *pcm, size_t n, uint64_t start_sample, int channel);
 int fvad_pipeline_set_recorder(fvad_pipeline *p, fvad_recording_fn fn, void *ctx);
 
-/* Multi-stream simulator core: n streams processed in lockstep on the given
- * devices (one engine per device, streams partitioned contiguously).
- * pcm[s] points to planar [channels][len[s]] audio of stream s. */
+/* Multi-stream simulator core (simulator.zig:217-228 runs one thread per
+ * instance): streams grouped by channel count, each group partitioned
+ * contiguously over the devices, one engine + host thread per part, lock-step
+ * pushes of ticks_per_push ticks.  pcm[s] points to planar [channels][len[s]]
+ * audio of stream s (fvad_multi_run), or a reader pulls it push by push
+ * (fvad_multi_run_stream: the simulator's streaming read loop,
+ * SimulationInstance.zig:171-203). */
 typedef struct fvad_multi fvad_multi;
 int fvad_multi_create(int n_streams, int n_channels, const fvad_model *model, const int *devices,
                       int n_devices, const fvad_vadm_config *cfg, int ticks_per_push, fvad_multi **out);
+/* per-stream channel counts and a whole VAD.Config */
+int fvad_multi_create_ex(int n_streams, const int *n_channels, const fvad_model *model, const int *devices,
+                         int n_devices, const fvad_vad_config *vad_config, int ticks_per_push, fvad_multi **out);
 void fvad_multi_destroy(fvad_multi *m);
 int fvad_multi_run(fvad_multi *m, const float *const *pcm, const size_t *len);
+/* reader: write up to max_frames frames of stream `stream` planar into
+ * channel_dst[c][0..), return the count (0 = end of stream).  Called from the
+ * part threads; a stream is always read by the same thread, in order. */
+typedef size_t (*fvad_read_fn)(void *ctx, int stream, float *const *channel_dst, size_t max_frames);
+int fvad_multi_run_stream(fvad_multi *m, fvad_read_fn read, void *ctx);
+/* segments of the main machine (machine 0) or alternative machine i (machine i + 1) */
+size_t fvad_multi_segments_alt(const fvad_multi *m, int stream, int machine, fvad_segment *out, size_t cap);
 size_t fvad_multi_segments(const fvad_multi *m, int stream, fvad_segment *out, size_t cap);
 
 /* Evaluator / statistics (Evaluator.zig:90-156, statistics.zig:85-284) */

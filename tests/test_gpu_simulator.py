@@ -109,3 +109,72 @@ def test_simulator_bad_plan(tmp_path):
                                         '"ref_path": "missing.txt"}]}')
     r = subprocess.run([SIM, "-i", str(tmp_path / "plan.json")], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "Failed to initialize simulation" in r.stdout
+
+
+@pytest.mark.parametrize("fft_size,use_denoiser,preload", [(1000, True, False), (2048, False, True),
+                                                           (3000, False, False)])
+def test_simulator_vad_config(fvad_mod, oracle_mod, tmp_path, fft_size, use_denoiser, preload):
+    """plan.json with a non-default VAD.Config (VAD.zig:17-23): fft_size,
+    use_denoiser, alternative machines; instances of different channel counts
+    (mono and stereo), streamed or preloaded.  Segments and TP/FP/FN equal the
+    oracle's AudioPipeline with the same config."""
+    alt = {"speech_threshold_factor": 9.0, "min_vad_duration_sec": 0.5}
+    main = {"speech_threshold_factor": 15.0}
+    plan = {"instances": [], "config": {"vad_config": {"fft_size": fft_size, "use_denoiser": use_denoiser,
+                                                       "vad_machine_config": main,
+                                                       "alt_vad_machine_configs": [alt]},
+                                        "preload_audio": preload}}
+    truth = {}
+    for i, secs, ch in ((0, 41.0, 2), (7, 33.7, 1), (19, 28.0, 2)):
+        x, lab = fvad_mod.synth_stream(i, int(48000 * secs), ch)
+        write_wav(tmp_path / ("s%d.wav" % i), x)
+        (tmp_path / ("s%d.txt" % i)).write_text("".join("%f\t%f\tspeech\n" % (a, b) for a, b in lab))
+        plan["instances"].append({"name": "i%d" % i, "audio_path": "s%d.wav" % i, "ref_path": "s%d.txt" % i})
+        truth["i%d" % i] = (x, oracle_mod.parse_audacity((tmp_path / ("s%d.txt" % i)).read_text()))
+    (tmp_path / "plan.json").write_text(json.dumps(plan))
+    js = tmp_path / "summary.json"
+    r = subprocess.run([SIM, "-i", str(tmp_path / "plan.json")], capture_output=True, text=True,
+                       env=dict(os.environ, FVAD_SIM_JSON=str(js)), timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(js.read_text())
+    om = oracle_mod.Model(seed=1)
+    mcfg = oracle_mod.VadmConfig.default()
+    mcfg.speech_threshold_factor = 15.0
+    acfg = oracle_mod.VadmConfig.default()
+    acfg.speech_threshold_factor, acfg.min_vad_duration_sec = 9.0, 0.5
+    for inst in out["instances"]:
+        x, refs = truth[inst["name"]]
+        p = oracle_mod.Pipeline(x.shape[0], om, fft_size=fft_size, use_denoiser=use_denoiser, main_cfg=mcfg,
+                                alt_cfgs=(acfg,))
+        for k in range(0, x.shape[1], 48000):
+            p.push([x[c, k:k + 48000] for c in range(x.shape[0])])
+        ref_segs = [(a, b) for a, b, _, _ in p.segments()]
+        assert [tuple(s) for s in inst["segments"]] == ref_segs, inst["name"]
+        st = oracle_mod.evaluate([(a / 48000.0, b / 48000.0) for a, b in ref_segs], refs, 0.7, 5, 10, 5)
+        for k in ("tp", "fp", "fn"):
+            key = {"tp": "true_positives_sec", "fp": "false_positives_sec", "fn": "false_negatives_sec"}[k]
+            assert np.float32(inst[k]) == np.float32(st[key])
+
+
+def test_multi_stream_reader_alt_machines(fvad_mod, oracle_mod):
+    """fvad_multi_run_stream (the streaming read loop) with mono and stereo
+    streams in one multi (two channel groups) and an alternative machine:
+    main and alternative segments equal the oracle's."""
+    m, om = fvad_mod.Model(seed=1), oracle_mod.Model(seed=1)
+    specs = [(0, 30.0, 2), (1, 21.3, 1), (2, 30.0, 2), (19, 17.1, 1), (5, 26.0, 2)]
+    streams = [fvad_mod.synth_stream(i, int(48000 * s), c)[0] for i, s, c in specs]
+    alt_f = fvad_mod.VadmConfig.default()
+    alt_f.speech_threshold_factor = 9.0
+    alt_o = oracle_mod.VadmConfig.default()
+    alt_o.speech_threshold_factor = 9.0
+    multi = fvad_mod.Multi(m, len(streams), [c for _, _, c in specs], devices=(0, 0), ticks_per_push=40,
+                           alt_cfgs=(alt_f,))
+    multi.run_stream(streams, chunk=48000 - 17)
+    n = 0
+    for s, x in enumerate(streams):
+        p = oracle_mod.Pipeline(x.shape[0], om, alt_cfgs=(alt_o,))
+        p.push([x[c] for c in range(x.shape[0])])
+        assert multi.segments(s) == p.segments(), s
+        assert multi.segments(s, 1) == p.segments(0), s
+        n += len(p.segments()) + len(p.segments(0))
+    assert n > 3
