@@ -271,7 +271,7 @@ constexpr int kLpRows = 2 * kLpStep;      // 16 samples; sample 2*n0-1 is carrie
 constexpr int kLpPR = kLpRows / 4;        // float4 per stream row of a chunk (= loads per lane)
 constexpr int kLpSPI = 64 / kLpPR;        // streams per load instruction
 constexpr int kLpCols = 64 + kLpSPI / 4;  // 4 * pitch = kLpSPI (mod 64): writes hit distinct banks
-constexpr int kLpChunks = kXlp / kLpStep;  // 54
+constexpr int kLpChunks = kXlp / kLpStep;  // 108
 static_assert(kXlp % kLpStep == 0, "x_lp chunking");
 
 struct LpSrc {
@@ -311,15 +311,6 @@ __device__ __forceinline__ float lp_value(const float *col, int u, float &s_prev
   return x;
 }
 
-// xf rows r = n0 - 480 + u of chunk n0 that the Syy recurrences read back
-__device__ __forceinline__ void plpc_back(const float *out, int n0, float (&bk)[kLpStep]) {
-#pragma unroll
-  for (int u = 0; u < kLpStep; u++) {
-    const int r = n0 + u - 480;
-    bk[u] = (r >= 0 && r < 294) ? out[r * ptile::kQuarter] : 0.0f;
-  }
-}
-
 // pass-2 state of one lane (k_plpc)
 struct Fir5State {
   float l[5];
@@ -328,14 +319,66 @@ struct Fir5State {
   float Sc = 1.0f, Sf = 1.0f, xx = 0.0f;
 };
 
+// Row stores of the tile buffer go through a per-wave LDS stage: a chunk's
+// rows (one value per lane each) are written to LDS [row][lane], then each
+// lane stores two float4 of its quarter's [row][16] block, so one store
+// instruction writes 1 KB in four 256-byte runs instead of 256 bytes in four
+// 64-byte pieces (measured: the per-step dword row stores cost k_plpc ~0.4 ms).
+// Row loads of the read-back (pass 2: xf[n - 480]; pass 3: the yy operands)
+// take the same route backwards: two float4 per lane of the quarter's block,
+// then LDS, then each lane reads its column.
+struct OutStage {
+  float xf[kLpStep][64];      // xf rows of the chunk (pass 2), yy rows (pass 3)
+  float sf[kLpStep][64];      // fine Syy rows
+  float sc[kLpStep / 2][64];  // coarse Syy rows
+  float in[kLpStep][64];      // read-back rows (pass 2), x[-i] rows (pass 3)
+  float in2[kLpStep][64];     // x[480 - i] rows (pass 3)
+};
+struct RowLd {
+  float4 v[2];
+};
+template <int NR>
+__device__ __forceinline__ void fetch_rows(const float *qbase, int row0, RowLd &r, int lane) {
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int j = (lane & 15) + 16 * k, u = j >> 2, c4 = j & 3;
+    r.v[k] = u < NR ? *reinterpret_cast<const float4 *>(qbase + (row0 + u) * ptile::kQuarter + 4 * c4)
+                    : make_float4(0, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void stage_rows(const RowLd &r, float (*ob)[64], int lane) {
+  const int q = lane >> 4;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int j = (lane & 15) + 16 * k, u = j >> 2, c4 = j & 3;
+    *reinterpret_cast<float4 *>(&ob[u][16 * q + 4 * c4]) = r.v[k];
+  }
+}
+// rows row0 .. row0 + NR - 1 of the lane's quarter (qbase = its [row][16] block)
+template <int NR>
+__device__ __forceinline__ void flush_rows(float *qbase, int row0, const float (*ob)[64], int lane) {
+  const int q = lane >> 4;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int j = (lane & 15) + 16 * k, u = j >> 2, c4 = j & 3;
+    if (u < NR)
+      *reinterpret_cast<float4 *>(qbase + (row0 + u) * ptile::kQuarter + 4 * c4) =
+          *reinterpret_cast<const float4 *>(&ob[u][16 * q + 4 * c4]);
+  }
+}
+
 // One chunk of pass 2.  Region R of n = n0 .. n0+7:
 //   1 [0, 384)    Syy initial sums      2 [384, 480)  + xx
 //   3 [480, 774)  xx + Syy recurrences  4 the chunk holding n = 773 (guarded)
 //   5 [774, 864)  xx only
 template <bool First, int R>
-__device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, float *out, int n0,
-                                           const float (&bk)[kLpStep]) {
-  float *xo = out + (ptile::kXf + n0) * ptile::kQuarter;
+__device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, float *qbase, int n0,
+                                           const RowLd &bk, OutStage &ob, int lane) {
+  constexpr int kR4 = (480 + 294) % kLpStep;  // region 4 starts at a chunk boundary
+  if (R == 3 || R == 4) {
+    stage_rows(bk, ob.in, lane);
+    wave_sync();
+  }
 #pragma unroll
   for (int u = 0; u < kLpStep; u++) {
     const float x = lp_value<First>(col, u, f.sp);
@@ -346,37 +389,89 @@ __device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, float
     y = y + f.l[3] * f.m4;
     y = y + f.l[4] * f.m5;
     f.m5 = f.m4, f.m4 = f.m3, f.m3 = f.m2, f.m2 = f.m1, f.m1 = x;
-    xo[u * ptile::kQuarter] = y;
+    ob.xf[u][lane] = y;
     if (R <= 2) {
       if ((u & 1) == 0) f.Sc = f.Sc + y * y;  // n0 is a multiple of 8: n even <=> u even
       f.Sf = f.Sf + y * y;
     }
-    if (R == 3 || (R == 4 && u < (480 + 294) % kLpStep)) {  // region 4 starts at a chunk boundary
-      const int i = n0 + u - 480;
-      const float yb = bk[u];
-      out[(ptile::kSf + i) * ptile::kQuarter] = f.Sf;
+    if (R == 3 || (R == 4 && u < kR4)) {
+      const float yb = ob.in[u][lane];
+      ob.sf[u][lane] = f.Sf;
       f.Sf += y * y - yb * yb;
       f.Sf = (1 > f.Sf) ? 1 : f.Sf;
       if ((u & 1) == 0) {
-        out[(ptile::kSc + (i >> 1)) * ptile::kQuarter] = f.Sc;
+        ob.sc[u >> 1][lane] = f.Sc;
         f.Sc += y * y - yb * yb;
         f.Sc = (1 > f.Sc) ? 1 : f.Sc;
       }
     }
     if (R >= 2) f.xx = f.xx + y * y;
   }
+  wave_sync();
+  flush_rows<kLpStep>(qbase, ptile::kXf + n0, ob.xf, lane);
+  if (R == 3) {
+    flush_rows<kLpStep>(qbase, ptile::kSf + n0 - 480, ob.sf, lane);
+    flush_rows<kLpStep / 2>(qbase, ptile::kSc + (n0 - 480) / 2, ob.sc, lane);
+  } else if (R == 4) {
+    flush_rows<kR4>(qbase, ptile::kSf + n0 - 480, ob.sf, lane);
+    flush_rows<(kR4 + 1) / 2>(qbase, ptile::kSc + (n0 - 480) / 2, ob.sc, lane);
+  }
+  wave_sync();
 }
 static_assert(384 % kLpStep == 0 && 480 % kLpStep == 0 && kLpStep % 2 == 0, "pass-2 regions");
 
-// occupancy: 186 VGPRs, 2 workgroups per CU; 3 measured the same (the kernel
-// is HBM-bound), 4 slower (spills)
+// Memory-level parallelism.  The kernel runs at 2 workgroups per CU (2 waves
+// per SIMD), and a pass whose chunk waits on its own loads stalls for a whole
+// HBM round trip (~2 us under load) per 8 steps.  So every pass walks its
+// chunks through a register ring: the loads of the next kLpPf (passes 1, 2:
+// pitch-buffer chunks and the Syy read-back) or kYyPf (pass 3) chunks are in
+// flight while a chunk is summed.  The chunk loops are unrolled by the ring
+// depth so ring slots are static registers.
 #ifndef FVAD_PLPC_OCC
 #define FVAD_PLPC_OCC 2
 #endif
+#ifndef FVAD_LP_PF
+#define FVAD_LP_PF 1
+#endif
+#ifndef FVAD_YY_PF
+#define FVAD_YY_PF 1
+#endif
+constexpr int kLpPf = FVAD_LP_PF, kYyPf = FVAD_YY_PF;
+constexpr int kYyChunks = 384 / kLpStep;
+static_assert(kLpChunks % kLpPf == 0 && kYyChunks % kYyPf == 0, "prefetch rings must divide the passes");
+
+// One pass over a tile's pitch-buffer chunks: chunk c is staged and handed
+// to body(c, slot) while the loads of chunks c + 1 .. c + kLpPf are in flight;
+// pre(c, slot) issues the pass's own extra loads for chunk c into ring slot
+// `slot` (kLpPf chunks ahead of its use).
+template <typename Pre, typename Body>
+__device__ __forceinline__ void lp_walk(const LpSrc &src, float *stg, int lane, Pre &&pre, Body &&body) {
+  float4 pf[kLpPf][kLpPR];
+#pragma unroll
+  for (int d = 0; d < kLpPf; d++) {
+    lp_fetch(src, d, pf[d]);
+    pre(d, d);
+  }
+  for (int c0 = 0; c0 < kLpChunks; c0 += kLpPf) {
+#pragma unroll
+    for (int dd = 0; dd < kLpPf; dd++) {
+      const int c = c0 + dd;
+      lp_stage(stg, lane, pf[dd]);
+      body(c, dd);
+      if (c + kLpPf < kLpChunks) {
+        lp_fetch(src, c + kLpPf, pf[dd]);
+        pre(c + kLpPf, dd);
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
   __shared__ float stg_all[4][kLpRows * kLpCols];
+  __shared__ __attribute__((aligned(16))) OutStage ost_all[4];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   float *stg = stg_all[w];
+  OutStage &ob = ost_all[w];
   const float *col = stg + lane;
   const int Vr = a.n_ticks * a.n_channels;
   const int n_sb = (a.n_streams + 63) >> 6;
@@ -385,6 +480,7 @@ __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
   // positions of the same streams share pitch-buffer samples in L2)
   const long long n_quads = (n_tiles + 3) / 4;
   __shared__ long long gq;
+  STAMP_INIT();
   if (tid == 0) gq = take_group(a, kWorkPlpc);
   __syncthreads();
   long long q = gq;
@@ -406,128 +502,134 @@ __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
     }
     // lane's output column: quarter (lane >> 4) of tile t, [row][16]
     float *out = a.ptile + ((size_t)(t * 4 + (lane >> 4)) * ptile::kRows) * ptile::kQuarter + (lane & 15);
-    float4 cur[kLpPR];
+    float *qbase = out - (lane & 15);
+    RSTAMP(3);
 
     // pass 1: x_lp -> _celt_autocorr (lag k: sum_{i<860} x[i] x[i+k], then the tail)
     float acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, acc4 = 0;
     float d0 = 0, d1 = 0, d2 = 0, d3 = 0;
     float h1 = 0, h2 = 0, h3 = 0, h4 = 0, sp = 0;
-    lp_fetch(src, 0, cur);
-    for (int c = 0; c < kLpChunks; c++) {
-      lp_stage(stg, lane, cur);
-      if (c + 1 < kLpChunks) lp_fetch(src, c + 1, cur);
-      if (c == 0) {
+    lp_walk(
+        src, stg, lane, [&](int, int) {},
+        [&](int c, int) {
+          if (c == 0) {
 #pragma unroll
-        for (int u = 0; u < kLpStep; u++) {
-          const float x = lp_value<true>(col, u, sp);
-          acc0 = acc0 + x * x;
-          if (u >= 1) acc1 = acc1 + h1 * x;
-          if (u >= 2) acc2 = acc2 + h2 * x;
-          if (u >= 3) acc3 = acc3 + h3 * x;
-          if (u >= 4) acc4 = acc4 + h4 * x;
-          h4 = h3, h3 = h2, h2 = h1, h1 = x;
-        }
-      } else if (c + 1 < kLpChunks) {
+            for (int u = 0; u < kLpStep; u++) {
+              const float x = lp_value<true>(col, u, sp);
+              acc0 = acc0 + x * x;
+              if (u >= 1) acc1 = acc1 + h1 * x;
+              if (u >= 2) acc2 = acc2 + h2 * x;
+              if (u >= 3) acc3 = acc3 + h3 * x;
+              if (u >= 4) acc4 = acc4 + h4 * x;
+              h4 = h3, h3 = h2, h2 = h1, h1 = x;
+            }
+          } else if (c + 1 < kLpChunks) {
 #pragma unroll
-        for (int u = 0; u < kLpStep; u++) {
-          const float x = lp_value<false>(col, u, sp);
-          acc0 = acc0 + x * x;
-          acc1 = acc1 + h1 * x;
-          acc2 = acc2 + h2 * x;
-          acc3 = acc3 + h3 * x;
-          acc4 = acc4 + h4 * x;
-          h4 = h3, h3 = h2, h2 = h1, h1 = x;
-        }
-      } else {
-        // n = 856..863: term i = n - k belongs to the 860-term sum while
-        // i < 860, else (n >= 860 + k) to the tail sum of x[n] x[n-k]
+            for (int u = 0; u < kLpStep; u++) {
+              const float x = lp_value<false>(col, u, sp);
+              acc0 = acc0 + x * x;
+              acc1 = acc1 + h1 * x;
+              acc2 = acc2 + h2 * x;
+              acc3 = acc3 + h3 * x;
+              acc4 = acc4 + h4 * x;
+              h4 = h3, h3 = h2, h2 = h1, h1 = x;
+            }
+          } else {
+            // n = 856..863: term i = n - k belongs to the 860-term sum while
+            // i < 860, else (n >= 860 + k) to the tail sum of x[n] x[n-k]
 #pragma unroll
-        for (int u = 0; u < kLpStep; u++) {
-          const int n = c * kLpStep + u;
-          const float x = lp_value<false>(col, u, sp);
-          if (n < 860) acc0 = acc0 + x * x; else d0 = d0 + x * x;
-          if (n - 1 < 860) acc1 = acc1 + h1 * x; else d1 = d1 + x * h1;
-          if (n - 2 < 860) acc2 = acc2 + h2 * x; else d2 = d2 + x * h2;
-          if (n - 3 < 860) acc3 = acc3 + h3 * x; else d3 = d3 + x * h3;
-          acc4 = acc4 + h4 * x;  // n - 4 <= 859
-          (void)n;
-          h4 = h3, h3 = h2, h2 = h1, h1 = x;
-        }
-      }
-    }
+            for (int u = 0; u < kLpStep; u++) {
+              const int n = c * kLpStep + u;
+              const float x = lp_value<false>(col, u, sp);
+              if (n < 860) acc0 = acc0 + x * x; else d0 = d0 + x * x;
+              if (n - 1 < 860) acc1 = acc1 + h1 * x; else d1 = d1 + x * h1;
+              if (n - 2 < 860) acc2 = acc2 + h2 * x; else d2 = d2 + x * h2;
+              if (n - 3 < 860) acc3 = acc3 + h3 * x; else d3 = d3 + x * h3;
+              acc4 = acc4 + h4 * x;  // n - 4 <= 859
+              h4 = h3, h3 = h2, h2 = h1, h1 = x;
+            }
+          }
+        });
+    RSTAMP(0);
     float acv[5] = {acc0 + d0, acc1 + d1, acc2 + d2, acc3 + d3, acc4 + 0.0f};
     float l[5];
     lpc_fir5_coeffs(acv, l);
 
     // pass 2: x_lp again -> celt_fir5 -> xf; Syy initial sums, xx; from
     // n = 480 on, the Syy recurrences with xf[n - 480] read back from the tile
-    // buffer (written by this lane 480 steps earlier, fetched a chunk ahead).
-    // The chunk body is specialised per region of n, so it has no branches.
+    // buffer (written by this lane 480 steps earlier, loaded kLpPf chunks
+    // ahead).  The chunk body is specialised per region of n, so it has no
+    // branches.
     Fir5State fs;
 #pragma unroll
     for (int i = 0; i < 5; i++) fs.l[i] = l[i];
-    float bk[kLpStep], bkn[kLpStep];
-#pragma unroll
-    for (int u = 0; u < kLpStep; u++) bk[u] = bkn[u] = 0.0f;
-    lp_fetch(src, 0, cur);
-    for (int c = 0; c < kLpChunks; c++) {
-      const int n0 = c * kLpStep;
-      lp_stage(stg, lane, cur);
-      if (c + 1 < kLpChunks) lp_fetch(src, c + 1, cur);
-      const int n1 = n0 + kLpStep;  // next chunk
-      if (n1 + kLpStep > 480 && n1 < 480 + 294) plpc_back(out, n1, bkn);
-      if (c == 0)
-        fir5_chunk<true, 1>(fs, col, out, n0, bk);
-      else if (n0 < 384)
-        fir5_chunk<false, 1>(fs, col, out, n0, bk);
-      else if (n0 < 480)
-        fir5_chunk<false, 2>(fs, col, out, n0, bk);
-      else if (n0 + kLpStep <= 480 + 294)
-        fir5_chunk<false, 3>(fs, col, out, n0, bk);
-      else if (n0 < 480 + 294)
-        fir5_chunk<false, 4>(fs, col, out, n0, bk);
-      else
-        fir5_chunk<false, 5>(fs, col, out, n0, bk);
-#pragma unroll
-      for (int u = 0; u < kLpStep; u++) bk[u] = bkn[u];
-    }
+    RowLd bk[kLpPf];
+    lp_walk(
+        src, stg, lane,
+        [&](int c, int slot) {
+          const int n0 = c * kLpStep;
+          if (n0 + kLpStep > 480 && n0 < 480 + 294) fetch_rows<kLpStep>(qbase, ptile::kXf + n0 - 480, bk[slot], lane);
+        },
+        [&](int c, int slot) {
+          const int n0 = c * kLpStep;
+          if (c == 0)
+            fir5_chunk<true, 1>(fs, col, qbase, n0, bk[slot], ob, lane);
+          else if (n0 < 384)
+            fir5_chunk<false, 1>(fs, col, qbase, n0, bk[slot], ob, lane);
+          else if (n0 < 480)
+            fir5_chunk<false, 2>(fs, col, qbase, n0, bk[slot], ob, lane);
+          else if (n0 + kLpStep <= 480 + 294)
+            fir5_chunk<false, 3>(fs, col, qbase, n0, bk[slot], ob, lane);
+          else if (n0 < 480 + 294)
+            fir5_chunk<false, 4>(fs, col, qbase, n0, bk[slot], ob, lane);
+          else
+            fir5_chunk<false, 5>(fs, col, qbase, n0, bk[slot], ob, lane);
+        });
+    RSTAMP(1);
     const float xx = fs.xx;
     out[ptile::kXx * ptile::kQuarter] = xx;
 
-    // pass 3: yy_lookup[i] = max(0, yy), yy += x[-i]^2 - x[480-i]^2 (x = xf + 384);
-    // the 2 x kLpStep rows of the next chunk are fetched while this one is summed
+    // pass 3: yy_lookup[i] = max(0, yy), yy += x[-i]^2 - x[480-i]^2 (x = xf + 384),
+    // i = 1 .. 384 in chunks of kLpStep, the rows of the next kYyPf chunks in flight
     float yy = xx;
     out[ptile::kYy * ptile::kQuarter] = xx;
-    float ya[kLpStep], yb[kLpStep];
+    // the last chunks of pass 2 stored the first rows read here (other lanes' stores)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    RowLd ya[kYyPf], yb[kYyPf];
+    // chunk c: i = i0 .. i0 + 7 (i0 = 1 + 8c) reads rows 383 - 8c - u and 863 - 8c - u
+    auto yy_fetch = [&](int c, int slot) {
+      fetch_rows<kLpStep>(qbase, ptile::kXf + 384 - kLpStep - c * kLpStep, ya[slot], lane);
+      fetch_rows<kLpStep>(qbase, ptile::kXf + 864 - kLpStep - c * kLpStep, yb[slot], lane);
+    };
 #pragma unroll
-    for (int u = 0; u < kLpStep; u++) {
-      ya[u] = out[(383 - u) * ptile::kQuarter];
-      yb[u] = out[(863 - u) * ptile::kQuarter];
+    for (int d = 0; d < kYyPf; d++) yy_fetch(d, d);
+    for (int c0 = 0; c0 < kYyChunks; c0 += kYyPf) {
+#pragma unroll
+      for (int dd = 0; dd < kYyPf; dd++) {
+        const int c = c0 + dd, i0 = 1 + c * kLpStep;
+        stage_rows(ya[dd], ob.in, lane);
+        stage_rows(yb[dd], ob.in2, lane);
+        if (c + kYyPf < kYyChunks) yy_fetch(c + kYyPf, dd);
+        wave_sync();
+#pragma unroll
+        for (int u = 0; u < kLpStep; u++) {
+          const float va = ob.in[kLpStep - 1 - u][lane], vb = ob.in2[kLpStep - 1 - u][lane];
+          yy = yy + va * va - vb * vb;
+          ob.xf[u][lane] = (0 > yy) ? 0 : yy;
+        }
+        wave_sync();
+        flush_rows<kLpStep>(qbase, ptile::kYy + i0, ob.xf, lane);
+        wave_sync();
+      }
     }
-    for (int i0 = 1; i0 <= 384; i0 += kLpStep) {
-      float na[kLpStep], nb[kLpStep];
-      const int i1 = i0 + kLpStep;
-#pragma unroll
-      for (int u = 0; u < kLpStep; u++) {
-        na[u] = i1 <= 384 ? out[(384 - i1 - u) * ptile::kQuarter] : 0.0f;
-        nb[u] = i1 <= 384 ? out[(864 - i1 - u) * ptile::kQuarter] : 0.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < kLpStep; u++) {
-        yy = yy + ya[u] * ya[u] - yb[u] * yb[u];
-        out[(ptile::kYy + i0 + u) * ptile::kQuarter] = (0 > yy) ? 0 : yy;
-      }
-#pragma unroll
-      for (int u = 0; u < kLpStep; u++) {
-        ya[u] = na[u];
-        yb[u] = nb[u];
-      }
-    }
+    RSTAMP(2);
     __syncthreads();
     if (tid == 0) gq = take_group(a, kWorkPlpc);
     __syncthreads();
     q = gq;
   }
+  STAMP_FLUSH(56, 4);
 }
 
 // ---------------------------------------------------------------------------
