@@ -332,8 +332,9 @@ struct OutStage {
   float sf[kLpStep][64];      // fine Syy rows
   float sc[kLpStep / 2][64];  // coarse Syy rows
   float in[kLpStep][64];      // read-back rows (pass 2), x[-i] rows (pass 3)
-  float in2[kLpStep][64];     // x[480 - i] rows (pass 3)
 };
+// pass 3 stages its x[480 - i] rows in the fine-Syy stage (unused after pass 2)
+#define in2 sf
 struct RowLd {
   float4 v[2];
 };
