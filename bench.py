@@ -65,6 +65,9 @@ def parse():
                     help="also time pushes from host buffers (PCIe-inclusive; reported as host_buffers, never value)")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="no GPU: gloo ranks with a stub engine (tests the launcher, barrier and max-reduce)")
+    ap.add_argument("--variants", type=int, default=1,
+                    help="staged runs: also time the fp16 engine mode (configs[4]'s variant) on the same "
+                         "workload and report it under `variants` (never `value`)")
     return ap.parse_args()
 
 
@@ -287,30 +290,44 @@ def main():
 
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     model = fvad.Model(seed=1)
-    eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=args.mode)
-    if args.mode != "fused" and not args.no_vadm:
-        eng.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
     base, _ = stream_partition(rank, B)
-    eng.load_synthetic(T, base=base)
 
-    for _ in range(args.warmup):
-        eng.run_resident(T)
-    eng.sync()
-    eng.clear_times()
-    barrier(dist, torch)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.run_resident(T)
-    eng.sync()
-    barrier(dist, torch)
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, dist, torch)
-    kt = eng.kernel_times()
+    def measure(mode):
+        """warmup, then exactly args.steps pushes between barriers; max over ranks"""
+        eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=mode)
+        if mode != "fused" and not args.no_vadm:
+            eng.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
+        eng.load_synthetic(T, base=base)
+        for _ in range(args.warmup):
+            eng.run_resident(T)
+        eng.sync()
+        eng.clear_times()
+        barrier(dist, torch)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.run_resident(T)
+        eng.sync()
+        barrier(dist, torch)
+        elapsed = max_over_ranks(time.perf_counter() - t0, dist, torch)
+        return eng, elapsed, eng.kernel_times()
 
+    eng, elapsed, kt = measure(args.mode)
     value = aggregate_rate(B * Ch * T, world, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
     host = host_rate(eng, args, rank, dist, torch) if args.host_rate else None
+    variants = None
+    if args.variants and args.mode == "staged":
+        del eng  # one engine's buffers at a time
+        _, el16, kt16 = measure("fp16")
+        variants = {"fp16": {
+            "value": round(aggregate_rate(B * Ch * T, world, args.steps, el16), 1), "unit": "frames/s",
+            "ms_per_step": round(1000.0 * el16 / args.steps, 3),
+            "dtype": "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
+            "k_gru16_ms": round(kt16["kernels"].get("k_gru16", 0.0), 4),
+            "parity": "tolerance (SURVEY.md 8(c): vad |d| <= 2e-2, segments identical; tests/test_gpu_fp16.py)",
+            "note": "BASELINE configs[4]'s fp16-GRU variant on the same workload and clock (bench.py --mode fp16 "
+                    "gives its full line)"}}
 
     if rank != 0:
         if dist is not None:
@@ -420,6 +437,8 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if variants is not None:
+        line["variants"] = variants
     if host is not None:
         line["host_buffers"] = host
         line["realtime_streams_host"] = round(host["value"] / (100.0 * Ch), 1)
