@@ -45,12 +45,26 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-// operand row of one stream, in 8-element chunks
+// operand row of one stream, in 8-element chunks.  The layers run a frame
+// apart (see the superstep plan), so the segments that layers of different
+// frames read are versioned by frame: features (5 versions, f % 5), dense
+// output (3, f % 3), vad state (3, f % 3), noise state (2, f & 1).
 enum OpSeg { kFeat = 0, kDense, kSv, kRsv, kSn, kRsn, kSd, kRsd, kNSeg };
-constexpr int kSegBase[kNSeg] = {0, 12, 15, 18, 21, 27, 33, 45};  // feature slot 1 at chunk 6
-constexpr int kZeroChunk = 57;
-constexpr int kRowChunks = 59;  // 944 B: rows of 16 streams fall on distinct 4-bank groups
+constexpr int kSegLen[kNSeg] = {6, 3, 3, 3, 6, 6, 12, 12};   // chunks of one version
+constexpr int kSegVer[kNSeg] = {5, 3, 3, 1, 2, 1, 1, 1};      // versions
+constexpr int seg_base(int g) {
+  int o = 0;
+  for (int i = 0; i < g; i++) o += kSegLen[i] * kSegVer[i];
+  return o;
+}
+constexpr int kSegBase[kNSeg] = {seg_base(0), seg_base(1), seg_base(2), seg_base(3),
+                                 seg_base(4), seg_base(5), seg_base(6), seg_base(7)};
+constexpr int kZeroChunk = seg_base(kNSeg);
+constexpr int kRowChunks = kZeroChunk + 2;  // odd: rows of 16 streams fall on distinct 4-bank groups
+static_assert(kRowChunks % 2 == 1, "operand row pitch");
 constexpr int kRowHalf = kRowChunks * 8;
+// versioned segment tags (op_chunk bits 8..10): 1 feat, 2 dense, 3 vad state, 4 noise state
+constexpr int seg_tag(int seg) { return seg == kFeat ? 1 : seg == kDense ? 2 : seg == kSv ? 3 : seg == kSn ? 4 : 0; }
 // image matrix -> operand segment of each of its rnnimg segments (fvad_internal.h)
 constexpr int kMatSeg[rnnimg::kMats][4] = {{kFeat, -1, -1, -1}, {kDense, kSv, -1, -1},   {kDense, kRsv, -1, -1},
                                            {kDense, kSv, kFeat, kSn}, {kDense, kSv, kFeat, kRsn},
@@ -72,7 +86,7 @@ constexpr int bias_base(int m) {
 constexpr int kBiasRows = bias_base(rnnimg::kMats);
 static_assert(nkb(5) == 7 && nkb(3) == 5 && nkb(0) == 2 && nkb(7) == 3 && nkb(8) == 1, "K blocks");
 
-// chunk q of matrix m -> operand chunk (feature chunks: slot 0; bit 0x100 marks them)
+// chunk q of matrix m -> operand chunk of version 0, its versioned-segment tag in bits 8..10
 constexpr int op_chunk(int m, int q) {
   int c0 = 0;
 #pragma unroll
@@ -80,12 +94,33 @@ constexpr int op_chunk(int m, int q) {
     const int n = rnnimg::pad8(rnnimg::kSegs[m][g]) / 8;
     if (q < c0 + n) {
       const int seg = kMatSeg[m][g];
-      return kSegBase[seg] + (q - c0) + (seg == kFeat ? 0x100 : 0);
+      return kSegBase[seg] + (q - c0) + (seg_tag(seg) << 8);
     }
     c0 += n;
   }
   return kZeroChunk;
 }
+
+// versions of the operand segments matrix M reads for its frame f:
+// the vad z|r gates read the vad state of frame f - 1, the noise z|r gates the
+// noise state of f - 1; everything else reads frame f's values
+struct Ver {
+  int f, d, v, n;  // byte offsets of the feature, dense, vad-state and noise-state versions
+  __device__ __forceinline__ int of(int tag) const { return tag == 1 ? f : tag == 2 ? d : tag == 3 ? v : tag == 4 ? n : 0; }
+};
+template <int M>
+__device__ __forceinline__ Ver versions(int f) {
+  Ver v;
+  const int fv = (M == 1) ? f - 1 : f;  // vad state version
+  const int fn = (M == 3) ? f - 1 : f;  // noise state version
+  v.f = ((f + 5) % 5) * kSegLen[kFeat] * 16;
+  v.d = ((f + 3) % 3) * kSegLen[kDense] * 16;
+  v.v = ((fv + 3) % 3) * kSegLen[kSv] * 16;
+  v.n = ((fn + 2) & 1) * kSegLen[kSn] * 16;
+  return v;
+}
+// chunk offset (in halfs) of version `ver` of segment seg
+__device__ __forceinline__ int seg_half(int seg, int ver) { return (kSegBase[seg] + ver * kSegLen[seg]) * 8; }
 
 }  // namespace g16
 
@@ -129,12 +164,8 @@ constexpr int kGNT = 512;    // 8 waves, 2 per SIMD (fragments + operands need >
 constexpr int kPfW = 30;     // raw feature words per stream and frame: Lyf[22], f34[7], silence
 constexpr int kFeatItems = kGS * (kBands + 7 + kCeps);
 
-struct Job {
-  int m = -1, tile = 0;
-};
-
-constexpr int kDzrFrags = 12 * 7;
-constexpr int kFr = 24;  // register fragment slots (see the wave plan)  // denoise z|r: the largest matrix lives in LDS (84 KB)
+constexpr int kDzrFrags = 12 * 7;  // denoise z|r: the largest matrix lives in LDS (84 KB)
+constexpr int kFr = 20;            // register fragment slots (see the wave plan)
 
 struct Lds {
   alignas(16) half8 dzr[kDzrFrags][64];
@@ -153,51 +184,39 @@ struct Lds {
   long long fbase[kGS];
 };
 
-__device__ __forceinline__ void job_init(Job &J, int m, int tile) {
-  J.m = m;
-  J.tile = tile;
+// A fragments of tile `tile` of matrix M into fr[F0 .. F0 + nkb(M))
+template <int F0, int M>
+__device__ __forceinline__ void load_frags(half8 (&fr)[kFr], const half8 *__restrict__ img, int tile, int lane) {
+  constexpr int NK = nkb(M);
+  static_assert(F0 + NK <= kFr, "fragment slots");
+  const half8 *src = img + (size_t)(frag_base(M) + tile * NK) * 64 + lane;
+#pragma unroll
+  for (int kb = 0; kb < NK; kb++) fr[F0 + kb] = src[kb * 64];
 }
 
-template <int F0, int NK>
-__device__ __forceinline__ void load_frags(half8 (&fr)[kFr], const half8 *__restrict__ img, const Job &J, int lane) {
-  if (J.m < 0) return;
-  int nk = 0, base = 0;
-#pragma unroll
-  for (int m = 0; m < rnnimg::kMats; m++)
-    if (m == J.m) {
-      nk = nkb(m);
-      base = frag_base(m);
-    }
-  const half8 *src = img + (size_t)(base + J.tile * nk) * 64 + lane;
-#pragma unroll
-  for (int kb = 0; kb < NK; kb++)
-    if (kb < nk) fr[F0 + kb] = src[kb * 64];
-}
-
-// acc = bias + sum over matrix M's K blocks of A . B (C-in and C-out of one
-// chain); M is known at every call site, so this lane's operand chunk of
-// block kb is a select over the four lane groups of compile-time offsets
+// this lane's B chunk of K block kb of matrix M (frame versions in V): a
+// select over the four lane groups of compile-time chunks, plus the version
+// offset of the segment the chunk belongs to
 template <int M>
-__device__ __forceinline__ half8 b_operand(const Lds &L, int lane, int kb, int fslot) {
+__device__ __forceinline__ half8 b_operand(const Lds &L, int lane, int kb, const Ver &V) {
   const int s = lane & 15, g = lane >> 4;
   const char *row = reinterpret_cast<const char *>(L.op[s]);
   const int c0 = op_chunk(M, 4 * kb), c1 = op_chunk(M, 4 * kb + 1), c2 = op_chunk(M, 4 * kb + 2),
             c3 = op_chunk(M, 4 * kb + 3);
   const int c = g == 0 ? c0 : g == 1 ? c1 : g == 2 ? c2 : c3;
-  return *reinterpret_cast<const half8 *>(row + (c & 0xff) * 16 + ((c & 0x100) ? fslot * 6 * 16 : 0));
+  return *reinterpret_cast<const half8 *>(row + (c & 0xff) * 16 + V.of(c >> 8));
 }
 
-// acc = bias + sum over matrix M's K blocks of A . B (C-in and C-out of one
-// chain); M is known at every call site, so this lane's operand chunk of
-// block kb is a select over the four lane groups of compile-time offsets.
-// A from registers fr[F0 + kb] (F0 >= 0) or from LDS (denoise z|r, F0 < 0).
+// acc = bias + sum over matrix M's K blocks of A . B for frame f (one MFMA
+// chain); A from registers fr[F0 + kb] (F0 >= 0) or from LDS (denoise z|r, F0 < 0)
 template <int F0, int M>
-__device__ __forceinline__ f4 mma_job(const half8 (&fr)[kFr], int tile, const Lds &L, int lane, int fslot) {
+__device__ __forceinline__ f4 mma_job(const half8 (&fr)[kFr], int tile, const Lds &L, int lane, int f) {
   constexpr int NK = nkb(M);
+  const Ver V = versions<M>(f);
   f4 acc = *reinterpret_cast<const f4 *>(&L.bias[bias_base(M) + tile * 16 + 4 * (lane >> 4)]);
 #pragma unroll
   for (int kb = 0; kb < NK; kb++) {
-    const half8 b = b_operand<M>(L, lane, kb, fslot);
+    const half8 b = b_operand<M>(L, lane, kb, V);
     half8 w;
     if constexpr (F0 >= 0)
       w = fr[F0 + kb];
@@ -234,50 +253,87 @@ __device__ __forceinline__ void epi_zr(Lds &L, const f4 &acc, int tile, int lane
   }
 }
 
-// candidate tile epilogue: s' = z s + (1 - z) act(sum) for active streams
+// candidate tile epilogue: s' = z s + (1 - z) act(sum) for active streams, the
+// new state into operand half offset `dst` (the frame's version); an inactive
+// stream keeps its state and still fills the frame's version with it
 template <int N, int PZ, int PS>
 __device__ __forceinline__ void epi_h(Lds &L, const f4 &acc, int tile, int lane, int act, float (*Z)[PZ],
-                                      float (*S)[PS], int st_seg, bool on) {
+                                      float (*S)[PS], int dst, bool on) {
   const int s = lane & 15, r0 = tile * 16 + 4 * (lane >> 4);
-  if (r0 >= N || !on) return;
-  const f4 z = *reinterpret_cast<const f4 *>(&Z[s][r0]);
+  if (r0 >= N) return;
   const f4 st = *reinterpret_cast<const f4 *>(&S[s][r0]);
+  if (!on) {
+    put_h4(&L.op[s][dst + r0], st[0], st[1], st[2], st[3]);
+    return;
+  }
+  const f4 z = *reinterpret_cast<const f4 *>(&Z[s][r0]);
   float n[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) n[i] = z[i] * st[i] + (1 - z[i]) * activate(L.tt, act, kWs * acc[i]);
   *reinterpret_cast<f4 *>(&S[s][r0]) = f4{n[0], n[1], n[2], n[3]};
-  put_h4(&L.op[s][kSegBase[st_seg] * 8 + r0], n[0], n[1], n[2], n[3]);
+  put_h4(&L.op[s][dst + r0], n[0], n[1], n[2], n[3]);
 }
 
 }  // namespace
 
+// The layers of one frame form a chain (dense -> vad -> noise -> denoise ->
+// denoise_output), but layer L of frame t only waits for layer L - 1 of t and
+// layer L of t - 1.  So superstep u runs dense(u), vad(u - 1), noise(u - 2),
+// denoise(u - 3), outputs(u - 2 / u - 4) side by side in two phases (all z|r
+// gates, then all candidates): two barriers per frame instead of seven.
+// Operands that layers of different frames read at once are versioned
+// (OpSeg).  Wave plan (waves w and w + 4 share a SIMD; balanced by per-wave
+// stamps, tools/stamps.py fp16):
+//   A  every wave denoise z|r(u-3) tile w (w0..3 also w+8, A from LDS);
+//      w0,1 dense(u) t w + the distance rows of the features of u+1 |
+//      w2,3 vad z|r(u-1) t w-2 | w4 vad z|r t2, noise z|r(u-2) t0, vad_out(u-2) |
+//      w5,6 noise z|r t 2w-9, 2w-8 | w5 den_out(u-4) t1 | w7 noise z|r t5,
+//      den_out t0; w2,3,6,7 the rest of the features of u+1
+//   B  w0..5 denoise h(u-3) t w; w4 noise h(u-2) t1; w6 noise h t0, vad h(u-1)
+//      t1; w7 noise h t2, vad h t0; w0,1 spectral variability(u+1); w2,3,5
+//      gains(u-4)
+// Register fragments (kFr = 20 slots of 8 f16): w0,1 dense 0-1, denoise h 2-8;
+// w2,3 vad z|r 0-1, denoise h 2-8; w4 vad z|r 0-1, noise z|r 2-6, vad_out 7,
+// denoise h 8-14, noise h 15-19; w5 noise z|r 0-4, 5-9, denoise h 10-16,
+// den_out 17-19; w6 noise z|r 0-4, 5-9, noise h 10-14, vad h 15-16;
+// w7 noise z|r 0-4, den_out 5-7, noise h 11-15, vad h 16-17.
 __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
   constexpr int S = kGS;
   __shared__ Lds L;
   const int tid = threadIdx.x, lane = tid & 63, W = tid >> 6;
   const int sb = blockIdx.x * S;
   const int *ra = a.rnn_act;
-  // ---- jobs of this wave (register slots: A = fr[0..4] noise z|r, E = fr[5..9]
-  // noise h, F = fr[10..16] denoise h, B = fr[17..19] dense / den_out /
-  // vad_out, C = fr[20..21] vad z|r, D = fr[22..23] vad h)
-  Job JA, JE, JF, JB, JC, JD;
-  if (W < 6) job_init(JA, 3, W);
-  if (W >= 5) job_init(JE, 4, W - 5);
-  if (W >= 2) job_init(JF, 6, W - 2);
-  if (W < 2) job_init(JB, 0, W);
-  else if (W < 4) job_init(JB, 7, W - 2);
-  else if (W == 6) job_init(JB, 8, 0);
-  if (W >= 4 && W < 7) job_init(JC, 1, W - 4);
-  if (W == 4 || W == 5) job_init(JD, 2, W - 4);
   half8 fr[kFr];
   {
     const half8 *img = reinterpret_cast<const half8 *>(a.gru16_frags);
-    load_frags<0, 5>(fr, img, JA, lane);
-    load_frags<5, 5>(fr, img, JE, lane);
-    load_frags<10, 7>(fr, img, JF, lane);
-    load_frags<17, 3>(fr, img, JB, lane);
-    load_frags<20, 2>(fr, img, JC, lane);
-    load_frags<22, 2>(fr, img, JD, lane);
+    if (W < 2) {
+      load_frags<0, 0>(fr, img, W, lane);
+      load_frags<2, 6>(fr, img, W, lane);
+    } else if (W < 4) {
+      load_frags<0, 1>(fr, img, W - 2, lane);
+      load_frags<2, 6>(fr, img, W, lane);
+    } else if (W == 4) {
+      load_frags<0, 1>(fr, img, 2, lane);
+      load_frags<2, 3>(fr, img, 0, lane);
+      load_frags<7, 8>(fr, img, 0, lane);
+      load_frags<8, 6>(fr, img, 4, lane);
+      load_frags<15, 4>(fr, img, 1, lane);
+    } else if (W == 5) {
+      load_frags<0, 3>(fr, img, 1, lane);
+      load_frags<5, 3>(fr, img, 2, lane);
+      load_frags<10, 6>(fr, img, 5, lane);
+      load_frags<17, 7>(fr, img, 1, lane);
+    } else if (W == 6) {
+      load_frags<0, 3>(fr, img, 3, lane);
+      load_frags<5, 3>(fr, img, 4, lane);
+      load_frags<10, 4>(fr, img, 0, lane);
+      load_frags<15, 2>(fr, img, 1, lane);
+    } else {
+      load_frags<0, 3>(fr, img, 5, lane);
+      load_frags<5, 7>(fr, img, 0, lane);
+      load_frags<11, 4>(fr, img, 2, lane);
+      load_frags<16, 2>(fr, img, 0, lane);
+    }
     const half8 *dz = img + (size_t)frag_base(5) * 64;
     for (int i = tid; i < kDzrFrags * 64; i += kGNT) (&L.dzr[0][0])[i] = dz[i];
   }
@@ -306,20 +362,21 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     L.fbase[tid] = (long long)s * a.V;
   }
   __syncthreads();
+  // states before frame 0 = the versions of frame -1 (vad 2, noise 1)
   for (int idx = tid; idx < S * 96; idx += kGNT) {
     const int s = idx / 96, i = idx - s * 96;
     const bool ok = sb + s < a.n_streams;
     const float *stp = a.state + (size_t)(sb + s) * st::kWords;
     if (i < 24) {
       L.sv[s][i] = ok ? stp[st::kVadGru + i] : 0.0f;
-      L.op[s][kSegBase[kSv] * 8 + i] = (_Float16)L.sv[s][i];
+      L.op[s][seg_half(kSv, 2) + i] = (_Float16)L.sv[s][i];
     }
     if (i < 48) {
       L.sn[s][i] = ok ? stp[st::kNoiseGru + i] : 0.0f;
-      L.op[s][kSegBase[kSn] * 8 + i] = (_Float16)L.sn[s][i];
+      L.op[s][seg_half(kSn, 1) + i] = (_Float16)L.sn[s][i];
     }
     L.sd[s][i] = ok ? stp[st::kDenGru + i] : 0.0f;
-    L.op[s][kSegBase[kSd] * 8 + i] = (_Float16)L.sd[s][i];
+    L.op[s][seg_half(kSd, 0) + i] = (_Float16)L.sd[s][i];
   }
   int maxnf = 0;
 #pragma unroll
@@ -335,7 +392,7 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     return a.silence[f] ? 1.0f : 0.0f;
   };
   // features of frame f from L.pf (k_rnn3's F-C: cepstral memory, deltas,
-  // 34..40, the new distance row) into feature slot f & 1; item (s, i)
+  // 34..40, the new distance row) into feature version f % 5; item (s, i)
   auto feat_c = [&](int f, int idx) {
     const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
     const bool valid = f < L.nfs[s];
@@ -345,7 +402,7 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
       if (valid && !on) a.vadf[L.fbase[s] + f] = 0;  // silent: X passes through, state untouched
     }
     if (!on) return;
-    _Float16 *feat = &L.op[s][(f & 1) * 6 * 8];
+    _Float16 *feat = &L.op[s][seg_half(g16::kFeat, f % 5)];
     const int mi = L.memid[s];
     const float *c0 = L.pf[s];
     if (i < kBands) {
@@ -392,7 +449,7 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     float sv = 0;
 #pragma unroll
     for (int k = 0; k < kCeps; k++) sv += m[k];
-    L.op[s][(f & 1) * 6 * 8 + 41] = (_Float16)(float)(sv / kCeps - 2.1);
+    L.op[s][seg_half(g16::kFeat, f % 5) + 41] = (_Float16)(float)(sv / kCeps - 2.1);
     int mid = L.memid[s] + 1;
     if (mid == kCeps) mid = 0;
     L.memid[s] = mid;
@@ -408,97 +465,138 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
   if (pf_lane) L.pf[pfs][pfi] = pf1;
   __syncthreads();
   const int col = lane & 15;
+  auto live = [&](int f) { return f >= 0 && f < maxnf; };
+  auto den_out = [&](const f4 &acc, int tile) {  // denoise_output tile -> the frame's gains
+    const int r0 = tile * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (r0 + i < kBands) L.gout[col][r0 + i] = activate(L.tt, ra[7], kWs * acc[i]);
+  };
+  auto on_of = [&](int f) { return L.act[f & 7][col] != 0; };
   STAMP_INIT();
-  for (int t = 0; t <= maxnf; t++) {
-    const int fs = t & 1;
-    const bool fr_t = t < maxnf;
-    const bool on_t = fr_t && L.act[t & 7][col];
-    // ---- P0: dense(t) [w0, w1], denoise_output(t-1) [w2, w3]
+#ifdef FVAD_STAMPS
+  // per-wave busy cycles of each phase (lane 0 of every wave): stamps[0..7] A, [8..15] B
+  unsigned long long wacc[2] = {0, 0}, wt0 = 0;
+#define WSTAMP_BEGIN() wt0 = __builtin_amdgcn_s_memtime()
+#define WSTAMP_END(p) wacc[p] += __builtin_amdgcn_s_memtime() - wt0
+#else
+#define WSTAMP_BEGIN() \
+  do {                 \
+  } while (0)
+#define WSTAMP_END(p) \
+  do {                \
+  } while (0)
+#endif
+  for (int u = 0; u < maxnf + 4; u++) {
+    const int fV = u - 1, fN = u - 2, fD = u - 3, fO = u - 4;
+    const float pf_next = fetch(u + 2);  // raw features of u + 2, staged at the end of phase B
+    // ---- phase A: z|r gates of vad(u-1), noise(u-2), denoise(u-3); dense(u),
+    // vad_out(u-2), den_out(u-4); features(u+1)
+    WSTAMP_BEGIN();
+    if (live(fD)) {
+      epi_zr<96>(L, mma_job<-1, 5>(fr, W, L, lane, fD), W, lane, L.zd, L.sd, kRsd);
+      if (W < 4) epi_zr<96>(L, mma_job<-1, 5>(fr, W + 8, L, lane, fD), W + 8, lane, L.zd, L.sd, kRsd);
+    }
     if (W < 2) {
-      if (fr_t) {
-        const f4 acc = mma_job<17, 0>(fr, JB.tile, L, lane, fs);
-        const int r0 = JB.tile * 16 + 4 * (lane >> 4);
+      if (u < maxnf) {
+        const f4 acc = mma_job<0, 0>(fr, W, L, lane, u);
+        const int r0 = W * 16 + 4 * (lane >> 4);
         if (r0 < 24) {
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; i++) v[i] = activate(L.tt, ra[0], kWs * acc[i]);
-          put_h4(&L.op[col][kSegBase[kDense] * 8 + r0], v[0], v[1], v[2], v[3]);
+          put_h4(&L.op[col][seg_half(kDense, u % 3) + r0], v[0], v[1], v[2], v[3]);
         }
       }
     } else if (W < 4) {
-      if (t >= 1) {
-        const f4 acc = mma_job<17, 7>(fr, JB.tile, L, lane, fs);
-        const int r0 = JB.tile * 16 + 4 * (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          if (r0 + i < kBands) L.gout[col][r0 + i] = activate(L.tt, ra[7], kWs * acc[i]);
+      if (live(fV)) epi_zr<24>(L, mma_job<0, 1>(fr, W - 2, L, lane, fV), W - 2, lane, L.zv, L.sv, kRsv);
+    } else if (W == 4) {
+      if (live(fV)) epi_zr<24>(L, mma_job<0, 1>(fr, 2, L, lane, fV), 2, lane, L.zv, L.sv, kRsv);
+      if (live(fN)) {
+        epi_zr<48>(L, mma_job<2, 3>(fr, 0, L, lane, fN), 0, lane, L.zn, L.sn, kRsn);
+        const f4 acc = mma_job<7, 8>(fr, 0, L, lane, fN);
+        if (lane < 16 && on_of(fN)) a.vadf[L.fbase[col] + fN] = activate(L.tt, ra[8], kWs * acc[0]);
       }
+    } else if (W < 7) {
+      if (live(fN)) {
+        epi_zr<48>(L, mma_job<0, 3>(fr, 2 * W - 9, L, lane, fN), 2 * W - 9, lane, L.zn, L.sn, kRsn);
+        epi_zr<48>(L, mma_job<5, 3>(fr, 2 * W - 8, L, lane, fN), 2 * W - 8, lane, L.zn, L.sn, kRsn);
+      }
+      if (W == 5 && live(fO)) den_out(mma_job<17, 7>(fr, 1, L, lane, fO), 1);
+    } else {
+      if (live(fN)) epi_zr<48>(L, mma_job<0, 3>(fr, 5, L, lane, fN), 5, lane, L.zn, L.sn, kRsn);
+      if (live(fO)) den_out(mma_job<5, 7>(fr, 0, L, lane, fO), 0);
     }
+    if (u + 1 < maxnf) {
+      // distance rows (the 22-term sums) one per lane on w0, w1; the rest on w2, w3, w6, w7
+      constexpr int kIt = kBands + 7 + kCeps, kLight = kBands + 7;
+      if (tid < S * kCeps)
+        feat_c(u + 1, (tid >> 3) * kIt + kLight + (tid & 7));
+      else if ((W & 3) >= 2)
+        for (int k = lane + 64 * ((W & 1) + (W >> 2) * 2); k < S * kLight; k += 4 * 64)
+          feat_c(u + 1, (k / kLight) * kIt + k % kLight);
+    }
+    WSTAMP_END(0);
     __syncthreads();
     RSTAMP(0);
-    // ---- P1: vad z|r(t) [w4..6], features(t+1) [w0..3], gains(t-1) [w7]
-    if (W >= 4 && W < 7) {
-      if (fr_t) epi_zr<24>(L, mma_job<20, 1>(fr, JC.tile, L, lane, fs), JC.tile, lane, L.zv, L.sv, kRsv);
-    } else if (W < 4) {
-      // distance rows (the 22-term sums) one per lane on w0, w1; the rest on w2, w3
-      if (t + 1 < maxnf) {
-        constexpr int kIt = kBands + 7 + kCeps, kLight = kBands + 7;
-        if (tid < S * kCeps)
-          feat_c(t + 1, (tid >> 3) * kIt + kLight + (tid & 7));
+    WSTAMP_BEGIN();
+    // ---- phase B: candidates of vad(u-1), noise(u-2), denoise(u-3); gains(u-4);
+    // spectral variability(u+1); raw features of u+2 staged
+    if (W < 6) {
+      if (live(fD)) {
+        const int dst = seg_half(kSd, 0);
+        const bool on = on_of(fD);
+        if (W < 4)
+          epi_h<96>(L, mma_job<2, 6>(fr, W, L, lane, fD), W, lane, ra[6], L.zd, L.sd, dst, on);
+        else if (W == 4)
+          epi_h<96>(L, mma_job<8, 6>(fr, 4, L, lane, fD), 4, lane, ra[6], L.zd, L.sd, dst, on);
         else
-          for (int k = tid - S * kCeps; k < S * kLight; k += 4 * 64 - S * kCeps)
-            feat_c(t + 1, (k / kLight) * kIt + k % kLight);
+          epi_h<96>(L, mma_job<10, 6>(fr, 5, L, lane, fD), 5, lane, ra[6], L.zd, L.sd, dst, on);
       }
-    } else if (t >= 1) {  // gain smoothing g = max(g, .6*lastg) (denoise.c), frame t-1
-      const int f1 = t - 1;
-      for (int idx = lane; idx < S * kBands; idx += 64) {
-        const int s = idx / kBands, i = idx - s * kBands;
-        if (!L.act[f1 & 7][s]) continue;
-        const long long f = L.fbase[s] + f1;
-        const float gi = L.gout[s][i];
-        const float al = .6f * L.lastg[s][i];
-        const float gsm = (gi > al) ? gi : al;
-        L.lastg[s][i] = gsm;
-        a.gr[f * kBands + i] = gi;
-        a.gs[f * kBands + i] = gsm;
+      if (W == 4 && live(fN))
+        epi_h<48>(L, mma_job<15, 4>(fr, 1, L, lane, fN), 1, lane, ra[4], L.zn, L.sn, seg_half(kSn, fN & 1), on_of(fN));
+      if (W < 2 && u + 1 < maxnf) feat_d(u + 1);
+      // gain smoothing g = max(g, .6*lastg) (denoise.c), frame u-4, on w2, w3, w5
+      if ((W == 2 || W == 3 || W == 5) && live(fO)) {
+        const int gl = lane + 64 * (W == 5 ? 2 : W - 2);
+        for (int idx = gl; idx < S * kBands; idx += 3 * 64) {
+          const int s = idx / kBands, i = idx - s * kBands;
+          if (!L.act[fO & 7][s]) continue;
+          const long long f = L.fbase[s] + fO;
+          const float gi = L.gout[s][i];
+          const float al = .6f * L.lastg[s][i];
+          const float gsm = (gi > al) ? gi : al;
+          L.lastg[s][i] = gsm;
+          a.gr[f * kBands + i] = gi;
+          a.gs[f * kBands + i] = gsm;
+        }
+      }
+    } else {
+      if (live(fN)) {
+        const int t = W == 6 ? 0 : 2;
+        const f4 acc = W == 6 ? mma_job<10, 4>(fr, 0, L, lane, fN) : mma_job<11, 4>(fr, 2, L, lane, fN);
+        epi_h<48>(L, acc, t, lane, ra[4], L.zn, L.sn, seg_half(kSn, fN & 1), on_of(fN));
+      }
+      if (live(fV)) {
+        const int t = W == 6 ? 1 : 0;
+        const f4 acc = W == 6 ? mma_job<15, 2>(fr, 1, L, lane, fV) : mma_job<16, 2>(fr, 0, L, lane, fV);
+        epi_h<24>(L, acc, t, lane, ra[2], L.zv, L.sv, seg_half(kSv, fV % 3), on_of(fV));
       }
     }
+    if (pf_lane) L.pf[pfs][pfi] = pf_next;  // read by the next phase A only
+    WSTAMP_END(1);
     __syncthreads();
     RSTAMP(1);
-    if (!fr_t) break;
-    // ---- P2: vad h(t) [w4, w5], spectral variability(t+1) [w0]
-    if (W == 4 || W == 5)
-      epi_h<24>(L, mma_job<22, 2>(fr, JD.tile, L, lane, fs), JD.tile, lane, ra[2], L.zv, L.sv, kSv, on_t);
-    else if (W < 2 && t + 1 < maxnf)
-      feat_d(t + 1);
-    __syncthreads();
-    RSTAMP(2);
-    // ---- P3: noise z|r(t) [w0..5], vad_output(t) [w6]; raw features of t+2 requested
-    const float pf_next = fetch(t + 2);
-    if (W < 6) {
-      epi_zr<48>(L, mma_job<0, 3>(fr, JA.tile, L, lane, fs), JA.tile, lane, L.zn, L.sn, kRsn);
-    } else if (W == 6) {
-      const f4 acc = mma_job<17, 8>(fr, JB.tile, L, lane, fs);
-      if (lane < 16 && on_t) a.vadf[L.fbase[col] + t] = activate(L.tt, ra[8], kWs * acc[0]);
-    }
-    __syncthreads();
-    RSTAMP(3);
-    // ---- P4: noise h(t) [w5..7]
-    if (W >= 5) epi_h<48>(L, mma_job<5, 4>(fr, JE.tile, L, lane, fs), JE.tile, lane, ra[4], L.zn, L.sn, kSn, on_t);
-    __syncthreads();
-    RSTAMP(4);
-    // ---- P5: denoise z|r(t), A from LDS: tile w [w0..7] and w + 8 [w0..3]
-    epi_zr<96>(L, mma_job<-1, 5>(fr, W, L, lane, fs), W, lane, L.zd, L.sd, kRsd);
-    if (W < 4) epi_zr<96>(L, mma_job<-1, 5>(fr, W + 8, L, lane, fs), W + 8, lane, L.zd, L.sd, kRsd);
-    __syncthreads();
-    RSTAMP(5);
-    // ---- P6: denoise h(t) [w2..7]; raw features of t+2 staged
-    if (W >= 2) epi_h<96>(L, mma_job<10, 6>(fr, JF.tile, L, lane, fs), JF.tile, lane, ra[6], L.zd, L.sd, kSd, on_t);
-    if (pf_lane) L.pf[pfs][pfi] = pf_next;
-    __syncthreads();
-    RSTAMP(6);
   }
-  STAMP_FLUSH(48, 7);
+#ifdef FVAD_STAMPS
+  if (lane == 0 && a.stamps) {
+    atomicAdd(&a.stamps[W], wacc[0]);
+    atomicAdd(&a.stamps[8 + W], wacc[1]);
+  }
+#endif
+#undef WSTAMP_BEGIN
+#undef WSTAMP_END
+  STAMP_FLUSH(48, 2);
   // ---- state write-back (streams that ran at least one frame)
   for (int idx = tid; idx < S * kCeps * kBands; idx += kGNT) {
     const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);

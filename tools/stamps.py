@@ -33,10 +33,9 @@ elif MODE == "staged":
              "noise h", "denoise z|r", "denoise h", "denoise_output", "gains + outputs + prefetch", "next act"]
     FFTA = ["group setup", "window scatter (global loads)", "FFT 960 x F", "X store + band sums + log10",
             "Ly chain + silence", "DCT(Ly)"]
-if MODE == "fp16":  # k_gru16 phases (fvad_gru16.hip), stamps[48..54]
-    GRU = ["P0 dense(t) + den_out(t-1)", "P1 vad z|r + features(t+1) + gains(t-1)",
-           "P2 vad h + spectral variability(t+1)", "P3 noise z|r + vad_out", "P4 noise h", "P5 denoise z|r",
-           "P6 denoise h"]
+if MODE == "fp16":  # k_gru16 supersteps (fvad_gru16.hip), stamps[48..49]
+    GRU = ["A  z|r gates vad(u-1) noise(u-2) denoise(u-3), dense(u), outputs, features(u+1)",
+           "B  candidates vad(u-1) noise(u-2) denoise(u-3), gains(u-4), spectral var(u+1)"]
 L = fvad.lib()
 L.fvad_engine_stamps.restype = C.c_int
 L.fvad_engine_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
@@ -52,10 +51,13 @@ buf = (C.c_ulonglong * 64)()
 assert L.fvad_engine_stamps(e.h, buf, 64) == 0
 if MODE == "fp16":
     frames = (B // 16) * 2 * T
-    gt = sum(buf[48:55])
+    gt = sum(buf[48:48 + len(GRU)])
     print("k_gru16: stamped cycles per frame step per WG: %.0f" % (gt / frames))
     for i, n in enumerate(GRU):
         print("%2d %-44s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[48 + i] / max(1, gt), buf[48 + i] / frames))
+    print("per-wave busy cycles per frame step (phase A | phase B):")
+    for w in range(8):
+        print("  w%d %8.0f | %8.0f" % (w, buf[w] / frames, buf[8 + w] / frames))
     sys.exit(0)
 tot = sum(buf[:24]) if MODE == "fused" else (sum(buf[:2]) if len(NAMES) > 12 else sum(buf[:12]))
 frames = B * 2 * T
