@@ -28,7 +28,10 @@ namespace fvad {
 //   Q5 remove_doubling products: lane = (frame, candidate c); candidate c's
 //      xcorr at T-1, T, T+1 share a sliding window of 3, plus xcorr(T1b);
 //      operands are read as aligned pairs (ds_read_b64: 64 banks, 2 steps
-//      per read), the lane's window parity resolved by selects
+//      per read), the lane's window parity resolved by selects.  Meanwhile
+//      wave 2 (idle in Q5) walks remove_doubling's yy_lookup recurrence from
+//      xx, lane per frame, on xf in LDS and leaves it in the tile buffer; the
+//      candidates' pitch gains read it after a barrier.
 // ---------------------------------------------------------------------------
 constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
 constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
@@ -242,18 +245,16 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     __syncthreads();
     RSTAMP(4);
     // Q5
-    if (tid < 15 * kPcF) {
+    const bool q5 = tid < 15 * kPcF && fval[tid / 15] && (tid % 15 == 0 || tid % 15 - 1 < nvs[tid / 15]);
+    float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
+    int Tc = 0, Tb = 0;
+    if (q5) {
       const int fr = tid / 15, c = tid - 15 * fr;
-      if (fval[fr] && (c == 0 || c - 1 < nvs[fr])) {
+      {
         const int T0 = T0s[fr];
-        const int Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
-        const int Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
-        // yy_lookup and xx gathers, consumed after the products
-        const float yyA = T[(ptile::kYy + Tc) * ptile::kQuarter + fr];
-        const float yyB = T[(ptile::kYy + Tb) * ptile::kQuarter + fr];
-        const float xx = T[ptile::kXx * ptile::kQuarter + fr];
+        Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
+        Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
         const float *X = xf[fr] + (kPitchMax >> 1);
-        float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
         // Operands come in 8-byte aligned pairs (ds_read_b64): the broadcast
         // x[j], x[j+1]; the window stream X[j - Tc - 1 + t] and the T1b stream
         // X[j - Tb + t], each read from the even index at or below its start
@@ -294,6 +295,31 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
           b1 = ob ? rn.x : rp.y;
           rp = rn;
         }
+      }
+    } else if (tid >= 128 && tid < 128 + kPcF && fval[tid - 128]) {
+      // yy_lookup[i] = max(0, yy), yy = (yy + x[-i]^2) - x[480-i]^2 from yy = xx,
+      // x = xf + 384 (remove_doubling), into the tile buffer's yy rows
+      const int fr = tid - 128;
+      float *Y = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter + h * kPcF + fr;
+      const float *xr = xf[fr];
+      float yy = Y[ptile::kXx * ptile::kQuarter];
+      Y[ptile::kYy * ptile::kQuarter] = yy;
+#pragma unroll 8
+      for (int i = 1; i <= 384; i++) {
+        const float va = xr[384 - i], vb = xr[864 - i];
+        yy = yy + va * va - vb * vb;
+        Y[(ptile::kYy + i) * ptile::kQuarter] = (0 > yy) ? 0 : yy;
+      }
+    }
+    __syncthreads();  // the yy rows are in the tile buffer (workgroup-scope fence)
+    RSTAMP(6);
+    if (q5) {
+      const int fr = tid / 15, c = tid - 15 * fr;
+      {
+        const int T0 = T0s[fr];
+        const float yyA = T[(ptile::kYy + Tc) * ptile::kQuarter + fr];
+        const float yyB = T[(ptile::kYy + Tb) * ptile::kQuarter + fr];
+        const float xx = T[ptile::kXx * ptile::kQuarter + fr];
         float *rg = a.rec + fidx[fr] * rec::kSize;
         const int off = pitch_offset(aP, a0, aM);
         if (c == 0) {
@@ -319,7 +345,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(5);
     g = gq;
   }
-  STAMP_FLUSH(32, 6);
+  STAMP_FLUSH(32, 7);
 }
 
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream) {

@@ -10,7 +10,7 @@
 //                           log/floor chain (Ly, E, silence gate), DCT(Ly)
 //                           (fvad_wave.hip)
 //   k_plpc    lane/frame    pitch_downsample (x_lp, autocorr, LPC, FIR5) and
-//                           every serial energy recurrence (Syy, xx, yy)
+//                           the serial energy recurrences Syy and xx
 //   k_pcorr   wg/8 frames   coarse and fine xcorr + find_best_pitch, every
 //                           remove_doubling inner product for every candidate
 //                           period (fvad_pitch.hip)
@@ -200,15 +200,16 @@ __global__ void __launch_bounds__(64) k_prep3(StagedArgs a) {
 // to its sequential selection), split by how each part parallelises:
 //
 //   k_plpc   lane per frame.  Every serial chain that depends only on the
-//            frame itself: x_lp, the 5 autocorr sums (860 terms each), LPC,
-//            the 5-tap FIR, the Syy recurrences of both find_best_pitch calls,
-//            xx and the yy_lookup recurrence.  A wave owns a tile of 64
+//            frame itself and streams its pitch buffer: x_lp, the 5 autocorr
+//            sums (860 terms each), LPC, the 5-tap FIR, the Syy recurrences of
+//            both find_best_pitch calls and xx.  A wave owns a tile of 64
 //            streams at one frame position (lane = stream), so all 64 lanes
 //            walk a chain.  Writes xf and the sequences to the tile buffer.
-//   k_pcorr  16 frames per workgroup, xf resident in LDS.  The inner products
-//            (coarse xcorr: 147 lags x 240, fine xcorr at <= 10 lags, the 59
-//            remove_doubling products), both find_best_pitch scans (lane per
-//            frame) and the pitch record for k_select.
+//   k_pcorr  8 frames per workgroup, xf resident in LDS.  The inner products
+//            (coarse xcorr: 147 lags x 240, fine xcorr at <= 10 lags, the
+//            remove_doubling products), both find_best_pitch scans and the
+//            yy_lookup recurrence (lane per frame) and the pitch record for
+//            k_select (fvad_pitch.hip).
 // Every C-order sum stays on one lane in its original order.
 // ---------------------------------------------------------------------------
 // Pitch record of a frame (k_pcorr -> k_select): everything of
@@ -324,17 +325,15 @@ struct Fir5State {
 // lane stores two float4 of its quarter's [row][16] block, so one store
 // instruction writes 1 KB in four 256-byte runs instead of 256 bytes in four
 // 64-byte pieces (measured: the per-step dword row stores cost k_plpc ~0.4 ms).
-// Row loads of the read-back (pass 2: xf[n - 480]; pass 3: the yy operands)
+// Row loads of the read-back (xf[n - 480] for the Syy recurrences)
 // take the same route backwards: two float4 per lane of the quarter's block,
 // then LDS, then each lane reads its column.
 struct OutStage {
-  float xf[kLpStep][64];      // xf rows of the chunk (pass 2), yy rows (pass 3)
+  float xf[kLpStep][64];      // xf rows of the chunk
   float sf[kLpStep][64];      // fine Syy rows
   float sc[kLpStep / 2][64];  // coarse Syy rows
-  float in[kLpStep][64];      // read-back rows (pass 2), x[-i] rows (pass 3)
+  float in[kLpStep][64];      // read-back rows xf[n - 480]
 };
-// pass 3 stages its x[480 - i] rows in the fine-Syy stage (unused after pass 2)
-#define in2 sf
 struct RowLd {
   float4 v[2];
 };
@@ -421,25 +420,18 @@ __device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, float
 }
 static_assert(384 % kLpStep == 0 && 480 % kLpStep == 0 && kLpStep % 2 == 0, "pass-2 regions");
 
-// Memory-level parallelism.  The kernel runs at 2 workgroups per CU (2 waves
-// per SIMD), and a pass whose chunk waits on its own loads stalls for a whole
-// HBM round trip (~2 us under load) per 8 steps.  So every pass walks its
-// chunks through a register ring: the loads of the next kLpPf (passes 1, 2:
-// pitch-buffer chunks and the Syy read-back) or kYyPf (pass 3) chunks are in
-// flight while a chunk is summed.  The chunk loops are unrolled by the ring
-// depth so ring slots are static registers.
+// Both passes walk their chunks through a register ring: the loads of the
+// next kLpPf chunks (pitch-buffer chunks and the Syy read-back) are in flight
+// while a chunk is summed; the chunk loops are unrolled by the ring depth so
+// ring slots are static registers (depths 1-4 measured alike; 1 kept).
 #ifndef FVAD_PLPC_OCC
 #define FVAD_PLPC_OCC 2
 #endif
 #ifndef FVAD_LP_PF
 #define FVAD_LP_PF 1
 #endif
-#ifndef FVAD_YY_PF
-#define FVAD_YY_PF 1
-#endif
-constexpr int kLpPf = FVAD_LP_PF, kYyPf = FVAD_YY_PF;
-constexpr int kYyChunks = 384 / kLpStep;
-static_assert(kLpChunks % kLpPf == 0 && kYyChunks % kYyPf == 0, "prefetch rings must divide the passes");
+constexpr int kLpPf = FVAD_LP_PF;
+static_assert(kLpChunks % kLpPf == 0, "prefetch ring must divide the passes");
 
 // One pass over a tile's pitch-buffer chunks: chunk c is staged and handed
 // to body(c, slot) while the loads of chunks c + 1 .. c + kLpPf are in flight;
@@ -590,40 +582,8 @@ __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
     const float xx = fs.xx;
     out[ptile::kXx * ptile::kQuarter] = xx;
 
-    // pass 3: yy_lookup[i] = max(0, yy), yy += x[-i]^2 - x[480-i]^2 (x = xf + 384),
-    // i = 1 .. 384 in chunks of kLpStep, the rows of the next kYyPf chunks in flight
-    float yy = xx;
-    out[ptile::kYy * ptile::kQuarter] = xx;
-    // the last chunks of pass 2 stored the first rows read here (other lanes' stores)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    RowLd ya[kYyPf], yb[kYyPf];
-    // chunk c: i = i0 .. i0 + 7 (i0 = 1 + 8c) reads rows 383 - 8c - u and 863 - 8c - u
-    auto yy_fetch = [&](int c, int slot) {
-      fetch_rows<kLpStep>(qbase, ptile::kXf + 384 - kLpStep - c * kLpStep, ya[slot], lane);
-      fetch_rows<kLpStep>(qbase, ptile::kXf + 864 - kLpStep - c * kLpStep, yb[slot], lane);
-    };
-#pragma unroll
-    for (int d = 0; d < kYyPf; d++) yy_fetch(d, d);
-    for (int c0 = 0; c0 < kYyChunks; c0 += kYyPf) {
-#pragma unroll
-      for (int dd = 0; dd < kYyPf; dd++) {
-        const int c = c0 + dd, i0 = 1 + c * kLpStep;
-        stage_rows(ya[dd], ob.in, lane);
-        stage_rows(yb[dd], ob.in2, lane);
-        if (c + kYyPf < kYyChunks) yy_fetch(c + kYyPf, dd);
-        wave_sync();
-#pragma unroll
-        for (int u = 0; u < kLpStep; u++) {
-          const float va = ob.in[kLpStep - 1 - u][lane], vb = ob.in2[kLpStep - 1 - u][lane];
-          yy = yy + va * va - vb * vb;
-          ob.xf[u][lane] = (0 > yy) ? 0 : yy;
-        }
-        wave_sync();
-        flush_rows<kLpStep>(qbase, ptile::kYy + i0, ob.xf, lane);
-        wave_sync();
-      }
-    }
+    // yy_lookup (remove_doubling's energy recurrence from xx) is k_pcorr's:
+    // it walks it on a wave its product phase leaves idle, from xf in LDS
     RSTAMP(2);
     __syncthreads();
     if (tid == 0) gq = take_group(a, kWorkPlpc);
