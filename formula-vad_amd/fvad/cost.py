@@ -132,16 +132,20 @@ def staged_kernels(n_channels=2, fft_size=2048):
     spec = 481 * 8  # one complex spectrum
     pitch = (p["pitch downsample + autocorr + LPC + FIR5"] + p["coarse xcorr 147x240 + find_best_pitch"] +
              p["fine xcorr <=10x480 + find_best_pitch"] + p["remove_doubling"] - rd * 12)
-    # k_plpc: x_lp, autocorr, LPC, FIR and the serial energy recurrences
-    # (coarse / fine Syy init + updates, xx, yy_lookup); k_pcorr the rest
+    # k_plpc: x_lp, autocorr, LPC, FIR and the serial energy recurrences of
+    # both find_best_pitch scans (Syy init + updates) and xx; k_pcorr the rest,
+    # remove_doubling's yy_lookup recurrence included (r2)
     plpc = (p["pitch downsample + autocorr + LPC + FIR5"] + 240 * 2 + 147 * 4 + 480 * 2 + 294 * 4 +
-            480 * 2 + 384 * 4)
+            480 * 2)
     k = {
         "k_prep3": (p["prep: s16 scale + HP biquad + rms"], 480 * 4 * 2 + 4.0 / C),
         "k_fftAw": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly,
                    960 * 4 + spec + 22 * 4 * 2 + 4),
-        "k_plpc": (plpc, 1728 * 4 + PTILE_ROWS * 4),
-        "k_pcorr": (pitch - plpc - rd * 4, (864 + 147 + 10 + 29 + 1) * 4 + 80 * 4),
+        # k_plpc: the pitch buffer in; xf, the Syy sequences and xx out.
+        # k_pcorr: those in, yy_lookup (read back at <= 29 periods) and the
+        # pitch record out
+        "k_plpc": (plpc, 1728 * 4 + (PTILE_ROWS - 385) * 4),
+        "k_pcorr": (pitch - plpc - rd * 4, (864 + 147 + 10 + 1 + 385 + 29) * 4 + 80 * 4),
         "k_select": (rd * 4 + rd * 12, 80 * 4 + 4),
         "k_pspecw": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
         # k_rnn3: cepstral memory, spectral variability, GRU stack, gain
