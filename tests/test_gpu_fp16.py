@@ -175,3 +175,35 @@ def test_fp16_resident_bench_shape(fvad_mod, oracle_mod, models):
         assert d <= VAD_ABS, (s, d)
         assert np.array_equal(fr["ratio"], np.concatenate([o["ratio"][:, s] for o in outs]))
     print("fp16 bench shape: max |dvad| %.3g over %d streams" % (worst, len(range(0, B, 61))))
+
+
+def test_fp16_fft_size_1000_segments(fvad_mod, oracle_mod, models):
+    """fp16 mode with a non-default VAD.Config (fft_size 1000: FFT B on the
+    mixed-radix block kernel, bands from FFT.freqToBin) and device VADMachines:
+    vad within tolerance, volume ratios and window ratios bit-identical (they
+    come before the GRU), band sums within BAND_REL, segment lists identical
+    to the oracle's (measured)."""
+    m, om = models
+    fft_size = 1000
+    step = np.float32(48000) / np.float32(fft_size)
+    bins = tuple(int(np.floor(np.float32(f) / step + np.float32(0.5))) for f in (100.0, 1500.0))
+    ids, secs = (0, 19), (20.0, 13.3)
+    streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip(ids, secs)]
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=50, fft_size=fft_size, bands=(bins,), mode="fp16")
+    eng.attach_vadm()
+    got = pu.engine_run(fvad_mod, eng, streams, 50, denoised=False)
+    for s, x in enumerate(streams):
+        n = x.shape[1]
+        p = oracle_mod.Pipeline(2, om, fft_size=fft_size, trace_frames=n // 480 + 1,
+                                trace_windows=n // fft_size + 2)
+        for k in range(0, n, 48000):
+            p.push([x[0, k:k + 48000], x[1, k:k + 48000]])
+        fr, wi = p.trace()
+        g = got[s]
+        assert float(np.abs(fr["vad"] - g["vad"]).max()) <= VAD_ABS
+        assert np.array_equal(fr["ratio"], g["ratio"])
+        assert len(wi) == int(g["win_flag"].sum()) > 0
+        assert np.array_equal(wi["ratio"], g["win_ratio"])
+        b_ref, b_got = wi["band"][:, :2], g["band"][:, :, 0]
+        assert float(np.abs(b_ref - b_got).max() / np.abs(b_ref).max()) <= BAND_REL
+        assert [(a, b) for a, b, _, _ in eng.segments(s)] == [(a, b) for a, b, _, _ in p.segments()]
