@@ -22,16 +22,15 @@ namespace fvad {
 //   Q1 coarse xcorr: lane = (frame, 5 consecutive lags), a register window of
 //      5 y values slides one sample per step (2 LDS reads per 5 MACs)
 //   Q2 coarse find_best_pitch, lane per frame; the fine Syy values at the
-//      <= 10 candidate lags are fetched here, used in Q4
+//      <= 10 candidate lags are fetched here, used in Q4.  Meanwhile wave 1
+//      walks remove_doubling's yy_lookup recurrence from xx, lane per frame,
+//      on xf in LDS, into the tile buffer (read in Q5)
 //   Q3 fine xcorr at the <= 10 lags within +-2 of 2*best (others are 0)
 //   Q4 fine find_best_pitch + pseudo-interpolation -> T0, candidate count
 //   Q5 remove_doubling products: lane = (frame, candidate c); candidate c's
 //      xcorr at T-1, T, T+1 share a sliding window of 3, plus xcorr(T1b);
 //      operands are read as aligned pairs (ds_read_b64: 64 banks, 2 steps
-//      per read), the lane's window parity resolved by selects.  Meanwhile
-//      wave 2 (idle in Q5) walks remove_doubling's yy_lookup recurrence from
-//      xx, lane per frame, on xf in LDS and leaves it in the tile buffer; the
-//      candidates' pitch gains read it after a barrier.
+//      per read), the lane's window parity resolved by selects
 // ---------------------------------------------------------------------------
 constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
 constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
@@ -175,6 +174,22 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         const int i = 2 * bst[u / 5] - 2 + (u % 5);
         sfv[u] = (i >= 0 && i < 294) ? T[(ptile::kSf + i) * ptile::kQuarter + fr] : 0.0f;
       }
+    } else if (tid >= 64 && tid < 64 + kPcF && fval[tid - 64]) {
+      // meanwhile wave 1 (idle in the scan) walks remove_doubling's yy_lookup
+      // recurrence: yy_lookup[i] = max(0, yy), yy = (yy + x[-i]^2) - x[480-i]^2
+      // from yy = xx, x = xf + 384; into the tile buffer's yy rows, read by Q5
+      // after the barriers of Q2..Q4
+      const int fr = tid - 64;
+      float *Y = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter + h * kPcF + fr;
+      const float *xr = xf[fr];
+      float yy = Y[ptile::kXx * ptile::kQuarter];
+      Y[ptile::kYy * ptile::kQuarter] = yy;
+#pragma unroll 8
+      for (int i = 1; i <= 384; i++) {
+        const float va = xr[384 - i], vb = xr[864 - i];
+        yy = yy + va * va - vb * vb;
+        Y[(ptile::kYy + i) * ptile::kQuarter] = (0 > yy) ? 0 : yy;
+      }
     }
     __syncthreads();
     RSTAMP(2);
@@ -245,16 +260,18 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     __syncthreads();
     RSTAMP(4);
     // Q5
-    const bool q5 = tid < 15 * kPcF && fval[tid / 15] && (tid % 15 == 0 || tid % 15 - 1 < nvs[tid / 15]);
-    float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
-    int Tc = 0, Tb = 0;
-    if (q5) {
+    if (tid < 15 * kPcF) {
       const int fr = tid / 15, c = tid - 15 * fr;
-      {
+      if (fval[fr] && (c == 0 || c - 1 < nvs[fr])) {
         const int T0 = T0s[fr];
-        Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
-        Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
+        const int Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
+        const int Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
+        // yy_lookup and xx gathers, consumed after the products
+        const float yyA = T[(ptile::kYy + Tc) * ptile::kQuarter + fr];
+        const float yyB = T[(ptile::kYy + Tb) * ptile::kQuarter + fr];
+        const float xx = T[ptile::kXx * ptile::kQuarter + fr];
         const float *X = xf[fr] + (kPitchMax >> 1);
+        float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
         // Operands come in 8-byte aligned pairs (ds_read_b64): the broadcast
         // x[j], x[j+1]; the window stream X[j - Tc - 1 + t] and the T1b stream
         // X[j - Tb + t], each read from the even index at or below its start
@@ -295,31 +312,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
           b1 = ob ? rn.x : rp.y;
           rp = rn;
         }
-      }
-    } else if (tid >= 128 && tid < 128 + kPcF && fval[tid - 128]) {
-      // yy_lookup[i] = max(0, yy), yy = (yy + x[-i]^2) - x[480-i]^2 from yy = xx,
-      // x = xf + 384 (remove_doubling), into the tile buffer's yy rows
-      const int fr = tid - 128;
-      float *Y = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter + h * kPcF + fr;
-      const float *xr = xf[fr];
-      float yy = Y[ptile::kXx * ptile::kQuarter];
-      Y[ptile::kYy * ptile::kQuarter] = yy;
-#pragma unroll 8
-      for (int i = 1; i <= 384; i++) {
-        const float va = xr[384 - i], vb = xr[864 - i];
-        yy = yy + va * va - vb * vb;
-        Y[(ptile::kYy + i) * ptile::kQuarter] = (0 > yy) ? 0 : yy;
-      }
-    }
-    __syncthreads();  // the yy rows are in the tile buffer (workgroup-scope fence)
-    RSTAMP(6);
-    if (q5) {
-      const int fr = tid / 15, c = tid - 15 * fr;
-      {
-        const int T0 = T0s[fr];
-        const float yyA = T[(ptile::kYy + Tc) * ptile::kQuarter + fr];
-        const float yyB = T[(ptile::kYy + Tb) * ptile::kQuarter + fr];
-        const float xx = T[ptile::kXx * ptile::kQuarter + fr];
         float *rg = a.rec + fidx[fr] * rec::kSize;
         const int off = pitch_offset(aP, a0, aM);
         if (c == 0) {
@@ -345,7 +337,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(5);
     g = gq;
   }
-  STAMP_FLUSH(32, 7);
+  STAMP_FLUSH(32, 6);
 }
 
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream) {
