@@ -75,7 +75,6 @@ struct fvad_engine {
   // k_vadm_hbm runs on a side stream over copies of one push's window outputs,
   // overlapped with the next push (it only depends on its own state)
   hipStream_t side = nullptr;
-  hipStream_t aux = nullptr;  // staged mode: k_fftAw concurrent with the pitch branch (FVAD_FORK)
   // staged mode: k_prep3 runs on pstream, so push k's prep overlaps push k-1's
   // kernels; xs / ratio / ticks are double-buffered (d_xs, d_ratio, d_ticks
   // alias the buffer of the latest push), buffer b is reused once the push that
@@ -86,7 +85,6 @@ struct fvad_engine {
   hipEvent_t ev_prep_done[2] = {}, ev_buf_free[2] = {};
   bool buf_busy[2] = {false, false};
   int next_buf = 0;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int n_events = 0;           // timing events per launch
   int last_event = 0;         // the one recorded last (the launch's end)
   hipEvent_t ev_copy = nullptr, ev_vadm = nullptr, ev_vt[2][2] = {};  // [slot][begin/end] timing pairs
@@ -304,7 +302,6 @@ void free_all(fvad_engine *e) {
   for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
   if (e->side) (void)hipStreamDestroy(e->side);
-  if (e->aux) (void)hipStreamDestroy(e->aux);
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
   if (e->cstream) (void)hipStreamDestroy(e->cstream);
   for (auto &sl : e->slots) {
@@ -320,8 +317,6 @@ void free_all(fvad_engine *e) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : e->ev_buf_free)
     if (ev) (void)hipEventDestroy(ev);
-  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->stream) (void)hipStreamDestroy(e->stream);
 }
 
@@ -403,10 +398,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
   if (c.mode != FVAD_MODE_FUSED &&
-      (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
-       hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
-       hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess ||
-       hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess ||
+      (hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[0], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[1], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_buf_free[0], hipEventDisableTiming) != hipSuccess ||
@@ -611,21 +603,13 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.raw_s16 = e->raw_s16;
   a.vadm = e->vadm;
   a.stamps = e->d_stamps;
-  // FVAD_FORK=1 runs k_fftAw on the aux stream beside the pitch branch.  Off by
-  // default: both are persistent grids sized to the whole GPU, and sharing it
-  // stretches the later one (measured 15.0 vs 14.1 ms per push).
-  static const bool fork = [] {
-    const char *v = getenv("FVAD_FORK");
-    return v && atoi(v) == 1;
-  }();
-  const fvad::StagedStreams st{e->stream, fork ? e->aux : e->stream, e->ev_fork, e->ev_join};
   if (c.use_denoiser) {
     HIP_TRY(fvad::launch_prep(a, e->pstream, timed ? e->ev : nullptr));
     HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
     HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
     // window output set b is free once push k-2's k_vadm_hbm has read it
     if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
-    HIP_TRY(fvad::launch_staged(a, e->grid_frames, st, timed ? e->ev : nullptr));
+    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr));
   } else {
     // no denoiser: raw input frames to the ring, windows, FFT B, all on the
     // engine stream after the input copy (queued on the prep stream)

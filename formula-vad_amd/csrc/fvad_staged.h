@@ -102,14 +102,6 @@ struct StagedArgs {
   unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn3
 };
 
-// Streams of one launch: k_fftAw runs on `aux` concurrently with the pitch
-// branch (k_plpc -> k_pcorr -> k_select) on `main` (FVAD_FORK=1; by default
-// aux == main); `fork` / `join` order them (k_prep3 before both, k_pspecw
-// after both).
-struct StagedStreams {
-  hipStream_t main, aux;
-  hipEvent_t fork, join;
-};
 // Timing events: kernel i runs between ev[kStagedTime[i][0]] and
 // ev[kStagedTime[i][1]]; ev[0] and ev[kStagedLast] bracket the launch.
 constexpr int kStagedEvents = 15, kStagedLast = 13;
@@ -120,7 +112,7 @@ constexpr int kStagedTime[kStagedKernels][2] = {{0, 1}, {2, 3},   {14, 4},  {4, 
 hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev);
 // Launch the other 10 kernels; when ev != nullptr their timing events are
 // recorded.
-hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev);
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev);
 // k_pcorr over `tiles` pitch tiles (fvad_pitch.hip)
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream);
 const char *staged_kernel_name(int i);

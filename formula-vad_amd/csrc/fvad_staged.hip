@@ -1702,8 +1702,7 @@ hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) 
   return hipSuccess;
 }
 
-hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st, hipEvent_t *ev) {
-  hipStream_t stream = st.main;
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev) {
   static const int g_plpc = resident_blocks(k_plpc, 256, n_cu);
   const long long frames = (long long)a.n_streams * a.V;
   auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
@@ -1712,21 +1711,13 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   FVAD_LAUNCH_TRY(hipMemsetAsync(a.work, 0, kWorkSlots * kQueues * sizeof(unsigned), stream));
 #define REC(k) \
   if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[k], stream))
-#define REC_AUX(k) \
-  if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[k], st.aux))
-  // fork: k_fftAw (aux) || pitch branch (main); both only read xs and write
-  // disjoint buffers (X, Ex, Lyf, silence | ptile, rec, pitch, pitch state).
-  // Without the fork (the default, aux == main) no fork / join events: a wait
-  // on the stream's own event still costs a barrier packet between kernels
-  const bool forked = st.aux != stream;
-  if (forked) {
-    FVAD_LAUNCH_TRY(hipEventRecord(st.fork, stream));
-    FVAD_LAUNCH_TRY(hipStreamWaitEvent(st.aux, st.fork, 0));
-  }
-  REC_AUX(2);
-  FVAD_LAUNCH_TRY(launch_wave(kWaveFftA, a, n_cu, st.aux));
-  REC_AUX(3);
-  if (forked) FVAD_LAUNCH_TRY(hipEventRecord(st.join, st.aux));
+  // k_fftAw and the pitch branch (k_plpc -> k_pcorr -> k_select) both only
+  // read xs; run side by side on two streams they stretch each other (both
+  // are persistent grids sized to the GPU: 15.0 vs 14.1 ms per push in r1),
+  // so they run in order on one stream
+  REC(2);
+  FVAD_LAUNCH_TRY(launch_wave(kWaveFftA, a, n_cu, stream));
+  REC(3);
   {
     const long long tiles = (long long)((a.n_streams + 63) / 64) * a.n_ticks * a.n_channels;
     REC(14);
@@ -1737,7 +1728,6 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   REC(5);
   FVAD_KERNEL_TRY(k_select, dim3((a.n_streams + kSelStreams - 1) / kSelStreams), dim3(64), 0, stream, a);
   REC(6);
-  if (forked) FVAD_LAUNCH_TRY(hipStreamWaitEvent(stream, st.join, 0));  // join
   REC(7);
   FVAD_LAUNCH_TRY(launch_wave(kWavePspec, a, n_cu, stream));
   REC(8);
@@ -1755,7 +1745,6 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, const StagedStreams &st,
   FVAD_LAUNCH_TRY(launch_fftb(a, n_cu, stream));
   REC(13);
 #undef REC
-#undef REC_AUX
   return hipSuccess;
 }
 
