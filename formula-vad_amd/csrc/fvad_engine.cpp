@@ -80,7 +80,7 @@ struct fvad_engine {
   // alias the buffer of the latest push), buffer b is reused once the push that
   // used it last has finished (ev_buf_free[b])
   hipStream_t pstream = nullptr;
-  float *d_xs_b[2] = {}, *d_ratio_b[2] = {};
+  float *d_xs_b[2] = {}, *d_ratio_b[2] = {}, *d_xlp_b[2] = {};
   int *d_ticks_b[2] = {};
   hipEvent_t ev_prep_done[2] = {}, ev_buf_free[2] = {};
   bool buf_busy[2] = {false, false};
@@ -103,7 +103,7 @@ struct fvad_engine {
   size_t vadm_buf_len = 0;
   int rnn_act[fvad::rnnimg::kMats] = {};
   long long *d_wstart = nullptr;
-  int V = 0, L = 0, wmax = 0, grid_frames = 0;
+  int V = 0, L = 0, LX = 0, wmax = 0, grid_frames = 0;
   int resident_ticks = 0;
   int n_kernels = 0;
   // per-kernel timing events, two sets used alternately so the host reads
@@ -285,7 +285,7 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
 
 void free_all(fvad_engine *e) {
   void *ptrs[] = {e->d_plan, e->d_weights, e->d_state, e->d_ring, e->d_pcm_b[0], e->d_pcm_b[1], e->d_xbuf, e->d_ratio_b[0],
-                  e->d_ratio_b[1], e->d_ticks_b[0], e->d_ticks_b[1], e->d_xs_b[0], e->d_xs_b[1],
+                  e->d_ratio_b[1], e->d_ticks_b[0], e->d_ticks_b[1], e->d_xs_b[0], e->d_xs_b[1], e->d_xlp_b[0], e->d_xlp_b[1],
                   e->d_vad,  e->wratio_b[0] ? e->wratio_b[0] : e->d_wratio,  e->wvad_b[0] ? e->wvad_b[0] : e->d_wvad,
                   e->band_b[0] ? e->band_b[0] : e->d_band, e->d_den,   e->wflag_b[0] ? e->wflag_b[0] : e->d_wflag,
                   e->d_model, e->d_stamps, e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
@@ -439,9 +439,11 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   } else {
     e->V = (int)(T * C);
     e->L = (fvad::kPitchBuf - fvad::kFrame) + e->V * fvad::kFrame;
+    e->LX = e->L / 2;
     e->wmax = (int)(T * fvad::kFrame / c.fft_size) + 2;
     const size_t F = B * e->V;
     if ((rc = dalloc(&e->d_xs_b[0], B * e->L)) || (rc = dalloc(&e->d_xs_b[1], B * e->L)) ||
+        (rc = dalloc(&e->d_xlp_b[0], B * e->LX)) || (rc = dalloc(&e->d_xlp_b[1], B * e->LX)) ||
         (rc = dalloc(&e->d_ratio_b[1], T * B)) || (rc = dalloc(&e->d_ticks_b[1], B)) || (rc = dalloc(&e->d_X, F * fvad::kFreq * 2)) ||
         (rc = dalloc(&e->d_P, F * fvad::kFreq * 2)) || (rc = dalloc(&e->d_Ex, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Ep, F * fvad::kBands)) || (rc = dalloc(&e->d_Exp, F * fvad::kBands)) ||
@@ -554,6 +556,8 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   a.ticks_valid = use_ticks ? e->d_ticks : nullptr;
   a.pcm = e->d_pcm;
   a.xs = e->d_xs;
+  a.xlp = e->d_xlp_b[b];
+  a.LX = e->LX;
   a.ratio = e->d_ratio;
   a.state = e->d_state;
   a.X = reinterpret_cast<float2 *>(e->d_X);

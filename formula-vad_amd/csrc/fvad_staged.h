@@ -63,6 +63,8 @@ struct StagedArgs {
   const int *ticks_valid;  // nullable
   const float *pcm;        // [t][s][c][480] normalised input
   float *xs;               // [s][L] high-passed s16-scale samples, 1248 history first
+  float *xlp;              // [s][LX] pitch_downsample's x_lp over xs (x_lp[m] from xs[2m-1..2m+1]),
+  int LX;                  //   624 history first (= 624 + V * 240); m = 0 unused
   float *ratio;            // [t][s] per-tick volume ratio
   float *state;            // [s][st::kWords]
   float2 *X;               // [f][481] analysis spectrum, then filtered/gained spectrum

@@ -50,6 +50,14 @@ __device__ __forceinline__ const float *frame_pb(const StagedArgs &a, int f) {
   const int s = f / a.V, v = f - s * a.V;
   return a.xs + (size_t)s * a.L + (size_t)v * kFrame;
 }
+// x_lp row of frame f: its x_lp[n] (n >= 1) is frame_xlp(a, f)[n]
+constexpr int kXlpHist = kHist / 2;  // 624
+__device__ __forceinline__ float *frame_xlp(const StagedArgs &a, int f) {
+  const int s = f / a.V, v = f - s * a.V;
+  return a.xlp + (size_t)s * a.LX + (size_t)v * (kFrame / 2);
+}
+// pitch_downsample's x_lp value from pitch-buffer samples x[2n-1], x[2n], x[2n+1] (n >= 1)
+__device__ __forceinline__ float xlp_value(float xm, float x0, float xp) { return .5f * (.5f * (xm + xp) + x0); }
 // frame index of slot fr of group g, or -1 (same rule as group_frames)
 __device__ __forceinline__ int frame_of(const StagedArgs &a, long long g, int F, int fr) {
   const long long f = g * F + fr;

@@ -96,12 +96,31 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
       const int f = frame_of(a, g, kWB, fr);
       if (f < 0) continue;
       float2 v[16];
-      wave_window(frame_pb(a, f) + (kPitchBuf - kWin), tb.hw, lane, v);
+      const float *pb = frame_pb(a, f);
+      // the frame's new x_lp values n = 624..863 (pitch buffer samples
+      // 1247..1727, inside the window): operands load before the transform
+      float q[4][3];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int n = kXlpHist + 64 * k + lane;
+        if (n < kXlp) {
+          q[k][0] = pb[2 * n - 1];
+          q[k][1] = pb[2 * n];
+          q[k][2] = pb[2 * n + 1];
+        }
+      }
+      wave_window(pb + (kPitchBuf - kWin), tb.hw, lane, v);
       wfft::run(v, tw, tb.tw, R, lane);
       float2 *X = a.X + (size_t)f * kFreq;
 #pragma unroll
       for (int r = 0; r < 8; r++)
         if (64 * r + lane < kFreq) X[64 * r + lane] = v[r];
+      float *xl = frame_xlp(a, f);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int n = kXlpHist + 64 * k + lane;
+        if (n < kXlp) xl[n] = xlp_value(q[k][0], q[k][1], q[k][2]);
+      }
 #pragma unroll
       for (int r = 0; r < 7; r++) {
         const int n = 64 * r + lane;

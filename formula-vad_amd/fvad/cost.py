@@ -135,17 +135,22 @@ def staged_kernels(n_channels=2, fft_size=2048):
     # k_plpc: x_lp, autocorr, LPC, FIR and the serial energy recurrences of
     # both find_best_pitch scans (Syy init + updates) and xx; k_pcorr the rest,
     # remove_doubling's yy_lookup recurrence included (r2)
-    plpc = (p["pitch downsample + autocorr + LPC + FIR5"] + 240 * 2 + 147 * 4 + 480 * 2 + 294 * 4 +
+    # x_lp itself (864 * 4 per frame in the reference) is computed once per
+    # push position: k_fftAw writes each frame's 240 new values into the x_lp
+    # rows (k_prep3 the history's), so the term is charged to k_fftAw
+    xlp = 864 * 4
+    plpc = (p["pitch downsample + autocorr + LPC + FIR5"] - xlp + 240 * 2 + 147 * 4 + 480 * 2 + 294 * 4 +
             480 * 2)
     k = {
         "k_prep3": (p["prep: s16 scale + HP biquad + rms"], 480 * 4 * 2 + 4.0 / C),
-        "k_fftAw": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly,
-                   960 * 4 + spec + 22 * 4 * 2 + 4),
-        # k_plpc: the pitch buffer in; xf, the Syy sequences and xx out.
+        "k_fftAw": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly + xlp,
+                   960 * 4 + spec + 22 * 4 * 2 + 4 + 240 * 4),
+        # k_plpc: the frame's x_lp window (+ 2 pitch-buffer samples for x_lp[0])
+        # in; xf, the Syy sequences and xx out.
         # k_pcorr: those in, yy_lookup (read back at <= 29 periods) and the
         # pitch record out
-        "k_plpc": (plpc, 1728 * 4 + (PTILE_ROWS - 385) * 4),
-        "k_pcorr": (pitch - plpc - rd * 4, (864 + 147 + 10 + 1 + 385 + 29) * 4 + 80 * 4),
+        "k_plpc": (plpc, (864 + 2) * 4 + (PTILE_ROWS - 385) * 4),
+        "k_pcorr": (pitch - xlp - plpc - rd * 4, (864 + 147 + 10 + 1 + 385 + 29) * 4 + 80 * 4),
         "k_select": (rd * 4 + rd * 12, 80 * 4 + 4),
         "k_pspecw": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
         # k_rnn3: cepstral memory, spectral variability, GRU stack, gain
