@@ -160,18 +160,24 @@ __global__ void __launch_bounds__(64) k_prep3(StagedArgs a) {
   const int C = a.n_channels, S = prep_streams(C), sb = blockIdx.x * S;
   const int ns = min(S, a.n_streams - sb);  // streams in this workgroup
   if (ns <= 0) return;
-  // pitch history of every stream -> xs[s][0..1248)
-  for (int idx = tid; idx < ns * kHist; idx += 64) {
-    const int s = idx / kHist, i = idx - s * kHist;
-    if (ticks_of(a, sb + s) > 0)
-      a.xs[(size_t)(sb + s) * a.L + i] = a.state[(size_t)(sb + s) * st::kWords + st::kPitch + kFrame + i];
-  }
-  // x_lp of the history (the first frame's x_lp[1..623]; k_fftAw writes the rest)
-  for (int idx = tid; idx < ns * kXlpHist; idx += 64) {
-    const int s = idx / kXlpHist, m = idx - s * kXlpHist;
-    if (m > 0 && ticks_of(a, sb + s) > 0) {
-      const float *h = a.state + (size_t)(sb + s) * st::kWords + st::kPitch + kFrame;
-      a.xlp[(size_t)(sb + s) * a.LX + m] = xlp_value(h[2 * m - 1], h[2 * m], h[2 * m + 1]);
+  // pitch history of every stream -> xs[s][0..1248), and its x_lp values
+  // (the first frame's x_lp[1..623]; k_fftAw writes the rest): one stream at a
+  // time, each lane's loads independent (unrolled), so the copies take a few
+  // memory latencies per stream rather than one per element
+  for (int s = 0; s < ns; s++) {
+    if (ticks_of(a, sb + s) == 0) continue;
+    const float *h = a.state + (size_t)(sb + s) * st::kWords + st::kPitch + kFrame;
+    float4 *x = reinterpret_cast<float4 *>(a.xs + (size_t)(sb + s) * a.L);
+#pragma unroll
+    for (int j = 0; j < (kHist / 4 + 63) / 64; j++) {
+      const int i = lane + 64 * j;
+      if (i < kHist / 4) x[i] = reinterpret_cast<const float4 *>(h)[i];
+    }
+    float *xl = a.xlp + (size_t)(sb + s) * a.LX;
+#pragma unroll
+    for (int j = 0; j < (kXlpHist + 63) / 64; j++) {
+      const int m = lane + 64 * j;
+      if (m > 0 && m < kXlpHist) xl[m] = xlp_value(h[2 * m - 1], h[2 * m], h[2 * m + 1]);
     }
   }
   {
@@ -194,12 +200,16 @@ __global__ void __launch_bounds__(64) k_prep3(StagedArgs a) {
   }
   __syncthreads();
   // pitch_buf after the last frame = the last 1728 samples of the row
-  for (int idx = tid; idx < ns * kPitchBuf; idx += 64) {
-    const int s = idx / kPitchBuf, i = idx - s * kPitchBuf;
+  for (int s = 0; s < ns; s++) {
     const int nt = ticks_of(a, sb + s);
-    if (nt > 0)
-      a.state[(size_t)(sb + s) * st::kWords + st::kPitch + i] =
-          a.xs[(size_t)(sb + s) * a.L + (size_t)(nt * C - 1) * kFrame + i];
+    if (nt == 0) continue;
+    const float4 *x = reinterpret_cast<const float4 *>(a.xs + (size_t)(sb + s) * a.L + (size_t)(nt * C - 1) * kFrame);
+    float4 *h = reinterpret_cast<float4 *>(a.state + (size_t)(sb + s) * st::kWords + st::kPitch);
+#pragma unroll
+    for (int j = 0; j < (kPitchBuf / 4 + 63) / 64; j++) {
+      const int i = lane + 64 * j;
+      if (i < kPitchBuf / 4) h[i] = x[i];
+    }
   }
 }
 

@@ -98,16 +98,16 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
       float2 v[16];
       const float *pb = frame_pb(a, f);
       // the frame's new x_lp values n = 624..863 (pitch buffer samples
-      // 1247..1727, inside the window): operands load before the transform
-      float q[4][3];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int n = kXlpHist + 64 * k + lane;
-        if (n < kXlp) {
-          q[k][0] = pb[2 * n - 1];
-          q[k][1] = pb[2 * n];
-          q[k][2] = pb[2 * n + 1];
-        }
+      // 1247..1727, inside the window), 4 per lane (lanes 0..59): samples
+      // 1247 + 8 * lane .. 1255 + 8 * lane load before the transform
+      static_assert(kXlp - kXlpHist == 4 * 60 && kHist % 4 == 0, "x_lp lanes");
+      float xm = 0;
+      float4 qa = make_float4(0, 0, 0, 0), qb = qa;
+      if (lane < 60) {
+        const float *q = pb + kHist + 8 * lane;
+        xm = q[-1];
+        qa = *reinterpret_cast<const float4 *>(q);
+        qb = *reinterpret_cast<const float4 *>(q + 4);
       }
       wave_window(pb + (kPitchBuf - kWin), tb.hw, lane, v);
       wfft::run(v, tw, tb.tw, R, lane);
@@ -115,11 +115,14 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
 #pragma unroll
       for (int r = 0; r < 8; r++)
         if (64 * r + lane < kFreq) X[64 * r + lane] = v[r];
-      float *xl = frame_xlp(a, f);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int n = kXlpHist + 64 * k + lane;
-        if (n < kXlp) xl[n] = xlp_value(q[k][0], q[k][1], q[k][2]);
+      if (lane < 60) {
+        // x_lp[n] = f(x[2n-1], x[2n], x[2n+1]), n = 624 + 4 * lane + t
+        float4 o;
+        o.x = xlp_value(xm, qa.x, qa.y);
+        o.y = xlp_value(qa.y, qa.z, qa.w);
+        o.z = xlp_value(qa.w, qb.x, qb.y);
+        o.w = xlp_value(qb.y, qb.z, qb.w);
+        *reinterpret_cast<float4 *>(frame_xlp(a, f) + kXlpHist + 4 * lane) = o;
       }
 #pragma unroll
       for (int r = 0; r < 7; r++) {
