@@ -16,22 +16,32 @@ namespace fvad {
 
 // ---------------------------------------------------------------------------
 // k_pcorr: one 256-thread workgroup per half quarter tile (8 streams at one
-// frame position; 38.5 KB of LDS, so 4 workgroups share a CU, 4 waves per
-// SIMD at 97 VGPRs, which leaves room beside them for k_prep3).
+// frame position; 39.8 KB of LDS, so 4 workgroups share a CU).
 //   Q0 xf (rows 0..863) and the coarse Syy sequence -> LDS
 //   Q1 coarse xcorr: lane = (frame, 5 consecutive lags), a register window of
-//      5 y values slides one sample per step (2 LDS reads per 5 MACs)
-//   Q2 coarse find_best_pitch, lane per frame; the fine Syy values at the
-//      <= 10 candidate lags are fetched here, used in Q4.  Meanwhile wave 1
-//      walks remove_doubling's yy_lookup recurrence from xx, lane per frame,
-//      on xf in LDS, into the tile buffer (read in Q5)
+//      5 y values slides one sample per step (2 LDS reads per 5 MACs); then
+//      the coarse scan's survivors: a prefix top-2 of the lags' xcorr^2/Syy
+//      ratios over the frame's 32 lanes drops every lag that provably cannot
+//      change find_best_pitch's state, and the rest are listed in lag order
+//   Q2 coarse find_best_pitch over the survivors (exact, lane per frame; ~3 k
+//      instead of ~23 k cycles for all 147 lags); the fine Syy values at the
+//      <= 10 candidate lags are fetched here, used in Q4
 //   Q3 fine xcorr at the <= 10 lags within +-2 of 2*best (others are 0)
 //   Q4 fine find_best_pitch + pseudo-interpolation -> T0, candidate count
 //   Q5 remove_doubling products: lane = (frame, candidate c); candidate c's
 //      xcorr at T-1, T, T+1 share a sliding window of 3, plus xcorr(T1b);
 //      operands are read as aligned pairs (ds_read_b64: 64 banks, 2 steps
 //      per read), the lane's window parity resolved by selects
+//   Beside Q2..Q4, wave 2 (idle there) walks remove_doubling's yy_lookup
+//   recurrence (lane per frame, 384 serial steps) into the tile buffer for Q5.
 // ---------------------------------------------------------------------------
+#ifndef FVAD_WALK_Q2
+#define FVAD_WALK_Q2 12
+#endif
+#ifndef FVAD_WALK_Q3
+#define FVAD_WALK_Q3 72
+#endif
+constexpr int kWalkQ2 = FVAD_WALK_Q2, kWalkQ3 = FVAD_WALK_Q3;  // yy walk blocks done by the end of Q2 / Q3 (of 97)
 constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
 constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
 constexpr int kPcNT = kPcL * kPcF;
@@ -39,12 +49,25 @@ static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
 constexpr int kPcXS = 870;  // xf row pitch: even (8-byte aligned pairs in Q5), = 6 mod 8 (conflict-free Q0 stores)
 constexpr int kPcSP = 153;  // coarse xcorr / Syy row pitch (odd; >= 147 rounded up to the scan block)
 
+// __shfl_up within 32-lane halves from an explicit lane id (`self`, made
+// opaque per group by the caller, so the bpermute addresses are not hoisted
+// out of the persistent loop into registers held for the whole kernel)
+__device__ __forceinline__ int shfl_up32(int v, int d, int self) {
+  const int idx = (self & 31) >= d ? self - d : self;
+  return __builtin_amdgcn_ds_bpermute(idx << 2, v);
+}
+__device__ __forceinline__ float shfl_up32(float v, int d, int self) {
+  return __int_as_float(shfl_up32(__float_as_int(v), d, self));
+}
+
 __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
   constexpr int NT = kPcNT;
   constexpr int kHalves = ptile::kQuarter / kPcF;
   __shared__ __attribute__((aligned(16))) float xf[kPcF][kPcXS];
   __shared__ float scl[kPcF][kPcSP], xc[kPcF][kPcSP];
   __shared__ float sfl[kPcF][10], fine[kPcF][10];
+  __shared__ unsigned char lst[kPcF][kPcSP - 1];  // lags of the coarse scan's survivors (Q1 -> Q2)
+  __shared__ int ncand[kPcF];
   __shared__ int best[kPcF][2], T0s[kPcF], nvs[kPcF], fval[kPcF];
   __shared__ long long fidx[kPcF];
   const int tid = threadIdx.x;
@@ -53,6 +76,9 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
   const long long nquarters = (long long)n_sb * Vr * 4;
   const long long ngroups = (nquarters + 7) / 8 * 16;  // whole blocks of 16 units; units past the quarters skip
   STAMP_INIT();
+#ifdef FVAD_STAMPS
+  unsigned long long st_scan = 0, st_walk = 0;  // lane 0 of waves 0 / 1: the coarse scan / the yy walk alone
+#endif
   __shared__ long long gq;
   if (threadIdx.x == 0) gq = take_group(a, kWorkPcorr);
   __syncthreads();
@@ -73,7 +99,8 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
       g = gq;
       continue;
     }
-    const float *T = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter + h * kPcF;
+    float *Tq = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter;  // the quarter's block
+    const float *T = Tq + h * kPcF;
     if (tid < kPcF) {
       const long long t = gq4 >> 2;
       const int q = (int)(gq4 & 3);
@@ -105,17 +132,17 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     // Q1: xcorr[k] = sum_j x_lp4[j] y_lp4[j+k], x_lp4[j] = xf[384+2j], y_lp4[m] = xf[2m]
     {
       constexpr int R = 5;
-      static_assert(R * (kPcL - 1) >= 147 && 240 % R == 0, "Q1 lag blocks");
-      const int fr = tid / kPcL, k0 = R * (tid % kPcL);
+      static_assert(R * (kPcL - 1) >= 147 && 240 % R == 0 && kPcL == 32, "Q1 lag blocks");
+      const int fr = tid / kPcL, l = tid % kPcL, k0 = R * l;
+      float acc[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) acc[r] = 0.0f;
       if (k0 < 147) {
         const float *X = xf[fr] + (kPitchMax >> 1);
         const float *Y = xf[fr] + 2 * k0;
-        float acc[R], win[R];
+        float win[R];
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-          acc[r] = 0.0f;
-          win[r] = Y[2 * r];
-        }
+        for (int r = 0; r < R; r++) win[r] = Y[2 * r];
         for (int jb = 0; jb < 240; jb += R) {
 #pragma unroll
           for (int u = 0; u < R; u++) {
@@ -129,43 +156,155 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         for (int r = 0; r < R; r++)
           if (k0 + r < 147) xc[fr][k0 + r] = acc[r];
       } else if (k0 < kPcSP) {
-        // lags 147.. pad the scan blocks: xcorr <= 0 never updates the best pair
+        // lags 147.. pad the scan's last block: xcorr <= 0 never updates the best pair
         for (int k = 147; k < kPcSP; k++) xc[fr][k] = -1.0f;
+      }
+      // Survivors of the coarse find_best_pitch.  A lag j changes the scan's
+      // state only if num_j * bd1 > bn1 * Syy_j against the second-best pair
+      // at j, whose ratio bn1 / bd1 is (up to float rounding) at least the
+      // second largest ratio num / Syy among the positive lags before j.  A
+      // lag whose ratio is below that by more than 0.1 % fails its test for
+      // certain and is dropped; the exact scan (Q2) then visits only the
+      // survivors, in order, and ends in the same state.  Ratios here are only
+      // a filter (rounded reciprocal); lags with xcorr <= 0 never update.
+      constexpr float kNoRatio = -__builtin_inff();
+      float rho[R];
+      float m1 = kNoRatio, m2 = kNoRatio;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        float v = kNoRatio;
+        if (k0 + r < 147 && acc[r] > 0) {
+          float x16 = acc[r];
+          x16 *= 1e-12f;
+          v = (x16 * x16) * __builtin_amdgcn_rcpf(scl[fr][k0 + r]);
+        }
+        rho[r] = v;
+        m2 = fmaxf(m2, fminf(m1, v));
+        m1 = fmaxf(m1, v);
+      }
+      int self = tid & 63;
+      asm volatile("" : "+v"(self));
+      // inclusive prefix top-2 over the frame's 32 lanes, then exclusive
+#pragma unroll
+      for (int d = 1; d < kPcL; d <<= 1) {
+        const float p1 = shfl_up32(m1, d, self), p2 = shfl_up32(m2, d, self);
+        if (l >= d) {
+          const float n2 = fmaxf(fminf(m1, p1), fmaxf(m2, p2));
+          m1 = fmaxf(m1, p1);
+          m2 = n2;
+        }
+      }
+      float e1 = shfl_up32(m1, 1, self), e2 = shfl_up32(m2, 1, self);
+      if (l == 0) e1 = e2 = kNoRatio;
+      unsigned mask = 0;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (rho[r] != kNoRatio && !(e2 > rho[r] * 1.001f)) mask |= 1u << r;
+        e2 = fmaxf(e2, fminf(e1, rho[r]));
+        e1 = fmaxf(e1, rho[r]);
+      }
+      // the survivors' lags in order
+      const int c = __builtin_popcount(mask);
+      int pos = c;
+#pragma unroll
+      for (int d = 1; d < kPcL; d <<= 1) {
+        const int t = shfl_up32(pos, d, self);
+        if (l >= d) pos += t;
+      }
+      int o = pos - c;
+#pragma unroll
+      for (int r = 0; r < R; r++)
+        if (mask & (1u << r)) lst[fr][o++] = (unsigned char)(k0 + r);
+      if (l == kPcL - 1) {
+        ncand[fr] = pos;
+        // pad entries: the scan runs whole blocks of 4 (lag 147: xcorr -1, no update)
+#pragma unroll
+        for (int u = 0; u < 4; u++) lst[fr][pos + u] = 147;
       }
     }
     __syncthreads();
     RSTAMP(1);
+    // remove_doubling's yy_lookup recurrence, lane per frame on wave 2 (idle
+    // from Q2 to Q4), in three pieces beside Q2, Q3 and Q4:
+    // yy_lookup[i] = max(0, yy), yy = (yy + x[-i]^2) - x[480-i]^2 from yy =
+    // xx, x = xf + 384, into the frame's yy row of the tile buffer as float4
+    // stores (block q = i 4q .. 4q+3), read by Q5
+    const bool walker = tid >= 128 && tid < 128 + kPcF && fval[tid - 128];
+    float wyy = 0;
+    float4 *wY = nullptr;
+    const float *wxr = nullptr;
+    if (walker) {
+      const int fr = tid - 128;
+      wY = reinterpret_cast<float4 *>(Tq + ptile::kYy * ptile::kQuarter + (h * kPcF + fr) * ptile::kYyPitch);
+      wxr = xf[fr];
+      wyy = Tq[ptile::kXx * ptile::kQuarter + h * kPcF + fr];
+    }
+    auto walk = [&](int q0, int q1) {
+#ifdef FVAD_STAMPS
+      const unsigned long long w0_ = __builtin_amdgcn_s_memtime();
+#endif
+      auto step = [&](int i) -> float {
+        const float va = wxr[384 - i], vb = wxr[864 - i];
+        wyy = wyy + va * va - vb * vb;
+        return (0 > wyy) ? 0 : wyy;
+      };
+      int q = q0;
+      if (q == 0) {
+        float4 o;
+        o.x = wyy;
+        o.y = step(1);
+        o.z = step(2);
+        o.w = step(3);
+        wY[0] = o;
+        q = 1;
+      }
+      const int qe = q1 < 96 ? q1 : 96;
+#pragma unroll 4
+      for (; q < qe; q++) {
+        float4 o;
+        o.x = step(4 * q);
+        o.y = step(4 * q + 1);
+        o.z = step(4 * q + 2);
+        o.w = step(4 * q + 3);
+        wY[q] = o;
+      }
+      if (q1 == 97) wY[96] = make_float4(step(384), 0.0f, 0.0f, 0.0f);
+#ifdef FVAD_STAMPS
+      if (tid == 128) st_walk += __builtin_amdgcn_s_memtime() - w0_;
+#endif
+    };
+    static_assert(4 * 97 == ptile::kYyPitch, "yy row");
     // Q2
     float sfv[10];
     if (tid < kPcF) {
       const int fr = tid;
+#ifdef FVAD_STAMPS
+      const unsigned long long s0_ = __builtin_amdgcn_s_memtime();
+#endif
       int bst[2] = {0, 1};
       float bn0 = -1, bn1 = -1, bd0 = 0, bd1 = 0;
       // operands of the next 4 lags load while these 4 are visited (8 ahead:
       // 112 VGPRs, and 4 x 112 + k_prep3's 96 no longer fit one SIMD's 512,
       // so the CUs that host k_prep3 lose a workgroup: 1.45 vs 1.39 ms)
       constexpr int B = 4;
-      float xb[B], yb[B];
+      int jb[B];
 #pragma unroll
-      for (int u = 0; u < B; u++) {
-        xb[u] = xc[fr][u];
-        yb[u] = scl[fr][u];
-      }
-      for (int i0 = 0; i0 < 147; i0 += B) {
-        float xn[B], yn[B];
+      for (int u = 0; u < B; u++) jb[u] = lst[fr][u];
+      const int n = ncand[fr];
+      for (int i0 = 0; i0 < n; i0 += B) {
+        int jn[B];
 #pragma unroll
-        for (int u = 0; u < B; u++) {
-          const int i = min(i0 + B + u, kPcSP - 1);
-          xn[u] = xc[fr][i];
-          yn[u] = scl[fr][i];
-        }
-#pragma unroll
-        for (int u = 0; u < B; u++) best_pitch_visit(xb[u], yb[u], i0 + u, bn0, bn1, bd0, bd1, bst);
+        for (int u = 0; u < B; u++) jn[u] = lst[fr][min(i0 + B + u, kPcSP - 2)];
+        float xb[B], yb[B];
 #pragma unroll
         for (int u = 0; u < B; u++) {
-          xb[u] = xn[u];
-          yb[u] = yn[u];
+          xb[u] = xc[fr][jb[u]];
+          yb[u] = scl[fr][jb[u]];
         }
+#pragma unroll
+        for (int u = 0; u < B; u++) best_pitch_visit(xb[u], yb[u], jb[u], bn0, bn1, bd0, bd1, bst);
+#pragma unroll
+        for (int u = 0; u < B; u++) jb[u] = jn[u];
       }
       best[fr][0] = bst[0];
       best[fr][1] = bst[1];
@@ -174,26 +313,16 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         const int i = 2 * bst[u / 5] - 2 + (u % 5);
         sfv[u] = (i >= 0 && i < 294) ? T[(ptile::kSf + i) * ptile::kQuarter + fr] : 0.0f;
       }
-    } else if (tid >= 64 && tid < 64 + kPcF && fval[tid - 64]) {
-      // meanwhile wave 1 (idle in the scan) walks remove_doubling's yy_lookup
-      // recurrence: yy_lookup[i] = max(0, yy), yy = (yy + x[-i]^2) - x[480-i]^2
-      // from yy = xx, x = xf + 384; into the tile buffer's yy rows, read by Q5
-      // after the barriers of Q2..Q4
-      const int fr = tid - 64;
-      float *Y = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter + h * kPcF + fr;
-      const float *xr = xf[fr];
-      float yy = Y[ptile::kXx * ptile::kQuarter];
-      Y[ptile::kYy * ptile::kQuarter] = yy;
-#pragma unroll 8
-      for (int i = 1; i <= 384; i++) {
-        const float va = xr[384 - i], vb = xr[864 - i];
-        yy = yy + va * va - vb * vb;
-        Y[(ptile::kYy + i) * ptile::kQuarter] = (0 > yy) ? 0 : yy;
-      }
+#ifdef FVAD_STAMPS
+      if (fr == 0) st_scan += __builtin_amdgcn_s_memtime() - s0_;
+#endif
+    } else if (walker) {
+      walk(0, kWalkQ2);
     }
     __syncthreads();
     RSTAMP(2);
     // Q3
+    if (walker) walk(kWalkQ2, kWalkQ3);
     if (tid < 10 * kPcF) {
       const int fr = tid / 10, u = tid - 10 * fr;
       const int bp0 = best[fr][0], bp1 = best[fr][1];
@@ -208,6 +337,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     __syncthreads();
     RSTAMP(3);
     // Q4
+    if (walker) walk(kWalkQ3, 97);
     if (tid < kPcF) {
       const int fr = tid;
 #pragma unroll
@@ -267,8 +397,9 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         const int Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
         const int Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
         // yy_lookup and xx gathers, consumed after the products
-        const float yyA = T[(ptile::kYy + Tc) * ptile::kQuarter + fr];
-        const float yyB = T[(ptile::kYy + Tb) * ptile::kQuarter + fr];
+        const float *yrow = Tq + ptile::kYy * ptile::kQuarter + (h * kPcF + fr) * ptile::kYyPitch;
+        const float yyA = yrow[Tc];
+        const float yyB = yrow[Tb];
         const float xx = T[ptile::kXx * ptile::kQuarter + fr];
         const float *X = xf[fr] + (kPitchMax >> 1);
         float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
@@ -338,6 +469,10 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     g = gq;
   }
   STAMP_FLUSH(32, 6);
+#ifdef FVAD_STAMPS
+  if (a.stamps && tid == 0) atomicAdd(&a.stamps[38], st_scan);
+  if (a.stamps && tid == 128) atomicAdd(&a.stamps[39], st_walk);
+#endif
 }
 
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream) {

@@ -15,14 +15,15 @@ constexpr int kPitchRecord = 80;  // floats per frame of the pitch record (k_pco
 
 // Pitch tile buffer (k_plpc -> k_pcorr): a tile is 64 streams at one frame
 // position; each quarter (16 streams) is one contiguous block of kRows rows of
-// 16 floats.
+// 16 floats (the yy_lookup region is laid out frame-major instead).
 namespace ptile {
 constexpr int kTile = 64, kQuarter = 16;
 constexpr int kXf = 0;              // xf[0..863]: x_lp after celt_fir5
 constexpr int kSc = 864;            // Syy before step i of the coarse find_best_pitch, i < 147
 constexpr int kSf = kSc + 147;      // Syy of the fine find_best_pitch, i < 294
-constexpr int kYy = kSf + 294;      // yy_lookup[0..384] (remove_doubling)
-constexpr int kXx = kYy + 385;      // xx
+constexpr int kYy = kSf + 294;      // yy_lookup[0..384] (remove_doubling), k_pcorr's own region:
+constexpr int kYyPitch = 388;       //   [16 frames][kYyPitch] (float4-aligned frame rows), kYyPitch rows of 16
+constexpr int kXx = kYy + kYyPitch;  // xx
 constexpr int kRows = kXx + 1;
 }  // namespace ptile
 

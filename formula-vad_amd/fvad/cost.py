@@ -17,7 +17,7 @@ FRAME = 480
 # channel-frame averages; tests/test_host_cpu.py recounts them
 MEASURED = {"fine_lags_per_frame": 9.4088, "rd_cands_per_frame": 7.1532, "silent_frac": 0.0,
             "frames_counted": 102400}
-PTILE_ROWS = 864 + 147 + 294 + 385 + 1  # k_plpc -> k_pcorr rows per frame (fvad_staged.h ptile)
+PTILE_ROWS = 864 + 147 + 294 + 388 + 1  # k_plpc -> k_pcorr rows per frame (fvad_staged.h ptile)
 
 
 def _fft960():
@@ -149,7 +149,7 @@ def staged_kernels(n_channels=2, fft_size=2048):
         # in; xf, the Syy sequences and xx out.
         # k_pcorr: those in, yy_lookup (read back at <= 29 periods) and the
         # pitch record out
-        "k_plpc": (plpc, (864 + 2) * 4 + (PTILE_ROWS - 385) * 4),
+        "k_plpc": (plpc, (864 + 2) * 4 + (PTILE_ROWS - 388) * 4),
         "k_pcorr": (pitch - xlp - plpc - rd * 4, (864 + 147 + 10 + 1 + 385 + 29) * 4 + 80 * 4),
         "k_select": (rd * 4 + rd * 12, 80 * 4 + 4),
         "k_pspecw": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),

@@ -51,6 +51,44 @@ def test_engine_bit_exact_ragged(fvad_mod, oracle_mod, models, mode):
         assert_stream_equal(r, g, 2)
 
 
+def periodic_streams(n):
+    """Strictly periodic inputs: their pitch cross-correlations repeat at every
+    multiple of the period, so the coarse and fine find_best_pitch scans see
+    runs of (near-)equal xcorr^2 / Syy ratios -- the case the staged path's
+    survivor filter (k_pcorr Q1) must get exactly right."""
+    t = np.arange(n) / 48000.0
+    sigs = [
+        0.3 * np.sin(2 * np.pi * 200.0 * t),                      # period 240 samples
+        0.25 * np.sign(np.sin(2 * np.pi * 150.0 * t)),            # square wave, period 320
+        0.2 * ((np.arange(n) % 480) == 0).astype(np.float64),     # impulse train, period 480
+        0.2 * (2 * ((np.arange(n) % 96) / 96.0) - 1),             # sawtooth, period 96 (x_lp: 48)
+        0.1 * np.sin(2 * np.pi * 250.0 * t) + 0.1 * np.sin(2 * np.pi * 500.0 * t),
+        np.full(n, 0.05),                                         # DC
+    ]
+    out = []
+    for i in range(0, len(sigs), 2):
+        out.append(np.stack([sigs[i], sigs[i + 1]]).astype(np.float32))
+    return out
+
+
+@pytest.mark.parametrize("mode", ["staged", "fp16"])
+def test_engine_periodic_inputs(fvad_mod, oracle_mod, models, mode):
+    """Tones, a square wave, an impulse train, a sawtooth and DC (3 s stereo):
+    staged bit-identical with the oracle; in fp16 mode the pitch path (which
+    is bit-exact there too) shows through identical ratio / window ratios."""
+    m, om = models
+    streams = periodic_streams(48000 * 3)
+    ref = pu.oracle_run(oracle_mod, om, streams)
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=50, want_denoised=True, mode=mode)
+    got = pu.engine_run(fvad_mod, eng, streams, 50)
+    for r, g in zip(ref, got):
+        if mode == "staged":
+            assert_stream_equal(r, g, 2)
+        else:
+            assert np.array_equal(r["frames"]["ratio"], g["ratio"])
+            assert np.array_equal(r["windows"]["ratio"], g["win_ratio"])
+
+
 @pytest.mark.parametrize("mode", ["staged", "fused"])
 @pytest.mark.parametrize("n_channels,fft_size", [(1, 2048), (2, 512), (3, 2048)])
 def test_engine_channels_and_fft_size(fvad_mod, oracle_mod, models, n_channels, fft_size, mode):

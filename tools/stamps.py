@@ -79,13 +79,14 @@ if MODE == "staged":
         print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[16 + i] / max(1, ft), buf[16 + i] / groups))
 
 if MODE == "staged":
-    PIT = ["Q0 xf + coarse Syy -> LDS", "Q1 coarse xcorr", "Q2 coarse scan (+ yy walk on w1)", "Q3 fine xcorr",
+    PIT = ["Q0 xf + coarse Syy -> LDS", "Q1 coarse xcorr", "Q2 coarse scan (survivors)", "Q3 fine xcorr",
            "Q4 fine scan", "Q5 remove_doubling products"]
     groups = B * 2 * T / 8.0
     pt = sum(buf[32:38])
     print("k_pcorr: stamped cycles per 8-frame group per WG: %.0f" % (pt / max(1, groups)))
     for i, n in enumerate(PIT):
         print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[32 + i] / max(1, pt), buf[32 + i] / groups))
+    print("   alone: coarse scan %8.0f, yy walk (wave 2, Q2..Q4) %8.0f cyc/group" % (buf[38] / groups, buf[39] / groups))
 
 if MODE == "staged":
     SYN = ["setup + X load + pitch gain r", "pitch filter + band terms", "band chains, norm, gains",
