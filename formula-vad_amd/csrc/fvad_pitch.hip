@@ -84,6 +84,11 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
   __syncthreads();
   long long g = gq;
   while (g < ngroups) {
+    // per-group opaque copy of tid: keeps the compiler from hoisting the
+    // phases' per-thread offsets out of the persistent loop into registers
+    // held for the whole kernel (124 -> 86 VGPRs)
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
     // group g -> (quarter tile, frame columns h*kPcF ..): T is the group's
     // first column, rows keep the quarter's 16-column pitch.  The halves of a
     // quarter are units x + 16 b and x + 16 b + 8, both from queue x (one
@@ -94,38 +99,45 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     const int h = (int)((g >> 3) & 1);
     if (gq4 >= nquarters) {  // padding unit of the last block (uniform branch)
       __syncthreads();
-      if (tid == 0) gq = take_group(a, kWorkPcorr);
+      if (tq == 0) gq = take_group(a, kWorkPcorr);
       __syncthreads();
       g = gq;
       continue;
     }
     float *Tq = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter;  // the quarter's block
     const float *T = Tq + h * kPcF;
-    if (tid < kPcF) {
+    if (tq < kPcF) {
       const long long t = gq4 >> 2;
       const int q = (int)(gq4 & 3);
       const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
-      const int s = sb * 64 + q * 16 + h * kPcF + tid;
-      fval[tid] = s < a.n_streams && v < ticks_of(a, s) * a.n_channels;
-      fidx[tid] = (long long)s * a.V + v;
+      const int s = sb * 64 + q * 16 + h * kPcF + tq;
+      fval[tq] = s < a.n_streams && v < ticks_of(a, s) * a.n_channels;
+      fidx[tq] = (long long)s * a.V + v;
     }
-    // Q0
+    // Q0: each thread's float4 loads go out in batches of kQ0B before their LDS
+    // stores (a few memory latencies per group instead of one per loop trip)
     constexpr int P4 = kPcF / 4;  // float4s per row and group
-    for (int idx = tid; idx < kXlp * P4; idx += NT) {
-      const int r = idx / P4, p = idx % P4;
-      const float4 w4 = *reinterpret_cast<const float4 *>(T + r * ptile::kQuarter + 4 * p);
-      xf[4 * p][r] = w4.x;
-      xf[4 * p + 1][r] = w4.y;
-      xf[4 * p + 2][r] = w4.z;
-      xf[4 * p + 3][r] = w4.w;
-    }
-    for (int idx = tid; idx < 147 * P4; idx += NT) {
-      const int r = idx / P4, p = idx % P4;
-      const float4 w4 = *reinterpret_cast<const float4 *>(T + (ptile::kSc + r) * ptile::kQuarter + 4 * p);
-      scl[4 * p][r] = w4.x;
-      scl[4 * p + 1][r] = w4.y;
-      scl[4 * p + 2][r] = w4.z;
-      scl[4 * p + 3][r] = w4.w;
+    constexpr int kQ0N = (kXlp + 147) * P4, kQ0B = 4;
+    for (int u0 = 0; u0 < kQ0N; u0 += NT * kQ0B) {
+      float4 w4[kQ0B];
+#pragma unroll
+      for (int u = 0; u < kQ0B; u++) {
+        const int idx = u0 + tq + NT * u, r = idx / P4, p = idx % P4;
+        const int row = r < kXlp ? r : ptile::kSc + (r - kXlp);
+        if (idx < kQ0N) w4[u] = *reinterpret_cast<const float4 *>(T + row * ptile::kQuarter + 4 * p);
+      }
+#pragma unroll
+      for (int u = 0; u < kQ0B; u++) {
+        const int idx = u0 + tq + NT * u, r = idx / P4, p = idx % P4;
+        if (idx < kQ0N) {
+          float *d = r < kXlp ? &xf[4 * p][r] : &scl[4 * p][r - kXlp];
+          const int pitch = r < kXlp ? kPcXS : kPcSP;
+          d[0] = w4[u].x;
+          d[pitch] = w4[u].y;
+          d[2 * pitch] = w4[u].z;
+          d[3 * pitch] = w4[u].w;
+        }
+      }
     }
     __syncthreads();
     RSTAMP(0);
@@ -133,7 +145,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     {
       constexpr int R = 5;
       static_assert(R * (kPcL - 1) >= 147 && 240 % R == 0 && kPcL == 32, "Q1 lag blocks");
-      const int fr = tid / kPcL, l = tid % kPcL, k0 = R * l;
+      const int fr = tq / kPcL, l = tq % kPcL, k0 = R * l;
       float acc[R];
 #pragma unroll
       for (int r = 0; r < R; r++) acc[r] = 0.0f;
@@ -182,7 +194,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         m2 = fmaxf(m2, fminf(m1, v));
         m1 = fmaxf(m1, v);
       }
-      int self = tid & 63;
+      int self = tq & 63;
       asm volatile("" : "+v"(self));
       // inclusive prefix top-2 over the frame's 32 lanes, then exclusive
 #pragma unroll
@@ -229,12 +241,12 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     // yy_lookup[i] = max(0, yy), yy = (yy + x[-i]^2) - x[480-i]^2 from yy =
     // xx, x = xf + 384, into the frame's yy row of the tile buffer as float4
     // stores (block q = i 4q .. 4q+3), read by Q5
-    const bool walker = tid >= 128 && tid < 128 + kPcF && fval[tid - 128];
+    const bool walker = tq >= 128 && tq < 128 + kPcF && fval[tq - 128];
     float wyy = 0;
     float4 *wY = nullptr;
     const float *wxr = nullptr;
     if (walker) {
-      const int fr = tid - 128;
+      const int fr = tq - 128;
       wY = reinterpret_cast<float4 *>(Tq + ptile::kYy * ptile::kQuarter + (h * kPcF + fr) * ptile::kYyPitch);
       wxr = xf[fr];
       wyy = Tq[ptile::kXx * ptile::kQuarter + h * kPcF + fr];
@@ -270,14 +282,14 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
       }
       if (q1 == 97) wY[96] = make_float4(step(384), 0.0f, 0.0f, 0.0f);
 #ifdef FVAD_STAMPS
-      if (tid == 128) st_walk += __builtin_amdgcn_s_memtime() - w0_;
+      if (tq == 128) st_walk += __builtin_amdgcn_s_memtime() - w0_;
 #endif
     };
     static_assert(4 * 97 == ptile::kYyPitch, "yy row");
     // Q2
     float sfv[10];
-    if (tid < kPcF) {
-      const int fr = tid;
+    if (tq < kPcF) {
+      const int fr = tq;
 #ifdef FVAD_STAMPS
       const unsigned long long s0_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -323,8 +335,8 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(2);
     // Q3
     if (walker) walk(kWalkQ2, kWalkQ3);
-    if (tid < 10 * kPcF) {
-      const int fr = tid / 10, u = tid - 10 * fr;
+    if (tq < 10 * kPcF) {
+      const int fr = tq / 10, u = tq - 10 * fr;
       const int bp0 = best[fr][0], bp1 = best[fr][1];
       const int i = (u < 5 ? 2 * bp0 : 2 * bp1) - 2 + (u % 5);
       const bool dup = u >= 5 && abs(i - 2 * bp0) <= 2;
@@ -338,8 +350,8 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(3);
     // Q4
     if (walker) walk(kWalkQ3, 97);
-    if (tid < kPcF) {
-      const int fr = tid;
+    if (tq < kPcF) {
+      const int fr = tq;
 #pragma unroll
       for (int u = 0; u < 10; u++) sfl[fr][u] = sfv[u];
       const int bp0 = best[fr][0], bp1 = best[fr][1];
@@ -390,8 +402,8 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     __syncthreads();
     RSTAMP(4);
     // Q5
-    if (tid < 15 * kPcF) {
-      const int fr = tid / 15, c = tid - 15 * fr;
+    if (tq < 15 * kPcF) {
+      const int fr = tq / 15, c = tq - 15 * fr;
       if (fval[fr] && (c == 0 || c - 1 < nvs[fr])) {
         const int T0 = T0s[fr];
         const int Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
@@ -463,7 +475,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         }
       }
     }
-    if (tid == 0) gq = take_group(a, kWorkPcorr);
+    if (tq == 0) gq = take_group(a, kWorkPcorr);
     __syncthreads();
     RSTAMP(5);
     g = gq;
