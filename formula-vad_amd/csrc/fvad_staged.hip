@@ -1275,47 +1275,82 @@ __global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
       int fd = istp[st::kFramesDone];
       float vol = stp[st::kVolAcc];
       const int FB = a.plan->nfft_b;
-      for (int t = 0; t < nt; t++) {
-        const size_t o = (size_t)t * a.n_streams + s;
-        const float ratio = a.ratio[o];
-        const long long a0 = (long long)fd * kFrame;
-        const long long wdone = a0 / FB;
-        const long long next_end = (wdone + 1) * FB;
-        const bool complete = a0 + kFrame >= next_end;
-        if (complete) {
-          const int r = (int)(next_end - a0);
-          vol += ratio * ((float)r / (float)FB);
-          a.out_win_ratio[o] = vol;
-          a.out_win_vad[o] = a.out_vad[o];
-          vol = 0;
-          if (kFrame - r > 0) vol += ratio * ((float)(kFrame - r) / (float)FB);
-          wt[j] = t;
-          wsx[j] = wdone * FB;
-          j++;
-        } else {
-          vol += ratio * ((float)kFrame / (float)FB);
-          a.out_win_ratio[o] = 0.0f;
-          a.out_win_vad[o] = 0.0f;
-          // no window completes in this tick: band sums are defined as 0
-          for (int i = 0; i < a.n_channels * a.n_bands; i++) a.out_band[o * a.n_channels * a.n_bands + i] = 0.0f;
+      // the per-tick inputs (ratio, vad) of 8 ticks load before any of their
+      // outputs is stored (stores between the loads would serialise them)
+      constexpr int kWmT = 8;
+      for (int t0 = 0; t0 < nt; t0 += kWmT) {
+        float rr[kWmT], vv[kWmT];
+#pragma unroll
+        for (int u = 0; u < kWmT; u++) {
+          const size_t o = (size_t)(t0 + u) * a.n_streams + s;
+          rr[u] = t0 + u < nt ? a.ratio[o] : 0.0f;
+          vv[u] = t0 + u < nt ? a.out_vad[o] : 0.0f;
         }
-        a.out_win_flag[o] = complete ? 1 : 0;
-        fd++;
+#pragma unroll
+        for (int u = 0; u < kWmT; u++) {
+          const int t = t0 + u;
+          if (t < nt) {
+          const size_t o = (size_t)t * a.n_streams + s;
+          const float ratio = rr[u];
+          const long long a0 = (long long)fd * kFrame;
+          const long long wdone = a0 / FB;
+          const long long next_end = (wdone + 1) * FB;
+          const bool complete = a0 + kFrame >= next_end;
+          if (complete) {
+            const int r = (int)(next_end - a0);
+            vol += ratio * ((float)r / (float)FB);
+            a.out_win_ratio[o] = vol;
+            a.out_win_vad[o] = vv[u];
+            vol = 0;
+            if (kFrame - r > 0) vol += ratio * ((float)(kFrame - r) / (float)FB);
+            wt[j] = t;
+            wsx[j] = wdone * FB;
+            j++;
+          } else {
+            vol += ratio * ((float)kFrame / (float)FB);
+            a.out_win_ratio[o] = 0.0f;
+            a.out_win_vad[o] = 0.0f;
+            // no window completes in this tick: band sums are defined as 0
+            for (int i = 0; i < a.n_channels * a.n_bands; i++) a.out_band[o * a.n_channels * a.n_bands + i] = 0.0f;
+          }
+          a.out_win_flag[o] = complete ? 1 : 0;
+          fd++;
+          }
+        }
       }
       istp[st::kFramesDone] = fd;
       stp[st::kVolAcc] = vol;
     }
     for (; j < a.wmax; j++) wt[j] = -1;
   }
-  // synthesis_mem for the next launch = second half of the last frame's window
-  for (int idx = tid; idx < kWmS * (kFrame / 4); idx += 64) {
-    const int sl = idx / (kFrame / 4), q = idx - sl * (kFrame / 4), s = sb + sl;
-    if (s >= a.n_streams) break;
-    const int nt = ticks_of(a, s);
-    if (nt <= 0) continue;
-    const float *yl = a.ys + ((size_t)s * a.V + (size_t)nt * a.n_channels - 1) * kWin + kFrame;
-    *reinterpret_cast<float4 *>(a.state + (size_t)s * st::kWords + st::kSyn + 4 * q) =
-        reinterpret_cast<const float4 *>(yl)[q];
+  // synthesis_mem for the next launch = second half of the last frame's
+  // window; each lane's float4 loads go out before its stores (a store
+  // between them would make every load wait for the one before)
+  // (4 streams per pass: lane = float4 q and q + 64 of each stream's 120)
+  constexpr int kSynQ = kFrame / 4, kSynS = 4;
+  static_assert(kSynQ <= 128 && kWmS % kSynS == 0, "synthesis copy");
+  for (int s0 = 0; s0 < kWmS; s0 += kSynS) {
+    float4 v[kSynS][2];
+    bool ok[kSynS][2];
+#pragma unroll
+    for (int k = 0; k < kSynS; k++) {
+      const int s = sb + s0 + k;
+      const int nt = s < a.n_streams ? ticks_of(a, s) : 0;
+      const float4 *yl = reinterpret_cast<const float4 *>(
+          a.ys + ((size_t)s * a.V + (size_t)max(nt, 1) * a.n_channels - 1) * kWin + kFrame);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int q = tid + 64 * h;
+        ok[k][h] = nt > 0 && q < kSynQ;
+        v[k][h] = ok[k][h] ? yl[q] : make_float4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kSynS; k++)
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+        if (ok[k][h])
+          reinterpret_cast<float4 *>(a.state + (size_t)(sb + s0 + k) * st::kWords + st::kSyn)[tid + 64 * h] = v[k][h];
   }
 }
 
