@@ -625,9 +625,13 @@ __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
 // k tests candidate k (T1 of k + 2), a ballot finds the last passing one (the
 // reference loop keeps overwriting, so the highest k wins) and its values are
 // read from its lane.  Every comparison and value is the reference's.  A
-// frame's record loads four frames ahead through a 4-slot register ring.
+// frame's record loads kSelRing - 1 frames ahead through a register ring.
 // ---------------------------------------------------------------------------
 constexpr int kSelStreams = 4;  // streams per 64-thread workgroup
+#ifndef FVAD_SEL_RING
+#define FVAD_SEL_RING 8
+#endif
+constexpr int kSelRing = FVAD_SEL_RING;  // frames of records in flight
 struct SelRec {
   int T0, nv, Tk, offk, off0;
   float g0, xy0, yy0, gk, xyk, yyk;
@@ -712,22 +716,24 @@ __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
     last_period = pi;
     last_gain = pg;
   };
-  SelRec r0{}, r1{}, r2{}, r3{};
-  sel_load(r0, rows, k, 0 < nf);
-  sel_load(r1, rows + rec::kSize, k, 1 < nf);
-  sel_load(r2, rows + 2 * rec::kSize, k, 2 < nf);
-  for (int v = 0; v < nfw; v += 4) {
-    sel_load(r3, rows + (size_t)(v + 3) * rec::kSize, k, v + 3 < nf);
-    step(r0, v);
-    if (v + 1 >= nfw) break;
-    sel_load(r0, rows + (size_t)(v + 4) * rec::kSize, k, v + 4 < nf);
-    step(r1, v + 1);
-    if (v + 2 >= nfw) break;
-    sel_load(r1, rows + (size_t)(v + 5) * rec::kSize, k, v + 5 < nf);
-    step(r2, v + 2);
-    if (v + 3 >= nfw) break;
-    sel_load(r2, rows + (size_t)(v + 6) * rec::kSize, k, v + 6 < nf);
-    step(r3, v + 3);
+  // records kSelRing frames ahead through a register ring (static slots: the
+  // loop over a ring turn is unrolled)
+  SelRec r[kSelRing];
+#pragma unroll
+  for (int u = 0; u < kSelRing - 1; u++) {
+    r[u] = SelRec{};
+    sel_load(r[u], rows + (size_t)u * rec::kSize, k, u < nf);
+  }
+  r[kSelRing - 1] = SelRec{};
+  for (int v = 0; v < nfw; v += kSelRing) {
+#pragma unroll
+    for (int u = 0; u < kSelRing; u++) {
+      if (v + u >= nfw) break;
+      // slot (u - 1) mod R was consumed last step: frame v + u + R - 1 goes there
+      const int ls = (u + kSelRing - 1) % kSelRing;
+      sel_load(r[ls], rows + (size_t)(v + u + kSelRing - 1) * rec::kSize, k, v + u + kSelRing - 1 < nf);
+      step(r[u], v + u);
+    }
   }
   if (sok && nf > 0 && k == 0) {
     istp[st::kLastPeriod] = last_period;
