@@ -431,13 +431,21 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         float w2 = ow ? q1.y : q1.x, w3 = ow ? qp.x : q1.y;
         v2f r0 = Bq[0], rp = Bq[1];
         float b0 = ob ? r0.y : r0.x, b1 = ob ? rp.x : r0.y;
+        const char *xb0 = reinterpret_cast<const char *>(&xf[0][0]);
+        int oX = (int)(reinterpret_cast<const char *>(Xp) - xb0), oW = (int)(reinterpret_cast<const char *>(W) - xb0),
+            oB = (int)(reinterpret_cast<const char *>(Bq) - xb0);
 #pragma unroll 4
         for (int i = 0; i < 240; i++) {  // j = 2i, 2i + 1
-          // an offset the compiler cannot see through keeps every pair load a
-          // single ds_read_b64 (64 banks) instead of merged ds_read2_b64s
-          int o = i;
-          asm volatile("" : "+v"(o));
-          const v2f xp = Xp[o], qn = W[o + 3], rn = Bq[o + 2];
+          // byte offsets the compiler cannot see through, bumped per step:
+          // every pair load stays a single ds_read_b64 (64 banks) instead of
+          // merged ds_read2_b64s, at one add per stream and step
+          const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
+          const v2f qn = *reinterpret_cast<const v2f *>(xb0 + oW + 24);
+          const v2f rn = *reinterpret_cast<const v2f *>(xb0 + oB + 16);
+          oX += 8;
+          oW += 8;
+          oB += 8;
+          asm volatile("" : "+v"(oX), "+v"(oW), "+v"(oB));
           aM = aM + xp.x * w0;
           a0 = a0 + xp.x * w1;
           aP = aP + xp.x * w2;
