@@ -41,6 +41,12 @@ namespace fvad {
 #ifndef FVAD_WALK_Q3
 #define FVAD_WALK_Q3 72
 #endif
+#ifndef FVAD_Q3_WIN
+#define FVAD_Q3_WIN 0
+#endif
+#ifndef FVAD_Q5_SPLIT
+#define FVAD_Q5_SPLIT 1
+#endif
 constexpr int kWalkQ2 = FVAD_WALK_Q2, kWalkQ3 = FVAD_WALK_Q3;  // yy walk blocks done by the end of Q2 / Q3 (of 97)
 constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
 constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
@@ -335,6 +341,39 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(2);
     // Q3
     if (walker) walk(kWalkQ2, kWalkQ3);
+#if FVAD_Q3_WIN
+    // lane (frame, window): the window's 5 lags from one register window of y
+    // sliding a sample per step (Q1's form), 5 independent sums each in j order
+    if (tq < 2 * kPcF) {
+      const int fr = tq >> 1, wdw = tq & 1;
+      const int bp0 = best[fr][0], bp1 = best[fr][1];
+      const int i0 = 2 * (wdw ? bp1 : bp0) - 2;
+      const int ib = i0 < 0 ? 0 : i0;  // first lag computed (lags < 0 do not exist)
+      const float *xl = xf[fr] + (kPitchMax >> 1), *y = xf[fr] + ib;
+      constexpr int R = 5;
+      float acc[R], win[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        acc[r] = 0.0f;
+        win[r] = y[r];
+      }
+      for (int jb = 0; jb < 480; jb += R) {
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+          const float xv = xl[jb + u];
+#pragma unroll
+          for (int r = 0; r < R; r++) acc[r] = acc[r] + xv * win[(r + u) % R];
+          win[u] = y[jb + u + R];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const int lag = ib + r, sl = lag - i0;
+        const bool dup = wdw && abs(lag - 2 * bp0) <= 2;
+        if (sl < R && lag < 294 && !dup) fine[fr][R * wdw + sl] = (-1 > acc[r]) ? -1 : acc[r];
+      }
+    }
+#else
     if (tq < 10 * kPcF) {
       const int fr = tq / 10, u = tq - 10 * fr;
       const int bp0 = best[fr][0], bp1 = best[fr][1];
@@ -346,6 +385,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         fine[fr][u] = (-1 > sum) ? -1 : sum;
       }
     }
+#endif
     __syncthreads();
     RSTAMP(3);
     // Q4
@@ -401,6 +441,106 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     }
     __syncthreads();
     RSTAMP(4);
+    // Q5
+#if FVAD_Q5_SPLIT
+    // Item (frame, candidate c) = lane fr * 15 + c of waves 0-1 for the
+    // sliding-window sums (T-1, T, T+1) and the same lane of waves 2-3 for the
+    // T1b sum, which goes through xc (dead since Q2) to the window lane: each
+    // wave's serial walk carries 3 or 1 chains instead of 4.
+    const bool q5b = tq >= 128;
+    const int q5i = q5b ? tq - 128 : tq;
+    const int q5f = q5i / 15, q5c = q5i - 15 * q5f;
+    const bool q5on = q5i < 15 * kPcF && fval[q5f] && (q5c == 0 ? !q5b : q5c - 1 < nvs[q5f]);
+    float aM = 0, a0 = 0, aP = 0;
+    int q5T0 = 0, q5Tc = 0, q5Tb = 0;
+    if (q5on) {
+      const int fr = q5f, c = q5c;
+      q5T0 = T0s[fr];
+      q5Tc = c == 0 ? q5T0 : rd_T1(q5T0, c + 1);
+      q5Tb = c == 0 ? q5T0 : rd_T1b(q5T0, q5Tc, c + 1);
+      const float *X = xf[fr] + (kPitchMax >> 1);
+      typedef float v2f __attribute__((ext_vector_type(2)));
+      const char *xb0 = reinterpret_cast<const char *>(&xf[0][0]);
+      const v2f *Xp = reinterpret_cast<const v2f *>(X);
+      int oX = (int)(reinterpret_cast<const char *>(Xp) - xb0);
+      if (q5b) {
+        // xcorr(T1b): X[j - Tb] in aligned pairs, the lane's parity by selects
+        const int mb = -q5Tb, ob = mb & 1;
+        const v2f *Bq = reinterpret_cast<const v2f *>(X + (mb - ob));
+        v2f r0 = Bq[0], rp = Bq[1];
+        float b0 = ob ? r0.y : r0.x, b1 = ob ? rp.x : r0.y;
+        int oB = (int)(reinterpret_cast<const char *>(Bq) - xb0);
+        float aB = 0;
+#pragma unroll 4
+        for (int i = 0; i < 240; i++) {
+          const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
+          const v2f rn = *reinterpret_cast<const v2f *>(xb0 + oB + 16);
+          oX += 8;
+          oB += 8;
+          asm volatile("" : "+v"(oX), "+v"(oB));
+          aB = aB + xp.x * b0;
+          aB = aB + xp.y * b1;
+          b0 = ob ? rp.y : rp.x;
+          b1 = ob ? rn.x : rp.y;
+          rp = rn;
+        }
+        xc[fr][c] = aB;
+      } else {
+        // xcorr at T+1, T, T-1 from one sliding window X[j - Tc - 1 + t]
+        const int m0 = -q5Tc - 1, ow = m0 & 1;
+        const v2f *W = reinterpret_cast<const v2f *>(X + (m0 - ow));
+        v2f q0 = W[0], q1 = W[1], qp = W[2];
+        float w0 = ow ? q0.y : q0.x, w1 = ow ? q1.x : q0.y;
+        float w2 = ow ? q1.y : q1.x, w3 = ow ? qp.x : q1.y;
+        int oW = (int)(reinterpret_cast<const char *>(W) - xb0);
+#pragma unroll 4
+        for (int i = 0; i < 240; i++) {  // j = 2i, 2i + 1
+          const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
+          const v2f qn = *reinterpret_cast<const v2f *>(xb0 + oW + 24);
+          oX += 8;
+          oW += 8;
+          asm volatile("" : "+v"(oX), "+v"(oW));
+          aM = aM + xp.x * w0;
+          a0 = a0 + xp.x * w1;
+          aP = aP + xp.x * w2;
+          aM = aM + xp.y * w1;
+          a0 = a0 + xp.y * w2;
+          aP = aP + xp.y * w3;
+          w0 = w2;
+          w1 = w3;
+          w2 = ow ? qp.y : qp.x;
+          w3 = ow ? qn.x : qp.y;
+          qp = qn;
+        }
+      }
+    }
+    __syncthreads();
+    if (q5on && !q5b) {
+      const int fr = q5f, c = q5c;
+      const float *yrow = Tq + ptile::kYy * ptile::kQuarter + (h * kPcF + fr) * ptile::kYyPitch;
+      const float yyA = yrow[q5Tc];
+      const float xx = T[ptile::kXx * ptile::kQuarter + fr];
+      float *rg = a.rec + fidx[fr] * rec::kSize;
+      const int off = pitch_offset(aP, a0, aM);
+      if (c == 0) {
+        rg[rec::kT0] = __int_as_float(q5T0);
+        rg[rec::kNValid] = __int_as_float(nvs[fr]);
+        rg[rec::kG0] = pitch_gain(a0, xx, yyA);
+        rg[rec::kXy0] = a0;
+        rg[rec::kYy0] = yyA;
+        rg[rec::kOff0] = __int_as_float(off);
+      } else {
+        const float yyB = yrow[q5Tb];
+        float *qk = rg + rec::kK + (c - 1) * rec::kKStride;
+        const float xy = .5f * (a0 + xc[fr][c]), yy = .5f * (yyA + yyB);
+        qk[0] = __int_as_float(q5Tc);
+        qk[1] = pitch_gain(xy, xx, yy);
+        qk[2] = xy;
+        qk[3] = yy;
+        qk[4] = __int_as_float(off);
+      }
+    }
+#else
     // Q5
     if (tq < 15 * kPcF) {
       const int fr = tq / 15, c = tq - 15 * fr;
@@ -483,6 +623,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         }
       }
     }
+#endif
     if (tq == 0) gq = take_group(a, kWorkPcorr);
     __syncthreads();
     RSTAMP(5);
