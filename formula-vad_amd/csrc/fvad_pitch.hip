@@ -44,6 +44,14 @@ namespace fvad {
 #ifndef FVAD_Q3_WIN
 #define FVAD_Q3_WIN 0
 #endif
+#ifndef FVAD_Q5_UNROLL
+#define FVAD_Q5_UNROLL 4
+#endif
+#ifndef FVAD_Q5_XPF
+#define FVAD_Q5_XPF 0  // 1: the broadcast x pair loads one step ahead of its use
+#endif
+#define FVAD_PRAGMA_(x) _Pragma(#x)
+#define FVAD_UNROLL(n) FVAD_PRAGMA_(unroll n)
 #ifndef FVAD_Q5_SPLIT
 #define FVAD_Q5_SPLIT 1
 #endif
@@ -471,9 +479,17 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         float b0 = ob ? r0.y : r0.x, b1 = ob ? rp.x : r0.y;
         int oB = (int)(reinterpret_cast<const char *>(Bq) - xb0);
         float aB = 0;
-#pragma unroll 4
+#if FVAD_Q5_XPF
+        v2f xq = *reinterpret_cast<const v2f *>(xb0 + oX);
+#endif
+        FVAD_UNROLL(FVAD_Q5_UNROLL)
         for (int i = 0; i < 240; i++) {
+#if FVAD_Q5_XPF
+          const v2f xp = xq;
+          xq = *reinterpret_cast<const v2f *>(xb0 + oX + 8);
+#else
           const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
+#endif
           const v2f rn = *reinterpret_cast<const v2f *>(xb0 + oB + 16);
           oX += 8;
           oB += 8;
@@ -493,9 +509,17 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         float w0 = ow ? q0.y : q0.x, w1 = ow ? q1.x : q0.y;
         float w2 = ow ? q1.y : q1.x, w3 = ow ? qp.x : q1.y;
         int oW = (int)(reinterpret_cast<const char *>(W) - xb0);
-#pragma unroll 4
+#if FVAD_Q5_XPF
+        v2f xq = *reinterpret_cast<const v2f *>(xb0 + oX);
+#endif
+        FVAD_UNROLL(FVAD_Q5_UNROLL)
         for (int i = 0; i < 240; i++) {  // j = 2i, 2i + 1
+#if FVAD_Q5_XPF
+          const v2f xp = xq;
+          xq = *reinterpret_cast<const v2f *>(xb0 + oX + 8);
+#else
           const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
+#endif
           const v2f qn = *reinterpret_cast<const v2f *>(xb0 + oW + 24);
           oX += 8;
           oW += 8;
