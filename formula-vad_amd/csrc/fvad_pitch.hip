@@ -41,20 +41,11 @@ namespace fvad {
 #ifndef FVAD_WALK_Q3
 #define FVAD_WALK_Q3 72
 #endif
-#ifndef FVAD_Q3_WIN
-#define FVAD_Q3_WIN 0
-#endif
 #ifndef FVAD_Q5_UNROLL
-#define FVAD_Q5_UNROLL 4
-#endif
-#ifndef FVAD_Q5_XPF
-#define FVAD_Q5_XPF 0  // 1: the broadcast x pair loads one step ahead of its use
+#define FVAD_Q5_UNROLL 4  // Q5 walk unroll (2 / 8 measured no better)
 #endif
 #define FVAD_PRAGMA_(x) _Pragma(#x)
 #define FVAD_UNROLL(n) FVAD_PRAGMA_(unroll n)
-#ifndef FVAD_Q5_SPLIT
-#define FVAD_Q5_SPLIT 1
-#endif
 constexpr int kWalkQ2 = FVAD_WALK_Q2, kWalkQ3 = FVAD_WALK_Q3;  // yy walk blocks done by the end of Q2 / Q3 (of 97)
 constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
 constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
@@ -349,39 +340,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(2);
     // Q3
     if (walker) walk(kWalkQ2, kWalkQ3);
-#if FVAD_Q3_WIN
-    // lane (frame, window): the window's 5 lags from one register window of y
-    // sliding a sample per step (Q1's form), 5 independent sums each in j order
-    if (tq < 2 * kPcF) {
-      const int fr = tq >> 1, wdw = tq & 1;
-      const int bp0 = best[fr][0], bp1 = best[fr][1];
-      const int i0 = 2 * (wdw ? bp1 : bp0) - 2;
-      const int ib = i0 < 0 ? 0 : i0;  // first lag computed (lags < 0 do not exist)
-      const float *xl = xf[fr] + (kPitchMax >> 1), *y = xf[fr] + ib;
-      constexpr int R = 5;
-      float acc[R], win[R];
-#pragma unroll
-      for (int r = 0; r < R; r++) {
-        acc[r] = 0.0f;
-        win[r] = y[r];
-      }
-      for (int jb = 0; jb < 480; jb += R) {
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-          const float xv = xl[jb + u];
-#pragma unroll
-          for (int r = 0; r < R; r++) acc[r] = acc[r] + xv * win[(r + u) % R];
-          win[u] = y[jb + u + R];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < R; r++) {
-        const int lag = ib + r, sl = lag - i0;
-        const bool dup = wdw && abs(lag - 2 * bp0) <= 2;
-        if (sl < R && lag < 294 && !dup) fine[fr][R * wdw + sl] = (-1 > acc[r]) ? -1 : acc[r];
-      }
-    }
-#else
     if (tq < 10 * kPcF) {
       const int fr = tq / 10, u = tq - 10 * fr;
       const int bp0 = best[fr][0], bp1 = best[fr][1];
@@ -393,7 +351,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         fine[fr][u] = (-1 > sum) ? -1 : sum;
       }
     }
-#endif
     __syncthreads();
     RSTAMP(3);
     // Q4
@@ -450,7 +407,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     __syncthreads();
     RSTAMP(4);
     // Q5
-#if FVAD_Q5_SPLIT
     // Item (frame, candidate c) = lane fr * 15 + c of waves 0-1 for the
     // sliding-window sums (T-1, T, T+1) and the same lane of waves 2-3 for the
     // T1b sum, which goes through xc (dead since Q2) to the window lane: each
@@ -479,17 +435,9 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         float b0 = ob ? r0.y : r0.x, b1 = ob ? rp.x : r0.y;
         int oB = (int)(reinterpret_cast<const char *>(Bq) - xb0);
         float aB = 0;
-#if FVAD_Q5_XPF
-        v2f xq = *reinterpret_cast<const v2f *>(xb0 + oX);
-#endif
         FVAD_UNROLL(FVAD_Q5_UNROLL)
         for (int i = 0; i < 240; i++) {
-#if FVAD_Q5_XPF
-          const v2f xp = xq;
-          xq = *reinterpret_cast<const v2f *>(xb0 + oX + 8);
-#else
           const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
-#endif
           const v2f rn = *reinterpret_cast<const v2f *>(xb0 + oB + 16);
           oX += 8;
           oB += 8;
@@ -509,17 +457,9 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         float w0 = ow ? q0.y : q0.x, w1 = ow ? q1.x : q0.y;
         float w2 = ow ? q1.y : q1.x, w3 = ow ? qp.x : q1.y;
         int oW = (int)(reinterpret_cast<const char *>(W) - xb0);
-#if FVAD_Q5_XPF
-        v2f xq = *reinterpret_cast<const v2f *>(xb0 + oX);
-#endif
         FVAD_UNROLL(FVAD_Q5_UNROLL)
         for (int i = 0; i < 240; i++) {  // j = 2i, 2i + 1
-#if FVAD_Q5_XPF
-          const v2f xp = xq;
-          xq = *reinterpret_cast<const v2f *>(xb0 + oX + 8);
-#else
           const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
-#endif
           const v2f qn = *reinterpret_cast<const v2f *>(xb0 + oW + 24);
           oX += 8;
           oW += 8;
@@ -564,90 +504,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         qk[4] = __int_as_float(off);
       }
     }
-#else
-    // Q5
-    if (tq < 15 * kPcF) {
-      const int fr = tq / 15, c = tq - 15 * fr;
-      if (fval[fr] && (c == 0 || c - 1 < nvs[fr])) {
-        const int T0 = T0s[fr];
-        const int Tc = c == 0 ? T0 : rd_T1(T0, c + 1);
-        const int Tb = c == 0 ? T0 : rd_T1b(T0, Tc, c + 1);
-        // yy_lookup and xx gathers, consumed after the products
-        const float *yrow = Tq + ptile::kYy * ptile::kQuarter + (h * kPcF + fr) * ptile::kYyPitch;
-        const float yyA = yrow[Tc];
-        const float yyB = yrow[Tb];
-        const float xx = T[ptile::kXx * ptile::kQuarter + fr];
-        const float *X = xf[fr] + (kPitchMax >> 1);
-        float aM = 0, a0 = 0, aP = 0, aB = 0;  // lags T+1, T, T-1, T1b
-        // Operands come in 8-byte aligned pairs (ds_read_b64): the broadcast
-        // x[j], x[j+1]; the window stream X[j - Tc - 1 + t] and the T1b stream
-        // X[j - Tb + t], each read from the even index at or below its start
-        // and shifted by the lane's parity (ow, ob) through selects.  Each sum
-        // still adds its products in j order.
-        const int m0 = -Tc - 1, ow = m0 & 1;
-        const int mb = c == 0 ? 0 : -Tb, ob = mb & 1;  // candidate 0 needs no T1b (broadcast address)
-        typedef float v2f __attribute__((ext_vector_type(2)));
-        const v2f *W = reinterpret_cast<const v2f *>(X + (m0 - ow));
-        const v2f *Bq = reinterpret_cast<const v2f *>(X + (mb - ob));
-        const v2f *Xp = reinterpret_cast<const v2f *>(X);
-        v2f q0 = W[0], q1 = W[1], qp = W[2];
-        float w0 = ow ? q0.y : q0.x, w1 = ow ? q1.x : q0.y;
-        float w2 = ow ? q1.y : q1.x, w3 = ow ? qp.x : q1.y;
-        v2f r0 = Bq[0], rp = Bq[1];
-        float b0 = ob ? r0.y : r0.x, b1 = ob ? rp.x : r0.y;
-        const char *xb0 = reinterpret_cast<const char *>(&xf[0][0]);
-        int oX = (int)(reinterpret_cast<const char *>(Xp) - xb0), oW = (int)(reinterpret_cast<const char *>(W) - xb0),
-            oB = (int)(reinterpret_cast<const char *>(Bq) - xb0);
-#pragma unroll 4
-        for (int i = 0; i < 240; i++) {  // j = 2i, 2i + 1
-          // byte offsets the compiler cannot see through, bumped per step:
-          // every pair load stays a single ds_read_b64 (64 banks) instead of
-          // merged ds_read2_b64s, at one add per stream and step
-          const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
-          const v2f qn = *reinterpret_cast<const v2f *>(xb0 + oW + 24);
-          const v2f rn = *reinterpret_cast<const v2f *>(xb0 + oB + 16);
-          oX += 8;
-          oW += 8;
-          oB += 8;
-          asm volatile("" : "+v"(oX), "+v"(oW), "+v"(oB));
-          aM = aM + xp.x * w0;
-          a0 = a0 + xp.x * w1;
-          aP = aP + xp.x * w2;
-          aB = aB + xp.x * b0;
-          aM = aM + xp.y * w1;
-          a0 = a0 + xp.y * w2;
-          aP = aP + xp.y * w3;
-          aB = aB + xp.y * b1;
-          w0 = w2;
-          w1 = w3;
-          w2 = ow ? qp.y : qp.x;
-          w3 = ow ? qn.x : qp.y;
-          qp = qn;
-          b0 = ob ? rp.y : rp.x;
-          b1 = ob ? rn.x : rp.y;
-          rp = rn;
-        }
-        float *rg = a.rec + fidx[fr] * rec::kSize;
-        const int off = pitch_offset(aP, a0, aM);
-        if (c == 0) {
-          rg[rec::kT0] = __int_as_float(T0);
-          rg[rec::kNValid] = __int_as_float(nvs[fr]);
-          rg[rec::kG0] = pitch_gain(a0, xx, yyA);
-          rg[rec::kXy0] = a0;
-          rg[rec::kYy0] = yyA;
-          rg[rec::kOff0] = __int_as_float(off);
-        } else {
-          float *qk = rg + rec::kK + (c - 1) * rec::kKStride;
-          const float xy = .5f * (a0 + aB), yy = .5f * (yyA + yyB);
-          qk[0] = __int_as_float(Tc);
-          qk[1] = pitch_gain(xy, xx, yy);
-          qk[2] = xy;
-          qk[3] = yy;
-          qk[4] = __int_as_float(off);
-        }
-      }
-    }
-#endif
     if (tq == 0) gq = take_group(a, kWorkPcorr);
     __syncthreads();
     RSTAMP(5);
