@@ -9,8 +9,12 @@ Workload: configs[4]'s per-GPU partition — 2048 synthetic 48 kHz stereo
 streams per GPU (16384 at 8 GPUs), weak scaling, f32 exact numerics.  A step
 = one push of TICKS ticks (480 samples per channel) for every stream of the
 partition — the staged pipeline's kernels (fvad_staged.hip; --mode fused:
-k_prep + k_frame) on the engine's HIP streams, input resident in HBM, device
-VADMachine included.
+k_prep + k_frame) on the engine's HIP streams, device VADMachine included.
+The input is RESIDENT_PUSHES distinct pushes (default 20 x 0.5 s = the first
+10 s of every stream: burst onsets, speech, the every-20th-stream digital
+silence at t = 5 s) held in HBM and cycled through push by push; with the
+driver's --warmup 5 --steps 20 the timed pushes are exactly one cycle, the
+input the flop counts of fvad/cost.py MEASURED were instrumented on.
 
 Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
 each rank runs its own stream partition; `--gpus N` without WORLD_SIZE
@@ -38,16 +42,19 @@ sys.path.insert(0, os.path.join(ROOT, "formula-vad_amd"))
 METRIC = "48 kHz 480-sample VAD frames/sec whole node; max concurrent real-time streams"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector peak (FMA = 2 flops per lane per cycle)
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense BF16/FP16 MFMA (no 2:1 sparsity)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # a timed region starts with no push in flight, so its first push runs its
-    # k_prep3 (~3 ms) unoverlapped; 30 steps keep that fill under 2 % of the
-    # steady-state streaming rate (10 steps: ~5 %)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=3)
+    # k_prep3 (~2.5 ms) unoverlapped: ~2 % of 20 steps.  warmup 5 + steps 20
+    # make the timed pushes exactly one cycle of the 20 resident pushes
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--resident-pushes", type=int, default=20,
+                    help="distinct pushes of synthetic input resident in HBM, cycled through (20 = 10 s)")
     ap.add_argument("--streams-per-gpu", type=int, default=2048)
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--ticks", type=int, default=50)
@@ -150,14 +157,18 @@ def _cpu_model():
         return ""
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, base=0):
     """The oracle's whole per-stream path (rnnoise + re-block + FFT B band sums
     + VADMachine: ora_bench_pipeline, the same work scope as the GPU step),
-    built -O3 -march=native -ffp-contract=off on this host, run single-core
-    and on the cores this process may use (at most 16: the GPU box's share of
-    its host).  Bounded sample: the first ticks of the same synthetic streams,
-    pushed in 50-tick chunks like the GPU step, repeated for about
-    --cpu-seconds each."""
+    built -O3 -march=native -ffp-contract=off on this host, one OS thread per
+    group of streams (simulator.zig:217-228 runs one per instance).  Timed
+    single-core and on every CPU this process may use, capped at 16: the GPU
+    box allots 16 of its host's hardware threads to one GPU and asks worker
+    pools to stay within that share.  Bounded sample: the first CPU_TICKS
+    ticks of the same synthetic streams as the GPU run's resident input, pushed
+    in 50-tick chunks like the GPU step, repeated for about --cpu-seconds each.
+    A whole-host figure (per-thread rate x the host's hardware threads) is
+    reported as an extrapolation, never as `value`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle
@@ -170,9 +181,12 @@ def cpu_baseline(args):
     threads = max(1, min(16, avail))
     S, T, Ch = args.cpu_streams, args.cpu_ticks, args.channels
     n = T * 480
+    total = args.resident_pushes * args.ticks
+    stride = max(1, args.streams_per_gpu // S)
     pcm = np.zeros((S, Ch, n), np.float32)
     for s in range(S):
-        pcm[s] = fvad.synth_stream(s * max(1, args.streams_per_gpu // S), n, Ch)[0]
+        x, _ = fvad.synth_stream(base + s * stride, total * 480, Ch)  # the resident input's generator length
+        pcm[s] = x[:, :n]
 
     def timed(nthr, streams):
         secs, reps = 0.0, 0
@@ -184,13 +198,18 @@ def cpu_baseline(args):
 
     one, one_s, one_r = timed(1, max(1, S // 16))
     allc, all_s, all_r = timed(threads, S)
+    hw = os.cpu_count() or threads
     return {"value": round(allc, 1), "unit": "frames/s", "cores": threads, "kind": "port",
             "single_core": round(one, 1),
+            "host_threads": hw,
+            "whole_host_extrapolated": round(allc / threads * hw, 1),
             "sample": "oracle whole path (rnnoise, FFT B band sums, VADMachine), -O3 -march=native "
-                      "-ffp-contract=off on %s (nproc %s, %d usable); all-core: %d streams x %d ticks x %d ch, "
-                      "%d threads, %d passes, %.1f s; single-core: %d streams, %d passes, %.1f s" % (
-                          cpu_model, os.cpu_count(), avail, S, T, Ch, threads, all_r, all_s,
-                          max(1, S // 16), one_r, one_s)}
+                      "-ffp-contract=off on %s; %d threads = this GPU's CPU allotment on a host of %d hardware "
+                      "threads (%d usable by this process; whole_host_extrapolated = per-thread rate x %d, not "
+                      "measured); sample: the first %d ticks (%.1f s) of %d of the %d streams (every %dth) x %d ch, "
+                      "%d passes in %.1f s; single-core: %d streams, %d passes, %.1f s" % (
+                          cpu_model, threads, hw, avail, hw, T, T * 0.01, S, args.streams_per_gpu, stride, Ch,
+                          all_r, all_s, max(1, S // 16), one_r, one_s)}
 
 
 class StubEngine:
@@ -221,32 +240,37 @@ def stub_main(args):
         time.sleep(0.01 * (1 + rank))
     barrier(dist, torch)
     elapsed = max_over_ranks(time.perf_counter() - t0, dist, torch)
+    # stand-in kernel table: rank r's k_a takes 1 + r ms, k_b 2 - r ms
+    kt = {"total_ms": 3.0, "runs": args.steps, "kernels": {"k_a": 1.0 + rank, "k_b": 2.0 - rank}}
+    kt, ranks = gather_kernel_tables(kt, dist, torch, rank)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": aggregate_rate(B * Ch * T, world, args.steps, elapsed),
                           "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": 1000.0 * elapsed / args.steps, "data": "stub (no GPU)",
-                          "config": {"streams_per_gpu": B, "first_stream": base}}), flush=True)
+                          "config": {"streams_per_gpu": B, "first_stream": base},
+                          "roofline": {"kernels": kt["kernels"], "ranks": ranks}}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
-def host_rate(eng, args, rank, dist, torch):
+def host_rate(eng, args, rank, dist, torch, base):
     """Streaming from host memory (fvad_engine_input_slot / submit / collect):
     two pushes in flight, the input's H2D copy over PCIe overlapping the
-    previous push's kernels, outputs copied back every push.  pinned: the
+    previous push's kernels, outputs copied back every push.  Input: the first
+    two pushes of the resident synthetic audio, alternating.  pinned: the
     producer writes each push into the engine's pinned slot (the copy cost of
     the producer itself is not counted); pageable: submit from an ordinary
     host array (plus a threaded copy into the slot)."""
-    import numpy as np
+    import fvad
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
-    rng = np.random.default_rng(rank)
-    src = (rng.standard_normal((T, B, Ch, 480), dtype=np.float32) * np.float32(0.05))
+    src = fvad.synth_ticks(base, B, Ch, args.resident_pushes * T, 0, 2 * T)
+    halves = (src[:T], src[T:])
     res = {}
     for kind in ("pinned", "pageable"):
         if kind == "pinned":
-            for _ in range(2):  # both slots hold a push's worth of input
+            for k in range(2):  # each slot holds one of the two pushes
                 sl = eng.input_slot()
-                sl[:T] = src
+                sl[:T] = halves[k]
                 eng.submit(sl[:T])
             eng.collect(want=False)
             eng.collect(want=False)
@@ -254,11 +278,11 @@ def host_rate(eng, args, rank, dist, torch):
         barrier(dist, torch)
         t0 = time.perf_counter()
         inflight = 0
-        for _ in range(args.steps):
+        for k in range(args.steps):
             if inflight == 2:
                 eng.collect(want=True)
                 inflight -= 1
-            eng.submit(eng.input_slot()[:T] if kind == "pinned" else src)
+            eng.submit(eng.input_slot()[:T] if kind == "pinned" else halves[k & 1])
             inflight += 1
         while inflight:
             eng.collect(want=True)
@@ -270,10 +294,30 @@ def host_rate(eng, args, rank, dist, torch):
                      1000.0 * sec / args.steps)
     return {"value": round(res["pinned"][0], 1), "unit": "frames/s", "ms_per_step": round(res["pinned"][1], 3),
             "pageable_value": round(res["pageable"][0], 1), "pageable_ms_per_step": round(res["pageable"][1], 3),
-            "input_bytes_per_step": int(src.nbytes),
-            "note": "streaming submit/collect, 2 pushes in flight: input from pinned host slots (value) or "
-                    "pageable host memory (pageable_value), H2D over PCIe inside the timed region and "
-                    "overlapped with the previous push; per-tick outputs copied back every push"}
+            "input_bytes_per_step": int(halves[0].nbytes),
+            "note": "streaming submit/collect, 2 pushes in flight, input = the first two pushes of the synthetic "
+                    "streams alternating: from pinned host slots (value) or pageable host memory (pageable_value), "
+                    "H2D over PCIe inside the timed region and overlapped with the previous push; per-tick "
+                    "outputs copied back every push"}
+
+
+def gather_kernel_tables(kt, dist, torch, rank):
+    """Every rank's per-kernel event times; the line reports the max over ranks
+    per kernel (the slowest rank sets the step) and which rank that was."""
+    if dist is None:
+        return kt, None
+    tables = [None] * dist.get_world_size()
+    dist.all_gather_object(tables, {"rank": rank, "kt": kt})
+    worst = {"total_ms": max(t["kt"]["total_ms"] for t in tables), "runs": min(t["kt"]["runs"] for t in tables),
+             "kernels": {}}
+    where = {}
+    for name in kt["kernels"]:
+        r = max(tables, key=lambda t: t["kt"]["kernels"].get(name, 0.0))
+        worst["kernels"][name] = r["kt"]["kernels"].get(name, 0.0)
+        where[name] = r["rank"]
+    per_rank = {str(t["rank"]): {"push_ms_avg": round(t["kt"]["total_ms"], 4),
+                                 "kernels": {k: round(v, 4) for k, v in t["kt"]["kernels"].items()}} for t in tables}
+    return worst, {"max_rank": where, "per_rank": per_rank}
 
 
 def main():
@@ -288,7 +332,7 @@ def main():
     import fvad
     from fvad import cost
 
-    B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
+    B, Ch, T, P = args.streams_per_gpu, args.channels, args.ticks, args.resident_pushes
     model = fvad.Model(seed=1)
     base, _ = stream_partition(rank, B)
 
@@ -297,7 +341,7 @@ def main():
         eng = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=mode)
         if mode != "fused" and not args.no_vadm:
             eng.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
-        eng.load_synthetic(T, base=base)
+        eng.load_synthetic(T, base=base, pushes=P)
         for _ in range(args.warmup):
             eng.run_resident(T)
         eng.sync()
@@ -311,15 +355,17 @@ def main():
         elapsed = max_over_ranks(time.perf_counter() - t0, dist, torch)
         return eng, elapsed, eng.kernel_times()
 
-    eng, elapsed, kt = measure(args.mode)
+    eng, elapsed, kt_local = measure(args.mode)
+    kt, ranks = gather_kernel_tables(kt_local, dist, torch, rank)
     value = aggregate_rate(B * Ch * T, world, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    host = host_rate(eng, args, rank, dist, torch) if args.host_rate else None
+    host = host_rate(eng, args, rank, dist, torch, base) if args.host_rate else None
     variants = None
     if args.variants and args.mode == "staged":
         del eng  # one engine's buffers at a time
         _, el16, kt16 = measure("fp16")
+        kt16, _ = gather_kernel_tables(kt16, dist, torch, rank)
         variants = {"fp16": {
             "value": round(aggregate_rate(B * Ch * T, world, args.steps, el16), 1), "unit": "frames/s",
             "ms_per_step": round(1000.0 * el16 / args.steps, 3),
@@ -328,14 +374,54 @@ def main():
             "parity": "tolerance (SURVEY.md 8(c): vad |d| <= 2e-2, segments identical; tests/test_gpu_fp16.py)",
             "note": "BASELINE configs[4]'s fp16-GRU variant on the same workload and clock (bench.py --mode fp16 "
                     "gives its full line)"}}
+    fvad.synth_cache_clear()
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
 
-    # roofline of the dominant kernel, per launch, from HIP events recorded
-    # around each kernel on the stream it runs on (fvad_engine_kernel_times)
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32" if args.mode != "fp16" else "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
+        "data": "synthetic",
+        "config": {"workload": "configs[4] per-GPU partition: %d synthetic 48 kHz streams x %d ch per GPU "
+                               "(%d at %d GPU), %d ticks (480 samples/ch) per step, %d distinct resident pushes "
+                               "(%.1f s of every stream) cycled, %s"
+                               % (B, Ch, B * world, world, T, P, P * T * 0.01,
+                                  "fp16 GRU weights on MFMA (configs[4] variant, tolerance parity)" if args.mode == "fp16"
+                                  else "fp32 weights, bit-exact path"),
+                   "streams_per_gpu": B, "channels": Ch, "ticks_per_step": T, "resident_pushes": P,
+                   "fft_size": 2048,
+                   "parallelism": "stream-partition x%d (no collectives)" % world, "mode": args.mode,
+                   "vad_machine": "device" if (args.mode != "fused" and not args.no_vadm) else "none"},
+        "realtime_streams": round(value / (100.0 * Ch), 1),
+        "roofline": roofline(args, kt, value, world, ms_per_step, cost, ranks),
+        "cpu_baseline": None,
+    }
+    if variants is not None:
+        line["variants"] = variants
+    if host is not None:
+        line["host_buffers"] = host
+        line["realtime_streams_host"] = round(host["value"] / (100.0 * Ch), 1)
+    if args.cpu_baseline:  # rank 0 only, at any N (the other ranks have finished)
+        try:
+            line["cpu_baseline"] = cpu_baseline(args, base)
+        except Exception as ex:  # never let the baseline leg kill the GPU measurement
+            line["cpu_baseline"] = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
+                                    "sample": "failed: %s" % ex}
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def roofline(args, kt, value, world, ms_per_step, cost, ranks):
+    """Roofline of the dominant kernel, per launch, from HIP events recorded
+    around each kernel on the stream it runs on (fvad_engine_kernel_times; at
+    N > 1 the max over ranks), plus the whole path against SURVEY.md 8(d)'s
+    ceilings."""
+    B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     frames_launch = B * Ch * T
     if args.mode == "fused":
         prep_share = cost.phases(Ch)["prep: s16 scale + HP biquad + rms"]
@@ -344,7 +430,12 @@ def main():
                              "bytes": cost.frame_kernel_bytes(B, Ch, T) / frames_launch}}
     else:
         per_k = cost.staged_kernels(Ch)
-    ridge = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    # bit-exact C-order sums: no product may fuse with its sum (-ffp-contract=off),
+    # so a flop is one lane-op and the attainable FP32 VALU rate is half the
+    # FMA-counted 157.3 TFLOP/s; a kernel is VALU-bound when its intensity
+    # clears THAT ridge (9.8 flop/B), HBM-bound otherwise
+    valu_nofma = FP32_PEAK_TFLOPS / 2
+    ridge = valu_nofma * 1e12 / (HBM_PEAK_GBS * 1e9)
     kernels = {}
     for name, ms in kt["kernels"].items():
         c = per_k[name]
@@ -361,7 +452,8 @@ def main():
     dom_s = kt["kernels"][dom] / 1000.0
     alg_flops = c["flops"] * frames_launch
     alg_bytes = c["bytes"] * frames_launch
-    compute_bound = c["flops"] / c["bytes"] >= ridge
+    intensity = c["flops"] / c["bytes"]
+    compute_bound = intensity >= ridge
     traffic = None
     pmc_src = None
     push_bytes = None
@@ -378,27 +470,44 @@ def main():
             traffic = None
     if compute_bound:
         achieved, peak, unit = alg_flops / dom_s / 1e12, FP32_PEAK_TFLOPS, "TFLOP/s"
+        attainable = min(valu_nofma, intensity * HBM_PEAK_GBS / 1000.0)
     else:
         achieved, peak, unit = alg_bytes / dom_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        attainable = HBM_PEAK_GBS
     # whole path: frames/s against the lower of the HBM and
-    # FP32-VALU ceilings for the path's algorithmic bytes / flops per frame
+    # FP32-VALU ceilings for the path's algorithmic bytes / flops per frame.
+    # fp16 mode: the GRU stack's flops run on f16 MFMA (2.5 PFLOP/s dense,
+    # v_mfma_f32_16x16x32_f16), the rest on the VALU
     f_alg = cost.flops_per_channel_frame(Ch)
     b_alg = cost.path_bytes_per_channel_frame(Ch)
+    f_gru = cost.phases(Ch)["GRU stack"] if args.mode == "fp16" else 0.0
     fps_gpu = value / world
     ceil_hbm = HBM_PEAK_GBS * 1e9 / b_alg
-    ceil_valu = FP32_PEAK_TFLOPS * 1e12 / f_alg
+    ceil_valu = 1.0 / ((f_alg - f_gru) / (FP32_PEAK_TFLOPS * 1e12) + f_gru / (F16_MFMA_PEAK_TFLOPS * 1e12))
     path = {"f_alg": round(f_alg), "b_alg": round(b_alg), "frames_per_s_per_gpu": round(fps_gpu, 1),
             "ceiling_hbm": round(ceil_hbm, 1), "ceiling_valu": round(ceil_valu, 1),
             "bound": "hbm" if ceil_hbm < ceil_valu else "valu",
             "frac": round(fps_gpu / min(ceil_hbm, ceil_valu), 5),
             "hbm_frac_alg": round(fps_gpu * b_alg / (HBM_PEAK_GBS * 1e9), 5),
             "valu_frac": round(fps_gpu * f_alg / (FP32_PEAK_TFLOPS * 1e12), 5)}
-    roofline = {
+    if f_gru:
+        path["ceiling_note"] = ("fp16 mode: the GRU stack's %d flop per frame priced at the f16 MFMA peak "
+                                "(%.0f TFLOP/s), the other %d at the FP32 VALU peak" % (
+                                    f_gru, F16_MFMA_PEAK_TFLOPS, f_alg - f_gru))
+    if compute_bound:
+        roof = ("FP32 VALU (157.3 TFLOP/s, FMA-counted; %s)" %
+                ("the GRU stack is on f16 MFMA, this kernel is not" if args.mode == "fp16" and dom != "k_gru16"
+                 else "no MFMA instruction runs in this kernel"))
+    else:
+        roof = "HBM3E 8 TB/s"
+    out = {
         "bound": "valu" if compute_bound else "hbm",
-        "roof": ("FP32 VALU (157.3 TFLOP/s; no MFMA instruction runs on this path)"
-                 if compute_bound else "HBM3E 8 TB/s"),
+        "roof": roof,
         "kernel": dom,
         "achieved": round(achieved, 4), "peak": peak, "unit": unit, "frac": round(achieved / peak, 5),
+        "attainable": round(attainable, 2), "frac_attainable": round(achieved / attainable, 5),
+        "attainable_note": "min(FP32 VALU without FMA = 78.65 TFLOP/s, intensity x 8 TB/s) for a VALU-bound "
+                           "kernel: the bit-exact C-order sums keep every mul and add separate",
         "traffic": traffic, "traffic_source": pmc_src,
         "alg_flops_per_launch": alg_flops, "alg_bytes_per_launch": alg_bytes,
         "flop_counts": "fvad/cost.py, data-dependent trip counts instrumented in the oracle (%s)" % (
@@ -408,43 +517,16 @@ def main():
         "path": path,
         "kernels": kernels,
     }
+    if ranks is not None:
+        out["ranks"] = ranks
+        out["kernels_note"] = "max over ranks per kernel (ranks.max_rank names the rank)"
     if push_bytes:
         # whole-push HBM traffic (PMC bytes of all its kernels) over the
         # measured time per push: the pipeline's average HBM utilisation
         gbs = push_bytes / (ms_per_step / 1000.0) / 1e9
-        roofline["push_hbm"] = {"bytes": push_bytes, "gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                "bytes_per_frame": round(push_bytes / frames_launch, 1)}
-    cpu = None
-    if args.cpu_baseline and world == 1:
-        try:
-            cpu = cpu_baseline(args)
-        except Exception as ex:  # never let the baseline leg kill the GPU measurement
-            cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port", "sample": "failed: %s" % ex}
-    line = {
-        "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32" if args.mode != "fp16" else "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
-        "data": "synthetic",
-        "config": {"workload": "configs[4] per-GPU partition: %d synthetic 48 kHz streams x %d ch per GPU "
-                               "(%d at %d GPU), %d ticks (480 samples/ch) per step, %s"
-                               % (B, Ch, B * world, world, T,
-                                  "fp16 GRU weights on MFMA (configs[4] variant, tolerance parity)" if args.mode == "fp16"
-                                  else "fp32 weights, bit-exact path"),
-                   "streams_per_gpu": B, "channels": Ch, "ticks_per_step": T, "fft_size": 2048,
-                   "parallelism": "stream-partition x%d (no collectives)" % world, "mode": args.mode,
-                   "vad_machine": "device" if (args.mode != "fused" and not args.no_vadm) else "none"},
-        "realtime_streams": round(value / (100.0 * Ch), 1),
-        "roofline": roofline,
-        "cpu_baseline": cpu,
-    }
-    if variants is not None:
-        line["variants"] = variants
-    if host is not None:
-        line["host_buffers"] = host
-        line["realtime_streams_host"] = round(host["value"] / (100.0 * Ch), 1)
-    print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        out["push_hbm"] = {"bytes": push_bytes, "gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                           "bytes_per_frame": round(push_bytes / frames_launch, 1)}
+    return out
 
 
 if __name__ == "__main__":

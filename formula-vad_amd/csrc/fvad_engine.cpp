@@ -123,6 +123,9 @@ struct fvad_engine {
   // its own.  ev_in_free[i]: buffer i's last reader (k_prep3 / k_prep) done.
   // run_resident reads d_pcm_b[0] (fvad_engine_load_synthetic).
   float *d_pcm_b[2] = {};
+  // fvad_engine_load_synthetic_ex with n_pushes > 1: [push][tick][stream][ch][480]
+  float *d_res = nullptr;
+  int res_pushes = 0, res_next = 0;
   hipEvent_t ev_in_free[2] = {};
   bool in_busy[2] = {false, false};
   int in_next = 0;
@@ -291,7 +294,7 @@ void free_all(fvad_engine *e) {
                   e->d_model, e->d_stamps, e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->d_gru16, e->d_gru16_bias, e->vadm.st, e->vadm.buf,
-                  e->vadm.seg, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband};
+                  e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &set : e->evs)
@@ -939,35 +942,51 @@ extern "C" int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_tic
 }
 
 extern "C" int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t base) {
+  return fvad_engine_load_synthetic_ex(e, n_ticks, 1, base);
+}
+
+// n_pushes distinct pushes of n_ticks resident in HBM: stream s's first
+// n_pushes * n_ticks ticks of fvad_synth_stream(base + s) (generated at that
+// length).  One push lives in the input buffer d_pcm_b[0]; more get their own
+// [push][tick][stream][ch][480] buffer, and run_resident cycles through them.
+extern "C" int fvad_engine_load_synthetic_ex(fvad_engine *e, int n_ticks, int n_pushes, uint32_t base) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   const fvad_engine_config &c = e->cfg;
   if (n_ticks < 1 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range");
+  if (n_pushes < 1) return fail(FVAD_EINVAL, "n_pushes must be >= 1");
   HIP_TRY(hipSetDevice(c.device));
-  const size_t n = (size_t)n_ticks * fvad::kFrame;
-  const size_t B = c.n_streams, C = c.n_channels;
-  std::vector<float> host((size_t)n_ticks * B * C * fvad::kFrame);
-  unsigned nthr = std::thread::hardware_concurrency();
-  if (nthr < 1) nthr = 1;
-  if (nthr > 16) nthr = 16;
-  std::vector<std::thread> pool;
-  for (unsigned w = 0; w < nthr; w++) {
-    pool.emplace_back([&, w]() {
-      std::vector<float> one(C * n);
-      for (size_t s = w; s < B; s += nthr) {
-        fvad_synth_stream(base + (uint32_t)s, n, (int)C, one.data(), nullptr, 0);
-        for (int t = 0; t < n_ticks; t++)
-          for (size_t ch = 0; ch < C; ch++)
-            std::memcpy(&host[(((size_t)t * B + s) * C + ch) * fvad::kFrame],
-                        &one[ch * n + (size_t)t * fvad::kFrame], fvad::kFrame * sizeof(float));
-      }
-    });
+  const size_t per_push = (size_t)n_ticks * c.n_streams * c.n_channels * fvad::kFrame;
+  std::vector<float> host;
+  try {
+    host.resize(per_push * n_pushes);
+  } catch (...) {
+    return fail(FVAD_ENOMEM, "host buffer for the synthetic input");
   }
-  for (auto &th : pool) th.join();
-  // buffer 0 may still be read by an in-flight push
-  const int rc = fvad_engine_sync(e);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpy(e->d_pcm_b[0], host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+  int rc = fvad_synth_ticks(base, c.n_streams, c.n_channels, n_ticks * n_pushes, 0, n_ticks * n_pushes, host.data());
+  if (rc) return fail(rc, "fvad_synth_ticks failed");
+  // buffer 0 (or the resident set) may still be read by an in-flight push
+  if ((rc = fvad_engine_sync(e))) return rc;
+  if (e->d_res) {
+    HIP_TRY(hipFree(e->d_res));
+    e->d_res = nullptr;
+  }
+  e->res_pushes = 0;
+  if (n_pushes == 1) {
+    HIP_TRY(hipMemcpy(e->d_pcm_b[0], host.data(), per_push * sizeof(float), hipMemcpyHostToDevice));
+  } else {
+    if ((rc = dalloc(&e->d_res, per_push * n_pushes))) return rc;
+    HIP_TRY(hipMemcpy(e->d_res, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+    e->res_pushes = n_pushes;
+  }
+  e->res_next = 0;
   e->resident_ticks = n_ticks;
+  return FVAD_OK;
+}
+
+extern "C" int fvad_engine_resident_seek(fvad_engine *e, int push) {
+  if (!e || e->resident_ticks < 1) return fail(FVAD_EINVAL, "no resident input");
+  if (push < 0 || push >= std::max(1, e->res_pushes)) return fail(FVAD_EINVAL, "push index out of range");
+  e->res_next = push;
   return FVAD_OK;
 }
 
@@ -981,7 +1000,13 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
   e->ev = e->evs[e->ev_slot];
   int rc = collect_slot(e, e->ev_slot);
   if (rc) return rc;
-  e->d_pcm = e->d_pcm_b[0];
+  if (e->res_pushes > 1) {  // the next of the resident pushes, cyclically
+    const size_t per_push = (size_t)e->resident_ticks * e->cfg.n_streams * e->cfg.n_channels * fvad::kFrame;
+    e->d_pcm = e->d_res + per_push * (size_t)e->res_next;
+    e->res_next = (e->res_next + 1) % e->res_pushes;
+  } else {
+    e->d_pcm = e->d_pcm_b[0];
+  }
   // FVAD_NO_EVENTS=1: no timing events (diagnostic: their cost on the push)
   static const bool no_events = [] {
     const char *v = getenv("FVAD_NO_EVENTS");
@@ -989,8 +1014,10 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
   }();
   if ((rc = launch(e, n_ticks, false, !no_events))) return rc;
   // a later submit / push must not overwrite buffer 0 under this run's prep
-  HIP_TRY(hipEventRecord(e->ev_in_free[0], input_reader(e)));
-  e->in_busy[0] = true;
+  if (e->res_pushes <= 1) {
+    HIP_TRY(hipEventRecord(e->ev_in_free[0], input_reader(e)));
+    e->in_busy[0] = true;
+  }
   return FVAD_OK;
 }
 

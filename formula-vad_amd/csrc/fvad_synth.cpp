@@ -12,11 +12,15 @@
 //     ground-truth labels (Audacity txt, seconds);
 //   * every 20th stream has 1 s of digital silence (exact zeros) at t = 5 s.
 // This is workload data for tests and bench; it is not part of the hot path.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
+#include <thread>
 #include <vector>
 
+#include "../../include/fvad.h"
 #include "fvad_internal.h"
 
 namespace {
@@ -168,4 +172,75 @@ extern "C" long fvad_synth_stream(uint32_t stream_id, size_t n, int n_ch, float 
     }
   }
   return n_labels;
+}
+
+// The same streams in the engine's push layout: ticks [tick0, tick0 + n_ticks)
+// of streams base .. base + n_streams - 1, each generated with length
+// total_ticks * 480 (the generator's output depends on the length), written
+// as out[t][s][c][480].  Generation runs on up to 16 host threads; the last
+// whole [total_ticks][streams][channels][480] block is cached, so the bench's
+// second engine (and its host-buffer leg) reuse it instead of regenerating
+// ~1 G samples.
+namespace {
+struct SynthCache {
+  std::mutex mu;
+  uint32_t base = 0;
+  int n_streams = 0, n_channels = 0, total_ticks = 0;
+  std::vector<float> data;  // [total_ticks][n_streams][n_channels][480]
+};
+SynthCache &synth_cache() {
+  static SynthCache c;
+  return c;
+}
+}  // namespace
+
+extern "C" int fvad_synth_ticks(uint32_t base, int n_streams, int n_channels, int total_ticks, int tick0,
+                                int n_ticks, float *out) {
+  if (n_streams < 1 || n_channels < 1 || total_ticks < 1 || tick0 < 0 || n_ticks < 0 ||
+      tick0 + n_ticks > total_ticks || (!out && n_ticks))
+    return FVAD_EINVAL;
+  constexpr size_t F = fvad::kFrame;
+  const size_t B = (size_t)n_streams, C = (size_t)n_channels, n = (size_t)total_ticks * F;
+  SynthCache &sc = synth_cache();
+  std::lock_guard<std::mutex> lock(sc.mu);
+  if (sc.base != base || sc.n_streams != n_streams || sc.n_channels != n_channels || sc.total_ticks != total_ticks ||
+      sc.data.empty()) {
+    sc.data.clear();
+    sc.data.shrink_to_fit();
+    try {
+      sc.data.resize((size_t)total_ticks * B * C * F);
+    } catch (...) {
+      sc.n_streams = 0;
+      return FVAD_ENOMEM;
+    }
+    unsigned nthr = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    float *dst = sc.data.data();
+    for (unsigned w = 0; w < nthr; w++) {
+      pool.emplace_back([=]() {
+        std::vector<float> one(C * n);
+        for (size_t s = w; s < B; s += nthr) {
+          fvad_synth_stream(base + (uint32_t)s, n, (int)C, one.data(), nullptr, 0);
+          for (size_t t = 0; t < (size_t)total_ticks; t++)
+            for (size_t ch = 0; ch < C; ch++)
+              std::memcpy(dst + ((t * B + s) * C + ch) * F, one.data() + ch * n + t * F, F * sizeof(float));
+        }
+      });
+    }
+    for (auto &th : pool) th.join();
+    sc.base = base;
+    sc.n_streams = n_streams;
+    sc.n_channels = n_channels;
+    sc.total_ticks = total_ticks;
+  }
+  if (n_ticks) std::memcpy(out, sc.data.data() + (size_t)tick0 * B * C * F, (size_t)n_ticks * B * C * F * sizeof(float));
+  return FVAD_OK;
+}
+
+extern "C" void fvad_synth_cache_clear(void) {
+  SynthCache &sc = synth_cache();
+  std::lock_guard<std::mutex> lock(sc.mu);
+  sc.data.clear();
+  sc.data.shrink_to_fit();
+  sc.n_streams = 0;
 }

@@ -144,6 +144,8 @@ SYMBOLS = [
     ("fvad_engine_submit", C.c_int, [C.c_void_p, F32P, C.c_int, I32P]),
     ("fvad_engine_collect", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]),
     ("fvad_engine_load_synthetic", C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
+    ("fvad_engine_load_synthetic_ex", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32]),
+    ("fvad_engine_resident_seek", C.c_int, [C.c_void_p, C.c_int]),
     ("fvad_engine_run_resident", C.c_int, [C.c_void_p, C.c_int]),
     ("fvad_engine_sync", C.c_int, [C.c_void_p]),
     ("fvad_engine_kernel_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
@@ -183,6 +185,8 @@ SYMBOLS = [
     ("fvad_eval_aggregate", None, [C.c_void_p, C.c_size_t, C.c_void_p]),
     ("fvad_parse_audacity", C.c_long, [C.c_char_p, C.c_size_t, F32P, C.c_size_t]),
     ("fvad_synth_stream", C.c_long, [C.c_uint32, C.c_size_t, C.c_int, F32P, F32P, C.c_size_t]),
+    ("fvad_synth_ticks", C.c_int, [C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, F32P]),
+    ("fvad_synth_cache_clear", None, []),
     ("fvad_simulator_main", C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
 ]
 
@@ -245,6 +249,20 @@ def synth_stream(stream_id, n_samples, n_channels=2, label_cap=4096):
     lab = np.zeros(2 * label_cap, np.float32)
     n = lib().fvad_synth_stream(stream_id, n_samples, n_channels, fptr(out), fptr(lab), label_cap)
     return out, lab[: 2 * min(n, label_cap)].reshape(-1, 2).copy()
+
+
+def synth_ticks(base, n_streams, n_channels, total_ticks, tick0=0, n_ticks=None):
+    """fvad_synth_ticks: [n_ticks][n_streams][n_channels][480] of the streams
+    base.. generated at total_ticks * 480 samples (cached in the library)."""
+    n_ticks = total_ticks - tick0 if n_ticks is None else n_ticks
+    out = np.zeros((n_ticks, n_streams, n_channels, FRAME), np.float32)
+    _check(lib().fvad_synth_ticks(base, n_streams, n_channels, total_ticks, tick0, n_ticks, fptr(out)),
+           "fvad_synth_ticks")
+    return out
+
+
+def synth_cache_clear():
+    lib().fvad_synth_cache_clear()
 
 
 class Engine:
@@ -329,8 +347,12 @@ class Engine:
     def reset(self):
         _check(lib().fvad_engine_reset(self.h), "fvad_engine_reset")
 
-    def load_synthetic(self, n_ticks, base=0):
-        _check(lib().fvad_engine_load_synthetic(self.h, n_ticks, base), "fvad_engine_load_synthetic")
+    def load_synthetic(self, n_ticks, base=0, pushes=1):
+        """pushes distinct resident pushes of n_ticks (run_resident cycles through them)."""
+        _check(lib().fvad_engine_load_synthetic_ex(self.h, n_ticks, pushes, base), "fvad_engine_load_synthetic_ex")
+
+    def resident_seek(self, push):
+        _check(lib().fvad_engine_resident_seek(self.h, push), "fvad_engine_resident_seek")
 
     def run_resident(self, n_ticks):
         _check(lib().fvad_engine_run_resident(self.h, n_ticks), "fvad_engine_run_resident")

@@ -13,10 +13,11 @@ breakdown is reproduced in DESIGN.md §5.
 FRAME = 480
 
 # tests/count_ops.py on the bench workload (256 of the 2048 synthetic streams,
-# 4 pushes of the same 50 resident ticks, as bench.py runs them): per
-# channel-frame averages; tests/test_host_cpu.py recounts them
-MEASURED = {"fine_lags_per_frame": 9.4088, "rd_cands_per_frame": 7.1532, "silent_frac": 0.0,
-            "frames_counted": 102400}
+# the 20 distinct resident 50-tick pushes = their first 10 s, as bench.py
+# cycles through them): per channel-frame averages; tests/test_host_cpu.py
+# recounts them
+MEASURED = {"fine_lags_per_frame": 9.3352, "rd_cands_per_frame": 6.6061, "silent_frac": 0.004516,
+            "frames_counted": 512000}
 PTILE_ROWS = 864 + 147 + 294 + 388 + 1  # k_plpc -> k_pcorr rows per frame (fvad_staged.h ptile)
 
 

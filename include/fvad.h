@@ -71,7 +71,8 @@ typedef struct kiss_fftr_state *kiss_fftr_cfg;
 /* kiss_fftr_alloc — FFT.zig:183,199.  Same lenmem protocol: with mem == NULL
  * or *lenmem too small it returns NULL and writes the required size into
  * *lenmem; otherwise the config lives in the caller's memory.  Forward only;
- * nfft must be even and nfft/2 a power of 4 (the reference uses 2048). */
+ * nfft must be even (kissfft's mixed radix: factors 4, 2, 3, 5 and generic
+ * primes, as kf_factor picks them; the reference uses 2048). */
 kiss_fftr_cfg kiss_fftr_alloc(int nfft, int inverse_fft, void *mem, size_t *lenmem);
 /* kiss_fftr — FFT.zig:90.  timedata: nfft floats; freqdata: nfft/2+1 bins. */
 void kiss_fftr(kiss_fftr_cfg cfg, const float *timedata, kiss_fft_cpx *freqdata);
@@ -169,7 +170,14 @@ int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_ticks);
 /* Device-resident variants for benchmarking / zero-copy producers. */
 /* allocate a device input of n_ticks and fill it with the synthetic generator */
 int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t stream_id_base);
-/* run one push over the resident device input, async on the engine stream */
+/* n_pushes distinct pushes of n_ticks resident in HBM: stream s's first
+ * n_pushes * n_ticks ticks of fvad_synth_stream(stream_id_base + s) (generated
+ * at that length); run_resident cycles through them, starting at push 0 */
+int fvad_engine_load_synthetic_ex(fvad_engine *e, int n_ticks, int n_pushes, uint32_t stream_id_base);
+/* the resident push the next run_resident reads */
+int fvad_engine_resident_seek(fvad_engine *e, int push);
+/* run one push over the resident device input (the next one of the cycle),
+ * async on the engine stream */
 int fvad_engine_run_resident(fvad_engine *e, int n_ticks);
 int fvad_engine_sync(fvad_engine *e);
 /* average per-launch kernel durations (ms) of the timed resident runs,
@@ -321,6 +329,14 @@ long fvad_parse_audacity(const char *txt, size_t len, float *from_to, size_t cap
 /* Synthetic 48 kHz onboard audio; returns label count */
 long fvad_synth_stream(uint32_t stream_id, size_t n, int n_channels, float *out, float *labels,
                        size_t label_cap);
+
+/* The same streams in the engine's push layout: ticks [tick0, tick0 + n_ticks)
+ * of streams base .. base + n_streams - 1, each generated at total_ticks * 480
+ * samples, into out[t][s][c][480].  The last whole block is cached in host
+ * memory (fvad_synth_cache_clear frees it). */
+int fvad_synth_ticks(uint32_t stream_id_base, int n_streams, int n_channels, int total_ticks, int tick0,
+                     int n_ticks, float *out);
+void fvad_synth_cache_clear(void);
 
 /* simulator -i plan.json (simulator.zig:74-139) — returns process exit code */
 int fvad_simulator_main(int argc, char **argv);

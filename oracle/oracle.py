@@ -309,11 +309,12 @@ class Pipeline:
         nf = C.c_size_t()
         nw = C.c_size_t()
         lib().ora_pipeline_trace_counts(self.h, C.byref(nf), C.byref(nw))
-        frames = np.array([(t.frame_index, t.vad_low, t.vol_ratio) for t in self.tf[:nf.value]],
-                          dtype=[("index", np.uint64), ("vad", np.float32), ("ratio", np.float32)])
-        wins = np.array([(t.index, tuple(t.band), t.vol_ratio, t.vad) for t in self.tw[:nw.value]],
-                        dtype=[("index", np.uint64), ("band", np.float32, 8), ("ratio", np.float32),
-                               ("vad", np.float32)])
+        # the trace structs read in place (same field layout: 16 and 48 bytes)
+        fdt = np.dtype([("index", np.uint64), ("vad", np.float32), ("ratio", np.float32)])
+        wdt = np.dtype([("index", np.uint64), ("band", np.float32, 8), ("ratio", np.float32), ("vad", np.float32)])
+        assert fdt.itemsize == C.sizeof(FrameTrace) and wdt.itemsize == C.sizeof(WindowTrace)
+        frames = np.frombuffer(self.tf, dtype=fdt, count=nf.value).copy()
+        wins = np.frombuffer(self.tw, dtype=wdt, count=nw.value).copy()
         return frames, wins
 
     def __del__(self):

@@ -1,12 +1,13 @@
 """Instrumented work counts of the bench workload (test infrastructure: runs
 the oracle, never imported by the product).
 
-The bench (bench.py) re-runs one resident push of 50 ticks of the synthetic
-streams fvad_synth_stream(base + s) per step.  This runs the same input through
-the oracle's whole per-stream path (ora_bench_pipeline: rnnoise + FFT B +
-VADMachine) for a strided sample of the 2048 streams, 4 pushes each, and
-counts per channel-frame what the algorithm actually does where its work is
-data dependent:
+The bench (bench.py) cycles through 20 resident pushes of 50 ticks: the first
+10 s of the synthetic streams fvad_synth_stream(base + s) (generated at that
+length); with --warmup 5 --steps 20 the timed pushes are exactly one cycle.
+This runs the same input through the oracle's whole per-stream path
+(ora_bench_pipeline: rnnoise + FFT B + VADMachine) for a strided sample of the
+2048 streams, in 50-tick pushes, and counts per channel-frame what the
+algorithm actually does where its work is data dependent:
 
   fine_lags   pitch_search's fine xcorr lags (|i - 2 best| <= 2 for either of
               the two coarse candidates: 5..10 per frame)
@@ -26,7 +27,7 @@ for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "formula-vad_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-STREAMS, STRIDE, TICKS, PUSHES, CHANNELS = 256, 8, 50, 4, 2
+STREAMS, STRIDE, TICKS, PUSHES, CHANNELS = 256, 8, 50, 20, 2
 
 
 def count(streams=STREAMS, stride=STRIDE, ticks=TICKS, pushes=PUSHES, channels=CHANNELS, threads=8):
@@ -36,8 +37,9 @@ def count(streams=STREAMS, stride=STRIDE, ticks=TICKS, pushes=PUSHES, channels=C
     n = ticks * 480
     pcm = np.zeros((streams, channels, n * pushes), np.float32)
     for i in range(streams):
-        x, _ = fvad.synth_stream(i * stride, n, channels)
-        pcm[i] = np.tile(x, (1, pushes))
+        # stride-8 ids shifted by i % 8, so the sample includes the every-20th
+        # stream with digital silence (ids = 19 mod 20 are odd)
+        pcm[i], _ = fvad.synth_stream(i * stride + i % stride, n * pushes, channels)
     _, c = oracle.bench_pipeline(pcm, chunk=n, n_threads=threads)
     f = c["frames"]
     return {"fine_lags_per_frame": round(c["fine_lags"] / f, 4), "rd_cands_per_frame": round(c["rd_cands"] / f, 4),

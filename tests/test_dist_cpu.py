@@ -72,3 +72,8 @@ def test_bench_self_launch_two_ranks():
     assert d["n_gpus"] == 2
     assert d["ms_per_step"] >= 20.0  # rank 1's 20 ms per step, not rank 0's 10
     assert d["value"] == pytest.approx(2048 * 2 * 50 * 2 / (d["ms_per_step"] / 1000.0), rel=1e-6)
+    # per-rank kernel tables, max over ranks per kernel (the slowest rank sets the step)
+    ro = d["roofline"]
+    assert ro["kernels"] == {"k_a": 2.0, "k_b": 2.0}
+    assert ro["ranks"]["max_rank"] == {"k_a": 1, "k_b": 0}
+    assert set(ro["ranks"]["per_rank"]) == {"0", "1"}

@@ -149,34 +149,6 @@ def test_fp16_twenty_streams_evaluator(fvad_mod, oracle_mod, models):
     assert tot["g"] == tot["o"], tot
 
 
-def test_fp16_resident_bench_shape(fvad_mod, oracle_mod, models):
-    """The bench's fp16 engine (2048 streams, 50-tick pushes, VADMachine
-    attached) against the oracle on a stride of streams over two pushes."""
-    m, om = models
-    B, T = 2048, 50
-    eng = fvad_mod.Engine(m, B, 2, max_ticks=T, mode="fp16")
-    eng.attach_vadm()
-    eng.load_synthetic(T, base=0)
-    outs = []
-    for _ in range(2):
-        eng.run_resident(T)
-        eng.sync()
-        outs.append(eng.fetch(T))
-    vad = np.concatenate([o["vad"] for o in outs])
-    worst = 0.0
-    for s in range(0, B, 61):
-        x = fvad_mod.synth_stream(s, T * 480, 2)[0]
-        p = oracle_mod.Pipeline(2, om, trace_frames=2 * T + 1)
-        p.push([x[0], x[1]])
-        p.push([x[0], x[1]])
-        fr, _ = p.trace()
-        d = float(np.abs(fr["vad"] - vad[:, s]).max())
-        worst = max(worst, d)
-        assert d <= VAD_ABS, (s, d)
-        assert np.array_equal(fr["ratio"], np.concatenate([o["ratio"][:, s] for o in outs]))
-    print("fp16 bench shape: max |dvad| %.3g over %d streams" % (worst, len(range(0, B, 61))))
-
-
 def test_fp16_fft_size_1000_segments(fvad_mod, oracle_mod, models):
     """fp16 mode with a non-default VAD.Config (fft_size 1000: FFT B on the
     mixed-radix block kernel, bands from FFT.freqToBin) and device VADMachines:

@@ -4,7 +4,7 @@
 #   tools/quick.sh [pytest -k expression]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-K=${1:-"test_engine_bit_exact_ragged or test_engine_channels or test_full_size_bench_config_parity or test_fp16_ragged"}
+K=${1:-"test_engine_bit_exact_ragged or test_engine_channels or test_configs3_shard or test_fp16_ragged"}
 timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "$K" \
   > gpurun_out/quick_test.log 2>&1 || { tail -30 gpurun_out/quick_test.log; exit 1; }
 tail -1 gpurun_out/quick_test.log
