@@ -106,6 +106,7 @@ struct fvad_engine {
   int V = 0, L = 0, LX = 0, wmax = 0, grid_frames = 0;
   int resident_ticks = 0;
   int n_kernels = 0;
+  bool olafb = false;  // staged: k_olafb in place of k_ola, k_winmeta, k_fftbw (kernel 8)
   // per-kernel timing events, two sets used alternately so the host reads
   // push k's events while push k+1 is already queued (no launch gap)
   hipEvent_t evs[2][FVAD_MAX_TIMES] = {};
@@ -389,6 +390,13 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   // frame's float4 writes never straddle its end (k_ola, k_ndring)
   e->ring_len = (c.fft_size + c.max_ticks * fvad::kFrame + 3) & ~3;
   e->n_kernels = c.mode != FVAD_MODE_FUSED ? fvad::kStagedKernels : 2;
+  if (c.mode != FVAD_MODE_FUSED && c.use_denoiser) {
+    fvad::StagedArgs probe{};
+    probe.nfft_b = c.fft_size;
+    probe.n_channels = c.n_channels;
+    e->olafb = fvad::olafb_fused(probe);
+    if (e->olafb) e->n_kernels = fvad::kStagedKernels - 2;  // k_olafb's events span k_ola's pair
+  }
   e->n_events = c.mode != FVAD_MODE_FUSED ? fvad::kStagedEvents : 3;
   e->last_event = c.mode != FVAD_MODE_FUSED ? fvad::kStagedLast : 2;
   static_assert(fvad::kStagedEvents <= FVAD_MAX_TIMES, "timing events");
@@ -425,7 +433,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
       (rc = dalloc(&e->d_ratio_b[0], T * B)) ||
       (rc = dalloc(&e->d_vad, T * B)) || (rc = dalloc(&e->d_wratio, T * B)) || (rc = dalloc(&e->d_wvad, T * B)) ||
       (rc = dalloc(&e->d_wflag, T * B)) || (rc = dalloc(&e->d_band, T * B * C * c.n_bands)) ||
-      (rc = dalloc(&e->d_ticks_b[0], B)) || (c.want_denoised && (rc = dalloc(&e->d_den, frames))))
+      (rc = dalloc(&e->d_ticks_b[0], 2 * B)) || (c.want_denoised && (rc = dalloc(&e->d_den, frames))))
     return bail(rc);
   e->d_pcm = e->d_pcm_b[0];
   if (hipEventCreateWithFlags(&e->ev_in_free[0], hipEventDisableTiming) != hipSuccess ||
@@ -447,7 +455,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     const size_t F = B * e->V;
     if ((rc = dalloc(&e->d_xs_b[0], B * e->L)) || (rc = dalloc(&e->d_xs_b[1], B * e->L)) ||
         (rc = dalloc(&e->d_xlp_b[0], B * e->LX)) || (rc = dalloc(&e->d_xlp_b[1], B * e->LX)) ||
-        (rc = dalloc(&e->d_ratio_b[1], T * B)) || (rc = dalloc(&e->d_ticks_b[1], B)) || (rc = dalloc(&e->d_X, F * fvad::kFreq * 2)) ||
+        (rc = dalloc(&e->d_ratio_b[1], T * B)) || (rc = dalloc(&e->d_ticks_b[1], 2 * B)) || (rc = dalloc(&e->d_X, F * fvad::kFreq * 2)) ||
         (rc = dalloc(&e->d_P, F * fvad::kFreq * 2)) || (rc = dalloc(&e->d_Ex, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Ep, F * fvad::kBands)) || (rc = dalloc(&e->d_Exp, F * fvad::kBands)) ||
         (rc = dalloc(&e->d_Lyf, F * fvad::kBands)) || (rc = dalloc(&e->d_f34, F * 8)) ||
@@ -537,7 +545,7 @@ int launch_fused(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   return FVAD_OK;
 }
 
-int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
+int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bool timed) {
   const fvad_engine_config &c = e->cfg;
   fvad::StagedArgs a;
   a.n_streams = c.n_streams;
@@ -557,6 +565,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   e->d_wvad = e->wvad_b[b];
   e->d_band = e->band_b[b];
   a.ticks_valid = use_ticks ? e->d_ticks : nullptr;
+  a.tail = use_tail ? e->d_ticks + c.n_streams : nullptr;  // [B..2B) of the ticks buffer
   a.pcm = e->d_pcm;
   a.xs = e->d_xs;
   a.xlp = e->d_xlp_b[b];
@@ -660,10 +669,10 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   return FVAD_OK;
 }
 
-int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
+int launch(fvad_engine *e, int n_ticks, bool use_ticks, bool timed, bool use_tail = false) {
   if (!e->cfg.use_denoiser) timed = false;  // the no-denoiser pipeline records no kernel events
   const int rc = e->cfg.mode == FVAD_MODE_FUSED ? launch_fused(e, n_ticks, use_ticks, timed)
-                                                 : launch_staged(e, n_ticks, use_ticks, timed);
+                                                 : launch_staged(e, n_ticks, use_ticks, use_tail, timed);
   if (!rc && timed) e->slot_pending[e->ev_slot] = true;
   return rc;
 }
@@ -764,6 +773,31 @@ int check_ticks(const fvad_engine *e, const int32_t *ticks_valid, int n_ticks) {
   return FVAD_OK;
 }
 
+// last_tick_samples (nullable): real samples in each stream's last valid tick.
+// Only the no-denoiser path consumes a partial tick (it reads fft_size frames,
+// VAD.zig:206-220); with the denoiser a frame needs all 480 samples.  Fills
+// tt = [ticks_valid (n_ticks where NULL) | tails] when tails are in use.
+int tail_ticks(const fvad_engine *e, const int32_t *ticks_valid, const int32_t *last, int n_ticks,
+               std::vector<int32_t> &tt) {
+  tt.clear();
+  if (!last) return FVAD_OK;
+  const int B = e->cfg.n_streams;
+  bool partial = false;
+  for (int s = 0; s < B; s++) {
+    if (last[s] < 1 || last[s] > fvad::kFrame) return fail(FVAD_EINVAL, "last_tick_samples out of range [1, 480]");
+    partial |= last[s] != fvad::kFrame;
+  }
+  if (!partial) return FVAD_OK;
+  if (e->cfg.use_denoiser || e->cfg.mode == FVAD_MODE_FUSED)
+    return fail(FVAD_EINVAL, "a partial tick is only consumed with use_denoiser = 0 (VAD.zig:206-220)");
+  tt.resize(2 * (size_t)B);
+  for (int s = 0; s < B; s++) {
+    tt[s] = ticks_valid ? ticks_valid[s] : n_ticks;
+    tt[B + s] = last[s];
+  }
+  return FVAD_OK;
+}
+
 // host copy into a pinned slot, split over threads for large inputs
 void par_copy(void *dst, const void *src, size_t bytes) {
   constexpr size_t kChunk = 8u << 20;
@@ -796,7 +830,7 @@ int ensure_slots(fvad_engine *e) {
   };
   for (auto &sl : e->slots) {
     int rc;
-    if ((rc = host(&sl.in, frames)) || (rc = host(&sl.ticks, B)) || (rc = host(&sl.vad, TB)) ||
+    if ((rc = host(&sl.in, frames)) || (rc = host(&sl.ticks, 2 * B)) || (rc = host(&sl.vad, TB)) ||
         (rc = host(&sl.ratio, TB)) || (rc = host(&sl.wflag, TB)) || (rc = host(&sl.wratio, TB)) ||
         (rc = host(&sl.wvad, TB)) || (rc = host(&sl.band, TB * C * c.n_bands)) ||
         (c.want_denoised && (rc = host(&sl.den, frames))))
@@ -813,12 +847,19 @@ int ensure_slots(fvad_engine *e) {
 
 extern "C" int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
                                 fvad_outputs *out) {
+  return fvad_engine_push_ex(e, pcm, n_ticks, ticks_valid, nullptr, out);
+}
+
+extern "C" int fvad_engine_push_ex(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
+                                   const int32_t *last_tick_samples, fvad_outputs *out) {
   if (!e || !pcm) return fail(FVAD_EINVAL, "null argument");
   const fvad_engine_config &c = e->cfg;
   if (n_ticks < 0 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range [0, max_ticks]");
   if (n_ticks == 0) return FVAD_OK;
   int rc = check_ticks(e, ticks_valid, n_ticks);
   if (rc) return rc;
+  std::vector<int32_t> tt;
+  if ((rc = tail_ticks(e, ticks_valid, last_tick_samples, n_ticks, tt))) return rc;
   HIP_TRY(hipSetDevice(c.device));
   const size_t bytes = (size_t)n_ticks * c.n_streams * c.n_channels * fvad::kFrame * sizeof(float);
   // staged: the inputs go through the prep stream (ticks buffer b is free
@@ -833,9 +874,13 @@ extern "C" int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, c
   }
   if ((rc = input_buffer(e, cs))) return rc;
   HIP_TRY(hipMemcpyAsync(e->d_pcm, pcm, bytes, hipMemcpyHostToDevice, cs));
-  if (ticks_valid)
+  if (!tt.empty()) {  // ticks and tails, [2 * B] (synchronous copy: tt is a local)
+    HIP_TRY(hipMemcpyAsync(dticks, tt.data(), sizeof(int32_t) * tt.size(), hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
+  } else if (ticks_valid) {
     HIP_TRY(hipMemcpyAsync(dticks, ticks_valid, sizeof(int32_t) * c.n_streams, hipMemcpyHostToDevice, cs));
-  if ((rc = launch(e, n_ticks, ticks_valid != nullptr, false))) return rc;
+  }
+  if ((rc = launch(e, n_ticks, ticks_valid != nullptr || !tt.empty(), false, !tt.empty()))) return rc;
   if ((rc = release_input(e))) return rc;
   return fetch(e, n_ticks, out);
 }
@@ -858,11 +903,18 @@ extern "C" float *fvad_engine_input_slot(fvad_engine *e) {
 }
 
 extern "C" int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid) {
+  return fvad_engine_submit_ex(e, pcm, n_ticks, ticks_valid, nullptr);
+}
+
+extern "C" int fvad_engine_submit_ex(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
+                                     const int32_t *last_tick_samples) {
   if (!e || !pcm) return fail(FVAD_EINVAL, "null argument");
   const fvad_engine_config &c = e->cfg;
   if (n_ticks < 1 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range [1, max_ticks]");
   int rc = check_ticks(e, ticks_valid, n_ticks);
   if (rc) return rc;
+  std::vector<int32_t> tt;
+  if ((rc = tail_ticks(e, ticks_valid, last_tick_samples, n_ticks, tt))) return rc;
   HIP_TRY(hipSetDevice(c.device));
   if ((rc = ensure_slots(e))) return rc;
   const int si = e->sub_next;
@@ -874,7 +926,11 @@ extern "C" int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks,
     if (sl.h2d_busy) HIP_TRY(hipEventSynchronize(sl.h2d));
     par_copy(sl.in, pcm, bytes);
   }
-  if (ticks_valid) std::memcpy(sl.ticks, ticks_valid, B * sizeof(int32_t));
+  if (!tt.empty())
+    std::memcpy(sl.ticks, tt.data(), tt.size() * sizeof(int32_t));
+  else if (ticks_valid)
+    std::memcpy(sl.ticks, ticks_valid, B * sizeof(int32_t));
+  const bool use_ticks = ticks_valid != nullptr || !tt.empty();
   // staged: copies on the copy stream, overlapping the previous push's
   // kernels; the prep stream waits for them.  Fused: everything in order on
   // the engine stream (its kernels read d_ticks in place).
@@ -882,19 +938,19 @@ extern "C" int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks,
   hipStream_t cs = staged ? e->cstream : e->stream;
   if ((rc = input_buffer(e, cs))) return rc;
   HIP_TRY(hipMemcpyAsync(e->d_pcm, sl.in, bytes, hipMemcpyHostToDevice, cs));
-  if (ticks_valid) {
+  if (use_ticks) {
     int *dticks = e->d_ticks;
     if (staged) {
       const int b = e->next_buf;
       if (e->buf_busy[b]) HIP_TRY(hipStreamWaitEvent(cs, e->ev_buf_free[b], 0));
       dticks = e->d_ticks_b[b];
     }
-    HIP_TRY(hipMemcpyAsync(dticks, sl.ticks, B * sizeof(int32_t), hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(dticks, sl.ticks, (tt.empty() ? B : 2 * B) * sizeof(int32_t), hipMemcpyHostToDevice, cs));
   }
   HIP_TRY(hipEventRecord(sl.h2d, cs));
   sl.h2d_busy = true;
   if (staged) HIP_TRY(hipStreamWaitEvent(e->pstream, sl.h2d, 0));
-  if ((rc = launch(e, n_ticks, ticks_valid != nullptr, false))) return rc;
+  if ((rc = launch(e, n_ticks, use_ticks, false, !tt.empty()))) return rc;
   if ((rc = release_input(e))) return rc;
   // outputs into the slot's pinned buffers, after the kernels on the engine
   // stream (the next push's kernels queue behind these copies)
@@ -1072,6 +1128,7 @@ extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
   if (e->cfg.mode == FVAD_MODE_FUSED) return i == 0 ? "k_prep" : "k_frame";
   if (e->cfg.mode == FVAD_MODE_FP16 && i == 6) return "k_gru16";
+  if (e->olafb && i == 8) return "k_olafb";
   return fvad::staged_kernel_name(i);
 }
 

@@ -458,19 +458,31 @@ extern "C" int fvad_pipeline_push(fvad_pipeline *p, const float *const *pcm, siz
   if (p->rec_fn)
     for (int c = 0; c < C; c++) p->hist[c].insert(p->hist[c].end(), pcm[c], pcm[c] + n);
   p->total_write_count += n;
-  size_t avail = p->pending[0].size() / fvad::kFrame;
+  // with the denoiser the VAD loop takes whole 480-sample frames and keeps
+  // the rest for the next push (VAD.zig:219-220); without it every sample
+  // goes in at once (the engine counts samples and completes each fft_size
+  // window as soon as its last sample is in, VAD.zig:206-212), the last tick
+  // partial
+  const size_t have = p->pending[0].size();
+  const bool nd = !p->ec.use_denoiser;
+  size_t left = nd ? have : have / fvad::kFrame * fvad::kFrame;
   size_t consumed = 0;
-  std::vector<StreamMachines *> sm{&p->sm};
-  while (avail > 0) {
-    const int nt = (int)std::min<size_t>(avail, (size_t)p->ec.max_ticks);
+  while (left > 0) {
+    const size_t take = std::min<size_t>(left, (size_t)p->ec.max_ticks * fvad::kFrame);
+    const int nt = (int)((take + fvad::kFrame - 1) / fvad::kFrame);
+    const int32_t last = (int32_t)(take - (size_t)(nt - 1) * fvad::kFrame);
     for (int t = 0; t < nt; t++)
-      for (int c = 0; c < C; c++)
-        std::memcpy(&p->pcm[((size_t)t * C + c) * fvad::kFrame], &p->pending[c][consumed + (size_t)t * fvad::kFrame],
-                    fvad::kFrame * sizeof(float));
-    int rc = fvad_engine_push(p->engine, p->pcm.data(), nt, nullptr, nullptr);
+      for (int c = 0; c < C; c++) {
+        const size_t k = t + 1 < nt ? fvad::kFrame : (size_t)last;
+        float *dst = &p->pcm[((size_t)t * C + c) * fvad::kFrame];
+        std::memcpy(dst, &p->pending[c][consumed + (size_t)t * fvad::kFrame], k * sizeof(float));
+        if (k < (size_t)fvad::kFrame) std::memset(dst + k, 0, (fvad::kFrame - k) * sizeof(float));
+      }
+    int rc = last == fvad::kFrame ? fvad_engine_push(p->engine, p->pcm.data(), nt, nullptr, nullptr)
+                                  : fvad_engine_push_ex(p->engine, p->pcm.data(), nt, nullptr, &last, nullptr);
     if (rc) return rc;
-    consumed += (size_t)nt * fvad::kFrame;
-    avail -= nt;
+    consumed += take;
+    left -= take;
   }
   for (int c = 0; c < C; c++) p->pending[c].erase(p->pending[c].begin(), p->pending[c].begin() + consumed);
   return p->rec_fn ? record_segments(p) : FVAD_OK;
@@ -585,8 +597,12 @@ extern "C" int fvad_multi_run_stream(fvad_multi *m, fvad_read_fn read, void *ctx
       std::vector<float> tmp((size_t)C * cap);
       std::vector<float *> dst(C);
       for (int c = 0; c < C; c++) dst[c] = tmp.data() + (size_t)c * cap;
-      std::vector<int32_t> valid(B);
+      std::vector<int32_t> valid(B), last(B);
       std::vector<char> done(B, 0);
+      // no denoiser: a stream's final partial tick goes in too (its samples
+      // can complete an fft_size window, VAD.zig:206-220); with the denoiser a
+      // tail shorter than a frame is never processed (VAD.zig:219)
+      const bool nd = !p.ec.use_denoiser;
       int in_flight = 0, rc = FVAD_OK, live = B;
       while (live > 0 && !rc) {
         float *buf = fvad_engine_input_slot(p.engine);
@@ -595,11 +611,11 @@ extern "C" int fvad_multi_run_stream(fvad_multi *m, fvad_read_fn read, void *ctx
           break;
         }
         int nt = 0;
+        bool partial = false;
         for (int b = 0; b < B; b++) {
           valid[b] = 0;
+          last[b] = fvad::kFrame;
           if (done[b]) continue;
-          // whole ticks only; a tail shorter than a frame is never processed
-          // (VAD.zig:219: the loop needs frame_size unread samples)
           size_t got = 0;
           while (got < cap) {
             std::vector<float *> d(C);
@@ -613,15 +629,24 @@ extern "C" int fvad_multi_run_stream(fvad_multi *m, fvad_read_fn read, void *ctx
             live--;
           }
           valid[b] = (int)(got / fvad::kFrame);
+          if (nd && got % fvad::kFrame) {
+            last[b] = (int32_t)(got % fvad::kFrame);
+            valid[b]++;
+            partial = true;
+          }
           nt = std::max(nt, valid[b]);
           for (int t = 0; t < valid[b]; t++)
-            for (int c = 0; c < C; c++)
-              std::memcpy(&buf[(((size_t)t * B + b) * C + c) * fvad::kFrame], dst[c] + (size_t)t * fvad::kFrame,
-                          fvad::kFrame * sizeof(float));
+            for (int c = 0; c < C; c++) {
+              const size_t k = t + 1 < valid[b] ? fvad::kFrame : (size_t)last[b];
+              float *d = &buf[(((size_t)t * B + b) * C + c) * fvad::kFrame];
+              std::memcpy(d, dst[c] + (size_t)t * fvad::kFrame, k * sizeof(float));
+              if (k < (size_t)fvad::kFrame) std::memset(d + k, 0, (fvad::kFrame - k) * sizeof(float));
+            }
         }
         if (nt == 0) break;
         if (in_flight == 2 && !(rc = fvad_engine_collect(p.engine, nullptr, nullptr))) in_flight--;
-        if (!rc && !(rc = fvad_engine_submit(p.engine, buf, nt, valid.data()))) in_flight++;
+        if (!rc && !(rc = fvad_engine_submit_ex(p.engine, buf, nt, valid.data(), partial ? last.data() : nullptr)))
+          in_flight++;
       }
       while (in_flight > 0) {
         const int r2 = fvad_engine_collect(p.engine, nullptr, nullptr);

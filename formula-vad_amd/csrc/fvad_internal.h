@@ -35,6 +35,7 @@ constexpr int kMaxFactors = 32;
 // ---------------------------------------------------------------------------
 namespace st {
 constexpr int kPitch = 0;                       // pitch_buf[1728] (last 480 = analysis_mem source)
+constexpr int kNdSamples = kPitch;              // use_denoiser = 0 (no pitch buffer): u64 samples consumed
 constexpr int kSyn = kPitch + kPitchBuf;        // synthesis_mem[480]
 constexpr int kCepsMem = kSyn + kFrame;         // cepstral_mem[8][22]
 constexpr int kLastG = kCepsMem + kCeps * kBands;  // lastg[22]

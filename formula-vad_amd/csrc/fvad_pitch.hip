@@ -51,6 +51,12 @@ constexpr int kPcF = 8;                // frames per workgroup (a quarter tile h
 constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
 constexpr int kPcNT = kPcL * kPcF;
 static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
+#ifndef FVAD_Q1_B64
+#define FVAD_Q1_B64 0
+#endif
+#ifndef FVAD_Q3_B64
+#define FVAD_Q3_B64 0
+#endif
 constexpr int kPcXS = 870;  // xf row pitch: even (8-byte aligned pairs in Q5), = 6 mod 8 (conflict-free Q0 stores)
 constexpr int kPcSP = 153;  // coarse xcorr / Syy row pitch (odd; >= 147 rounded up to the scan block)
 
@@ -158,15 +164,27 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         const float *X = xf[fr] + (kPitchMax >> 1);
         const float *Y = xf[fr] + 2 * k0;
         float win[R];
+#if FVAD_Q1_B64
+        // y values as the low half of an 8-byte read: lanes 10 floats apart
+        // fall on distinct 64-bank pairs (ds_read_b64), where 4-byte reads
+        // (32-bank map) collide two to a bank
+        auto yld = [&](int m) -> float {
+          float2 p = *reinterpret_cast<const float2 *>(Y + 2 * m);
+          asm volatile("" : "+v"(p));
+          return p.x;
+        };
+#else
+        auto yld = [&](int m) -> float { return Y[2 * m]; };
+#endif
 #pragma unroll
-        for (int r = 0; r < R; r++) win[r] = Y[2 * r];
+        for (int r = 0; r < R; r++) win[r] = yld(r);
         for (int jb = 0; jb < 240; jb += R) {
 #pragma unroll
           for (int u = 0; u < R; u++) {
             const float xv = X[2 * (jb + u)];
 #pragma unroll
             for (int r = 0; r < R; r++) acc[r] = acc[r] + xv * win[(r + u) % R];
-            win[u] = Y[2 * (jb + u + R)];  // lag k0+R-1 at step jb+u+1
+            win[u] = yld(jb + u + R);  // lag k0+R-1 at step jb+u+1
           }
         }
 #pragma unroll
@@ -340,6 +358,49 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(2);
     // Q3
     if (walker) walk(kWalkQ2, kWalkQ3);
+#if FVAD_Q3_B64
+    // lanes by lag parity: wave 0 = the 6 even lags of each frame (u % 5 in
+    // {0, 2, 4}), wave 1 = the 4 odd ones, so each wave reads its y operands
+    // as aligned pairs (ds_read_b64) without per-lane parity selects; x is
+    // the frame's aligned pair row (broadcast to its lanes)
+    if (tq < 6 * kPcF || (tq >= 64 && tq < 64 + 4 * kPcF)) {
+      const bool odd = tq >= 64;
+      const int e = odd ? tq - 64 : tq, per = odd ? 4 : 6;
+      const int fr = e / per, k = e - per * fr;
+      // u: window (k / (per / 2)), position within the window by parity
+      const int win = k / (per / 2), kk = k - win * (per / 2);
+      const int u = 5 * win + (odd ? 1 + 2 * kk : 2 * kk);
+      const int bp0 = best[fr][0], bp1 = best[fr][1];
+      const int i = (u < 5 ? 2 * bp0 : 2 * bp1) - 2 + (u % 5);
+      const bool dup = u >= 5 && abs(i - 2 * bp0) <= 2;
+      if (i >= 0 && i < 294 && !dup) {
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        const v2f *xp = reinterpret_cast<const v2f *>(xf[fr] + (kPitchMax >> 1));
+        float sum = 0.0f;
+        if (!odd) {
+          const v2f *yp = reinterpret_cast<const v2f *>(xf[fr] + i);
+#pragma unroll 8
+          for (int j = 0; j < 240; j++) {
+            const v2f xv = xp[j], yv = yp[j];
+            sum = sum + xv.x * yv.x;
+            sum = sum + xv.y * yv.y;
+          }
+        } else {
+          // y[2j] = pair(i - 1 + 2j).y, y[2j + 1] = pair(i + 1 + 2j).x
+          const v2f *yp = reinterpret_cast<const v2f *>(xf[fr] + i - 1);
+          v2f prev = yp[0];
+#pragma unroll 8
+          for (int j = 0; j < 240; j++) {
+            const v2f xv = xp[j], nx = yp[j + 1];
+            sum = sum + xv.x * prev.y;
+            sum = sum + xv.y * nx.x;
+            prev = nx;
+          }
+        }
+        fine[fr][u] = (-1 > sum) ? -1 : sum;
+      }
+    }
+#else
     if (tq < 10 * kPcF) {
       const int fr = tq / 10, u = tq - 10 * fr;
       const int bp0 = best[fr][0], bp1 = best[fr][1];
@@ -351,6 +412,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         fine[fr][u] = (-1 > sum) ? -1 : sum;
       }
     }
+#endif
     __syncthreads();
     RSTAMP(3);
     // Q4

@@ -62,6 +62,7 @@ struct StagedArgs {
   int V;                   // frame-row stride per stream (= max_ticks * C)
   int L;                   // xs row length (= 1248 + V * 480)
   const int *ticks_valid;  // nullable
+  const int *tail;         // nullable: real samples (1..480) in each stream's last valid tick (use_denoiser = 0)
   const float *pcm;        // [t][s][c][480] normalised input
   float *xs;               // [s][L] high-passed s16-scale samples, 1248 history first
   float *xlp;              // [s][LX] pitch_downsample's x_lp over xs (x_lp[m] from xs[2m-1..2m+1]),
@@ -119,9 +120,12 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
 // k_pcorr over `tiles` pitch tiles (fvad_pitch.hip)
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream);
 const char *staged_kernel_name(int i);
+// true when launch_staged runs k_olafb in place of k_ola, k_winmeta, k_fftbw
+bool olafb_fused(const StagedArgs &a);
 // The wave-per-frame FFT kernels (fvad_wave.hip), persistent grids; kWaveFftB
-// needs fft_size 2048 (a 1024-point complex transform).
-enum WaveKernel { kWaveFftA, kWavePspec, kWaveSynth, kWaveFftB };
+// needs fft_size 2048 (a 1024-point complex transform); kWaveOlaFb (k_ola +
+// k_winmeta + k_fftbw fused) needs fft_size 2048 and n_channels <= 4.
+enum WaveKernel { kWaveFftA, kWavePspec, kWaveSynth, kWaveFftB, kWaveOlaFb };
 hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream);
 // Device VADMachines over the window outputs a.out_* of one push: overlap =
 // the light HBM variant meant to co-run with the next push on a side stream.

@@ -1643,11 +1643,23 @@ int resident_blocks(K kernel, int threads, int n_cu) {
 
 // ---------------------------------------------------------------------------
 // use_denoiser = false (VAD.zig:206-212,239-249): the pipeline reads fft_size
-// frames of raw input straight into FFT B; no rnnoise, no per-frame vad.
-// k_ndring: input ticks -> the stream's re-block ring (k_ola's float4 layout),
-// per-tick vad / ratio set to -1 (not produced by the reference on this path),
-// the raw input as the "denoised" output.
+// frames of raw input straight into FFT B; no rnnoise, no per-frame vad.  The
+// reference takes a window as soon as fft_size samples are in, whatever the
+// size of the pushes, so this path counts samples, not ticks: a stream's last
+// valid tick may hold only a.tail[s] real samples (the end of a stream, or the
+// remainder of an AudioPipeline push), and st::kNdSamples (u64) is the
+// stream's absolute sample count.
+// k_ndring: the real input samples -> the stream's re-block ring, per-tick vad
+// / ratio set to -1 (not produced by the reference on this path), the raw
+// input as the "denoised" output.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int nd_real(const StagedArgs &a, int s, int t, int nt) {
+  return (a.tail && t == nt - 1) ? a.tail[s] : kFrame;
+}
+__device__ __forceinline__ unsigned long long *nd_count(const StagedArgs &a, int s) {
+  return reinterpret_cast<unsigned long long *>(a.state + (size_t)s * st::kWords + st::kNdSamples);
+}
+
 __global__ void __launch_bounds__(256) k_ndring(StagedArgs a) {
   const int C = a.n_channels, V = a.V;
   const int q = threadIdx.x & 127;
@@ -1657,13 +1669,15 @@ __global__ void __launch_bounds__(256) k_ndring(StagedArgs a) {
   const int nt = ticks_of(a, s);
   if (v >= nt * C) return;
   const int t = v / C, c = v - t * C, i = 4 * q;
-  const float *stp = a.state + (size_t)s * st::kWords;
   const size_t o = (size_t)t * a.n_streams + s;
   const float4 x = *reinterpret_cast<const float4 *>(a.pcm + (o * C + c) * kFrame + i);
-  const int frames_done = reinterpret_cast<const int *>(stp)[st::kFramesDone];
-  long long ri = (long long)(frames_done + t) * kFrame % a.ring_len + i;
-  if (ri >= a.ring_len) ri -= a.ring_len;
-  *reinterpret_cast<float4 *>(a.ring + ((size_t)s * C + c) * a.ring_len + ri) = x;
+  const int n = nd_real(a, s, t, nt);
+  const unsigned long long p0 = *nd_count(a, s) + (unsigned long long)t * kFrame + i;
+  float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
+  const float xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int e = 0; e < 4; e++)
+    if (i + e < n) ring[(p0 + e) % (unsigned long long)a.ring_len] = xv[e];
   if (a.out_den) *reinterpret_cast<float4 *>(a.out_den + (o * C + c) * kFrame + i) = x;
   if (i == 0 && c == 0) {
     a.out_vad[o] = -1.0f;
@@ -1671,10 +1685,11 @@ __global__ void __launch_bounds__(256) k_ndring(StagedArgs a) {
   }
 }
 
-// k_ndmeta: window completion per tick (the k_winmeta rule); a completed
-// window's volume ratio is preAnalyzeSegment over its fft_size input samples
-// (VAD.zig:253-272: rmsVolume per channel = sqrt(sum x^2 / n), the sum in
-// sample order; min / max over channels); lane per stream.
+// k_ndmeta: window completion per tick (a window completes in the tick that
+// brings its last sample); a completed window's volume ratio is
+// preAnalyzeSegment over its fft_size input samples (VAD.zig:253-272:
+// rmsVolume per channel = sqrt(sum x^2 / n), the sum in sample order; min /
+// max over channels); lane per stream.
 __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
   const int s = blockIdx.x * 64 + threadIdx.x;
   if (s >= a.n_streams) return;
@@ -1683,20 +1698,20 @@ __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
   long long *wsx = a.win_start + (size_t)s * a.wmax;
   int j = 0;
   if (nt > 0) {
-    int *istp = reinterpret_cast<int *>(a.state + (size_t)s * st::kWords);
-    int fd = istp[st::kFramesDone];
+    unsigned long long *cnt = nd_count(a, s);
+    const unsigned long long sd0 = *cnt;
     for (int t = 0; t < nt; t++) {
       const size_t o = (size_t)t * a.n_streams + s;
-      const long long a0 = (long long)fd * kFrame;
-      const long long wdone = a0 / FB;
-      const long long next_end = (wdone + 1) * FB;
-      const bool complete = a0 + kFrame >= next_end;
+      const unsigned long long a0 = sd0 + (unsigned long long)t * kFrame;
+      const unsigned long long wdone = a0 / (unsigned)FB;
+      const unsigned long long next_end = (wdone + 1) * (unsigned)FB;
+      const bool complete = a0 + (unsigned)nd_real(a, s, t, nt) >= next_end;
       if (complete) {
-        const long long ws = wdone * FB;
+        const unsigned long long ws = wdone * (unsigned)FB;
         float vol_min = 1, vol_max = 0;
         for (int c = 0; c < C; c++) {
           const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
-          long long ri = ws % a.ring_len;
+          long long ri = (long long)(ws % (unsigned long long)a.ring_len);
           float sum = 0.0f;
           for (int n = 0; n < FB; n++) {
             const float x = ring[ri];
@@ -1710,7 +1725,7 @@ __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
         a.out_win_ratio[o] = vol_max == 0 ? 0.0f : vol_min / vol_max;
         a.out_win_vad[o] = -1.0f;
         wt[j] = t;
-        wsx[j] = ws;
+        wsx[j] = (long long)ws;
         j++;
       } else {
         a.out_win_ratio[o] = 0.0f;
@@ -1718,9 +1733,8 @@ __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
         for (int i = 0; i < C * a.n_bands; i++) a.out_band[o * C * a.n_bands + i] = 0.0f;
       }
       a.out_win_flag[o] = complete ? 1 : 0;
-      fd++;
     }
-    istp[st::kFramesDone] = fd;
+    *cnt = sd0 + (unsigned long long)(nt - 1) * kFrame + (unsigned)nd_real(a, s, nt - 1, nt);
   }
   for (; j < a.wmax; j++) wt[j] = -1;
 }
@@ -1762,6 +1776,16 @@ hipError_t launch_fftb(const StagedArgs &a, int n_cu, hipStream_t stream) {
   (void)attr;
   FVAD_KERNEL_TRY(k_fftb<256>, dim3(a.n_streams * a.wmax), dim3(256), fftb_lds_bytes(a), stream, a);
   return hipSuccess;
+}
+
+// the fused synthesis tail (k_olafb) serves fft_size 2048 with <= 4 channels;
+// FVAD_OLAFB=0 selects k_ola + k_winmeta + k_fftbw (A/B)
+bool olafb_fused(const StagedArgs &a) {
+  static const bool off = [] {
+    const char *v = getenv("FVAD_OLAFB");
+    return v && atoi(v) == 0;
+  }();
+  return !off && a.nfft_b == 2048 && a.n_channels <= 4;
 }
 
 hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) {
@@ -1813,12 +1837,21 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   REC(9);
   FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
   REC(10);
-  FVAD_KERNEL_TRY(k_ola, dim3((unsigned)((frames + 1) / 2)), dim3(256), 0, stream, a);
-  REC(11);
-  FVAD_KERNEL_TRY(k_winmeta, dim3((a.n_streams + kWmS - 1) / kWmS), dim3(64), 0, stream, a);
-  REC(12);
-  FVAD_LAUNCH_TRY(launch_fftb(a, n_cu, stream));
-  REC(13);
+  if (olafb_fused(a)) {
+    // overlap-add, window bookkeeping and FFT B in one kernel (k_olafb);
+    // the k_winmeta / k_fftbw events bracket nothing
+    FVAD_LAUNCH_TRY(launch_wave(kWaveOlaFb, a, n_cu, stream));
+    REC(11);
+    REC(12);
+    REC(13);
+  } else {
+    FVAD_KERNEL_TRY(k_ola, dim3((unsigned)((frames + 1) / 2)), dim3(256), 0, stream, a);
+    REC(11);
+    FVAD_KERNEL_TRY(k_winmeta, dim3((a.n_streams + kWmS - 1) / kWmS), dim3(64), 0, stream, a);
+    REC(12);
+    FVAD_LAUNCH_TRY(launch_fftb(a, n_cu, stream));
+    REC(13);
+  }
 #undef REC
   return hipSuccess;
 }

@@ -381,34 +381,163 @@ struct FbTabs {
   float2 t5[4][3][64];  // stage 5: [d3][r][lane]: twb[(r + 1) (lane + 64 d3)]
 };
 
+// Per-workgroup stage-4/5 twiddle tables; stage-2/3 twiddles come per
+// transform from the plan (FbTw, cached loads) so they do not hold registers
+// between transforms.
+struct FbTw {
+  float2 s2[4][3], s3[3], tw0;
+};
+__device__ __forceinline__ void fftb_tabs_load(FbTabs &tb, const Plan *__restrict__ P, int tid, int nt) {
+  const float2 *__restrict__ twb = reinterpret_cast<const float2 *>(P->twb);
+  for (int i = tid; i < 4 * 3 * 16; i += nt) {
+    const int d2 = i / 48, r = (i / 16) % 3, u = i % 16;
+    tb.t4[d2][r][u] = twb[4 * (r + 1) * (u + 16 * d2)];
+  }
+  for (int i = tid; i < 4 * 3 * 64; i += nt) {
+    const int d3 = i / 192, r = (i / 64) % 3, l = i % 64;
+    tb.t5[d3][r][l] = twb[(r + 1) * (l + 64 * d3)];
+  }
+}
+__device__ __forceinline__ void fftb_tw_load(FbTw &w, const Plan *__restrict__ P, int lane) {
+  // opaque offset: the loads stay at the transform instead of being hoisted
+  const float2 *__restrict__ twb = reinterpret_cast<const float2 *>(P->twb) + opaque0();
+#pragma unroll
+  for (int d0 = 0; d0 < 4; d0++)
+#pragma unroll
+    for (int r = 0; r < 3; r++) w.s2[d0][r] = twb[64 * (r + 1) * d0];
+#pragma unroll
+  for (int r = 0; r < 3; r++) w.s3[r] = twb[16 * (r + 1) * (lane >> 2)];
+  w.tw0 = twb[0];
+}
+
+// FFT B of one windowed 2048-sample frame given in layout X (register r of
+// lane l = packed input k = l + 64 r), then kiss_fftr's split for the
+// reported bins, magnitudes and the band sums in bin order; lane b < n_bands
+// returns band b's sum.  R: the wave's exchange region (kFbSlots float2; the
+// caller's input may live there until v is loaded); mag: kFbMag floats.
+__device__ __forceinline__ float fftb_bands(float2 (&v)[16], float2 *R, float *mag, const FbTabs &tb,
+                                            const StagedArgs &a, int lane) {
+  const Plan *__restrict__ P = a.plan;
+  FbTw w;
+  fftb_tw_load(w, P, lane);
+  const float2 *__restrict__ sup = reinterpret_cast<const float2 *>(P->superb);
+  const int nb = a.n_bands, lo = a.bin_lo_all, hi = a.bin_hi_all;
+  // stage 1 (m = 1, over d0), stage 2 (m = 4, over d1, u = d0)
+#pragma unroll
+  for (int d1 = 0; d1 < 4; d1++) {
+    float2 F[4] = {v[d1], v[d1 + 4], v[d1 + 8], v[d1 + 12]};
+    bfly4(F, 1, w.tw0, w.tw0, w.tw0);
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[d1 + 4 * u] = F[u];
+  }
+#pragma unroll
+  for (int d0 = 0; d0 < 4; d0++) {
+    float2 F[4] = {v[4 * d0], v[4 * d0 + 1], v[4 * d0 + 2], v[4 * d0 + 3]};
+    bfly4(F, 1, w.s2[d0][0], w.s2[d0][1], w.s2[d0][2]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[4 * d0 + u] = F[u];
+  }
+  // X -> Y
+  wfft::wsync();
+  {
+    float2 *wr = R + (lane & 3) + 260 * ((lane >> 2) & 3) + 64 * (lane >> 4);  // + 4 d0 + 16 d1
+#pragma unroll
+    for (int r = 0; r < 16; r++) wr[4 * (r >> 2) + 16 * (r & 3)] = v[r];
+  }
+  wfft::wsync();
+  {
+    const float2 *rd = R + lane;  // + 64 d2 + 260 d3
+#pragma unroll
+    for (int r = 0; r < 16; r++) v[r] = rd[64 * (r & 3) + 260 * (r >> 2)];
+  }
+  // stage 3 (m = 16, over d2, u = lane >> 2), stage 4 (m = 64, over d3, u = (lane >> 2) + 16 d2)
+#pragma unroll
+  for (int d3 = 0; d3 < 4; d3++) {
+    float2 F[4] = {v[4 * d3], v[4 * d3 + 1], v[4 * d3 + 2], v[4 * d3 + 3]};
+    bfly4(F, 1, w.s3[0], w.s3[1], w.s3[2]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[4 * d3 + u] = F[u];
+  }
+#pragma unroll
+  for (int d2 = 0; d2 < 4; d2++) {
+    float2 F[4] = {v[d2], v[d2 + 4], v[d2 + 8], v[d2 + 12]};
+    const int u16 = lane >> 2;
+    bfly4(F, 1, tb.t4[d2][0][u16], tb.t4[d2][1][u16], tb.t4[d2][2][u16]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[d2 + 4 * u] = F[u];
+  }
+  wfft::wsync();
+  // Y -> Z
+  {
+    float2 *wr = R + (lane >> 2) + 260 * (lane & 3);  // + 16 d2 + 64 d3
+#pragma unroll
+    for (int r = 0; r < 16; r++) wr[16 * (r & 3) + 64 * (r >> 2)] = v[r];
+  }
+  wfft::wsync();
+  {
+    const float2 *rd = R + lane;  // + 64 d3 + 260 d4
+#pragma unroll
+    for (int r = 0; r < 16; r++) v[r] = rd[64 * (r & 3) + 260 * (r >> 2)];
+  }
+  // stage 5 (m = 256, over d4, u = lane + 64 d3)
+#pragma unroll
+  for (int d3 = 0; d3 < 4; d3++) {
+    float2 F[4] = {v[d3], v[d3 + 4], v[d3 + 8], v[d3 + 12]};
+    bfly4(F, 1, tb.t5[d3][0][lane], tb.t5[d3][1][lane], tb.t5[d3][2][lane]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[d3 + 4 * u] = F[u];
+  }
+  wfft::wsync();
+  // natural order into the region (bins 64 r + lane), then kiss_fftr's
+  // split for the bins the bands use, magnitudes, band sums in bin order
+#pragma unroll
+  for (int r = 0; r < 16; r++) R[64 * r + lane] = v[r];
+  wfft::wsync();
+  const int nc = 1024;
+  for (int k = lo + lane; k <= hi; k += 64) {
+    float re, imv;
+    if (k == 0) {
+      re = R[0].x + R[0].y;
+      imv = 0;
+    } else if (k == nc) {
+      re = R[0].x - R[0].y;
+      imv = 0;
+    } else {
+      const int kk = (k < nc / 2) ? k : nc - k;
+      const float2 fpk = R[kk];
+      const float2 fpnk = make_float2(R[nc - kk].x, -R[nc - kk].y);
+      const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
+      const float2 tw2 = cmul(f2k, sup[kk - 1]);
+      if (k < nc / 2) {
+        re = (f1k.x + tw2.x) * ((float).5);
+        imv = (f1k.y + tw2.y) * ((float).5);
+      } else {
+        re = (f1k.x - tw2.x) * ((float).5);
+        imv = (tw2.y - f1k.y) * ((float).5);
+      }
+    }
+    const float r2 = re * re, i2 = imv * imv;
+    mag[k - lo] = sqrtf(r2 + i2) * P->norm_b;
+  }
+  wfft::wsync();
+  float acc = 0.0f;
+  if (lane < nb)
+    for (int k = a.band_lo[lane]; k <= a.band_hi[lane]; k++) acc += mag[k - lo];
+  wfft::wsync();
+  return acc;
+}
+
 __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftbw(StagedArgs a) {
   __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][kFbSlots];
   __shared__ float mg[kWNW][kFbMag];
   __shared__ FbTabs tb;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const Plan *__restrict__ P = a.plan;
-  const float2 *__restrict__ twb = reinterpret_cast<const float2 *>(P->twb);
-  const float2 *__restrict__ sup = reinterpret_cast<const float2 *>(P->superb);
-  for (int i = tid; i < 4 * 3 * 16; i += 64 * kWNW) {
-    const int d2 = i / 48, r = (i / 16) % 3, u = i % 16;
-    tb.t4[d2][r][u] = twb[4 * (r + 1) * (u + 16 * d2)];
-  }
-  for (int i = tid; i < 4 * 3 * 64; i += 64 * kWNW) {
-    const int d3 = i / 192, r = (i / 64) % 3, l = i % 64;
-    tb.t5[d3][r][l] = twb[(r + 1) * (l + 64 * d3)];
-  }
-  float2 s2[4][3], s3[3];
-#pragma unroll
-  for (int d0 = 0; d0 < 4; d0++)
-#pragma unroll
-    for (int r = 0; r < 3; r++) s2[d0][r] = twb[64 * (r + 1) * d0];
-#pragma unroll
-  for (int r = 0; r < 3; r++) s3[r] = twb[16 * (r + 1) * (lane >> 2)];
-  const float2 tw0 = twb[0];
+  fftb_tabs_load(tb, P, tid, 64 * kWNW);
   __syncthreads();
   float2 *R = Rg[wv];
   float *mag = mg[wv];
-  const int C = a.n_channels, nb = a.n_bands, lo = a.bin_lo_all, hi = a.bin_hi_all;
+  const int C = a.n_channels, nb = a.n_bands;
   const long long items = (long long)a.n_streams * a.wmax * C;
   // static assignment: most (stream, slot) items are empty slots, and a queue
   // atomic per item costs more than the skip
@@ -437,109 +566,193 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftbw(StagedArgs a) {
       const float t1 = ring[i1] * P->hannb[2 * k + 1];
       v[r] = make_float2(t0, t1);
     }
-    // stage 1 (m = 1, over d0), stage 2 (m = 4, over d1, u = d0)
-#pragma unroll
-    for (int d1 = 0; d1 < 4; d1++) {
-      float2 F[4] = {v[d1], v[d1 + 4], v[d1 + 8], v[d1 + 12]};
-      bfly4(F, 1, tw0, tw0, tw0);
-#pragma unroll
-      for (int u = 0; u < 4; u++) v[d1 + 4 * u] = F[u];
+    const float band = fftb_bands(v, R, mag, tb, a, lane);
+    if (lane < nb) a.out_band[(((size_t)t * a.n_streams + s) * C + c) * nb + lane] = band;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_olafb (fft_size 2048, C <= 4): k_ola + k_winmeta + k_fftbw in one kernel
+// (BASELINE configs[4]'s fusion of the synthesis tail: overlap-add ->
+// 480 -> 2048 re-block -> FFT B -> band sums, VAD.zig:298-348,
+// PipelineFFT.zig:88-112).  A workgroup takes 4 / C streams, wave = (stream,
+// channel).  The wave walks its channel's ticks: overlap-add of the ys rows
+// (the next tick's rows load during this tick), the denoised samples go
+// straight into the wave's LDS window (the current FFT-B window, VAD.zig's
+// fft_input_buffer), and when a tick completes the window the wave runs FFT B
+// on it in place (fftb_bands) -- the re-block ring in HBM only carries the
+// partial window from one push to the next (<= 2047 samples per channel
+// instead of every sample written and read back).  The window bookkeeping of
+// k_winmeta (completion, share-weighted volume ratio, window vad) runs on
+// every wave of the stream identically; channel 0 writes it.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_olafb(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][kFbSlots];  // window samples, then the FFT exchanges
+  __shared__ float mg[kWNW][kFbMag];
+  __shared__ float ovg[kWNW][kFrame];  // a completing tick's samples past the window
+  __shared__ FbTabs tb;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const Plan *__restrict__ P = a.plan;
+  fftb_tabs_load(tb, P, tid, 64 * kWNW);
+  __syncthreads();
+  constexpr int FB = 2048;
+  float *ov = ovg[wv];
+  static_assert(kFbSlots * 2 >= FB, "window fits the exchange region");
+  float2 *R = Rg[wv];
+  float *W = reinterpret_cast<float *>(R);
+  float *mag = mg[wv];
+  const int C = a.n_channels, nb = a.n_bands, B = a.n_streams, V = a.V;
+  const int G = kWNW / C;  // streams per workgroup item
+  const int sw = wv / C, c = wv - sw * C;
+  const float kInv = a.raw_s16 ? 1.0f : 1.0f / (float)32767;
+  const int rl = a.ring_len;
+  for (int sb = blockIdx.x * G; sb < B; sb += gridDim.x * G) {
+    const int s = sb + sw;
+    const bool on = sw < G && s < B;
+    const int nt = on ? ticks_of(a, s) : 0;
+    float *stp = a.state + (size_t)(on ? s : 0) * st::kWords;
+    int fd0 = 0;
+    float vol = 0;
+    if (nt > 0) {
+      fd0 = reinterpret_cast<const int *>(stp)[st::kFramesDone];
+      vol = stp[st::kVolAcc];
     }
-#pragma unroll
-    for (int d0 = 0; d0 < 4; d0++) {
-      float2 F[4] = {v[4 * d0], v[4 * d0 + 1], v[4 * d0 + 2], v[4 * d0 + 3]};
-      bfly4(F, 1, s2[d0][0], s2[d0][1], s2[d0][2]);
-#pragma unroll
-      for (int u = 0; u < 4; u++) v[4 * d0 + u] = F[u];
+    // the partial window carried from the previous push: samples [ws, fd0 * 480)
+    long long ws = (long long)fd0 * kFrame / FB * FB;
+    const float *ring = a.ring + ((size_t)(on ? s : 0) * C + c) * rl;
+    if (nt > 0) {
+      const int ncarry = (int)((long long)fd0 * kFrame - ws);
+      const int r0 = (int)(ws % rl);
+      for (int i = lane; i < ncarry; i += 64) {
+        int ri = r0 + i;
+        ri -= ri >= rl ? rl : 0;
+        W[i] = ring[ri];
+      }
     }
-    // X -> Y
-    {
-      float2 *w = R + (lane & 3) + 260 * ((lane >> 2) & 3) + 64 * (lane >> 4);  // + 4 d0 + 16 d1
+    // the stream's synthesis memory is read (tick 0, channel 0) before the
+    // last channel's wave replaces it
+    __syncthreads();
+    if (nt > 0) {
+      const float *ysr = a.ys + (size_t)s * V * kWin;
+      // lane l < 60 owns samples 8 l .. 8 l + 7 of each tick
+      const bool sl = lane < 60;
+      const int q = 8 * lane;
+      auto load = [&](int t, float4 (&cur)[2], float4 (&prv)[2]) {
+        const int v = t * C + c;
+        const float *cp = ysr + (size_t)v * kWin + q;
+        const float *pp = v == 0 ? stp + st::kSyn + q : ysr + (size_t)(v - 1) * kWin + kFrame + q;
+        if (sl) {
+          cur[0] = *reinterpret_cast<const float4 *>(cp);
+          cur[1] = *reinterpret_cast<const float4 *>(cp + 4);
+          prv[0] = *reinterpret_cast<const float4 *>(pp);
+          prv[1] = *reinterpret_cast<const float4 *>(pp + 4);
+        }
+      };
+      float4 cn[2] = {}, pn[2] = {};
+      load(0, cn, pn);
+      for (int t = 0; t < nt; t++) {
+        float4 cur[2] = {cn[0], cn[1]}, prv[2] = {pn[0], pn[1]};
+        const long long p0 = (long long)(fd0 + t) * kFrame;
+        const int off = (int)(p0 - ws);  // window position of the tick's first sample
+        const bool complete = off + kFrame >= FB;
+        // the next tick's rows load now, or after this tick's FFT B (the
+        // transform needs the registers)
+        if (!complete && t + 1 < nt) load(t + 1, cn, pn);
+        float o[8];
+        o[0] = (cur[0].x + prv[0].x) * kInv;
+        o[1] = (cur[0].y + prv[0].y) * kInv;
+        o[2] = (cur[0].z + prv[0].z) * kInv;
+        o[3] = (cur[0].w + prv[0].w) * kInv;
+        o[4] = (cur[1].x + prv[1].x) * kInv;
+        o[5] = (cur[1].y + prv[1].y) * kInv;
+        o[6] = (cur[1].z + prv[1].z) * kInv;
+        o[7] = (cur[1].w + prv[1].w) * kInv;
+        const size_t ot = (size_t)t * B + s;
+        if (a.out_den && sl) {
+          float4 *dp = reinterpret_cast<float4 *>(a.out_den + (ot * C + c) * kFrame + q);
+          dp[0] = make_float4(o[0], o[1], o[2], o[3]);
+          dp[1] = make_float4(o[4], o[5], o[6], o[7]);
+        }
+        // samples inside the current window
+        if (sl) {
 #pragma unroll
-      for (int r = 0; r < 16; r++) w[4 * (r >> 2) + 16 * (r & 3)] = v[r];
-    }
-    wfft::wsync();
-    {
-      const float2 *rd = R + lane;  // + 64 d2 + 260 d3
+          for (int e = 0; e < 8; e++)
+            if (off + q + e < FB) W[off + q + e] = o[e];
+        }
+        // vad_low (VAD.zig:284-293) and the window bookkeeping (VAD.zig:298-348)
+        float vad_low = 1;
+        for (int cc = 0; cc < C; cc++) {
+          const float vv = a.vadf[(size_t)s * V + t * C + cc];
+          if (vv < vad_low) vad_low = vv;
+        }
+        const float ratio = a.ratio[ot];
+        if (complete) {
+          const int r = FB - off;
+          vol += ratio * ((float)r / (float)FB);
+          if (c == 0 && lane == 0) {
+            a.out_win_ratio[ot] = vol;
+            a.out_win_vad[ot] = vad_low;
+          }
+          vol = 0;
+          if (kFrame - r > 0) vol += ratio * ((float)(kFrame - r) / (float)FB);
+          // the tick's samples past the window wait in ov during FFT B
+          if (sl) {
 #pragma unroll
-      for (int r = 0; r < 16; r++) v[r] = rd[64 * (r & 3) + 260 * (r >> 2)];
-    }
-    // stage 3 (m = 16, over d2, u = lane >> 2), stage 4 (m = 64, over d3, u = (lane >> 2) + 16 d2)
+            for (int e = 0; e < 8; e++)
+              if (off + q + e >= FB) ov[off + q + e - FB] = o[e];
+          }
+          // FFT B of the completed window, in place
+          wfft::wsync();
+          float2 v[16];
 #pragma unroll
-    for (int d3 = 0; d3 < 4; d3++) {
-      float2 F[4] = {v[4 * d3], v[4 * d3 + 1], v[4 * d3 + 2], v[4 * d3 + 3]};
-      bfly4(F, 1, s3[0], s3[1], s3[2]);
-#pragma unroll
-      for (int u = 0; u < 4; u++) v[4 * d3 + u] = F[u];
-    }
-#pragma unroll
-    for (int d2 = 0; d2 < 4; d2++) {
-      float2 F[4] = {v[d2], v[d2 + 4], v[d2 + 8], v[d2 + 12]};
-      const int u16 = lane >> 2;
-      bfly4(F, 1, tb.t4[d2][0][u16], tb.t4[d2][1][u16], tb.t4[d2][2][u16]);
-#pragma unroll
-      for (int u = 0; u < 4; u++) v[d2 + 4 * u] = F[u];
-    }
-    wfft::wsync();
-    // Y -> Z
-    {
-      float2 *w = R + (lane >> 2) + 260 * (lane & 3);  // + 16 d2 + 64 d3
-#pragma unroll
-      for (int r = 0; r < 16; r++) w[16 * (r & 3) + 64 * (r >> 2)] = v[r];
-    }
-    wfft::wsync();
-    {
-      const float2 *rd = R + lane;  // + 64 d3 + 260 d4
-#pragma unroll
-      for (int r = 0; r < 16; r++) v[r] = rd[64 * (r & 3) + 260 * (r >> 2)];
-    }
-    // stage 5 (m = 256, over d4, u = lane + 64 d3)
-#pragma unroll
-    for (int d3 = 0; d3 < 4; d3++) {
-      float2 F[4] = {v[d3], v[d3 + 4], v[d3 + 8], v[d3 + 12]};
-      bfly4(F, 1, tb.t5[d3][0][lane], tb.t5[d3][1][lane], tb.t5[d3][2][lane]);
-#pragma unroll
-      for (int u = 0; u < 4; u++) v[d3 + 4 * u] = F[u];
-    }
-    wfft::wsync();
-    // natural order into the region (bins 64 r + lane), then kiss_fftr's
-    // split for the bins the bands use, magnitudes, band sums in bin order
-#pragma unroll
-    for (int r = 0; r < 16; r++) R[64 * r + lane] = v[r];
-    wfft::wsync();
-    const int nc = 1024;
-    for (int k = lo + lane; k <= hi; k += 64) {
-      float re, imv;
-      if (k == 0) {
-        re = R[0].x + R[0].y;
-        imv = 0;
-      } else if (k == nc) {
-        re = R[0].x - R[0].y;
-        imv = 0;
-      } else {
-        const int kk = (k < nc / 2) ? k : nc - k;
-        const float2 fpk = R[kk];
-        const float2 fpnk = make_float2(R[nc - kk].x, -R[nc - kk].y);
-        const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
-        const float2 tw2 = cmul(f2k, sup[kk - 1]);
-        if (k < nc / 2) {
-          re = (f1k.x + tw2.x) * ((float).5);
-          imv = (f1k.y + tw2.y) * ((float).5);
+          for (int rr = 0; rr < 16; rr++) {
+            const int k = lane + 64 * rr;
+            const float2 x = *reinterpret_cast<const float2 *>(W + 2 * k);
+            v[rr] = make_float2(x.x * P->hannb[2 * k], x.y * P->hannb[2 * k + 1]);
+          }
+          const float band = fftb_bands(v, R, mag, tb, a, lane);
+          if (lane < nb) a.out_band[(ot * C + c) * nb + lane] = band;
+          // they start the next window
+          for (int i = lane; i < off + kFrame - FB; i += 64) W[i] = ov[i];
+          ws += FB;
+          if (t + 1 < nt) load(t + 1, cn, pn);
         } else {
-          re = (f1k.x - tw2.x) * ((float).5);
-          imv = (tw2.y - f1k.y) * ((float).5);
+          vol += ratio * ((float)kFrame / (float)FB);
+          if (c == 0 && lane == 0) {
+            a.out_win_ratio[ot] = 0.0f;
+            a.out_win_vad[ot] = 0.0f;
+          }
+          if (lane < nb) a.out_band[(ot * C + c) * nb + lane] = 0.0f;
+        }
+        if (c == 0 && lane == 0) {
+          a.out_vad[ot] = vad_low;
+          a.out_win_flag[ot] = complete ? 1 : 0;
         }
       }
-      const float r2 = re * re, i2 = imv * imv;
-      mag[k - lo] = sqrtf(r2 + i2) * P->norm_b;
+      // the partial window goes back to the ring for the next push
+      wfft::wsync();
+      const int ncarry = (int)((long long)(fd0 + nt) * kFrame - ws);
+      const int r0 = (int)(ws % rl);
+      float *rw = a.ring + ((size_t)s * C + c) * rl;
+      for (int i = lane; i < ncarry; i += 64) {
+        int ri = r0 + i;
+        ri -= ri >= rl ? rl : 0;
+        rw[ri] = W[i];
+      }
     }
-    wfft::wsync();
-    if (lane < nb) {
-      float acc = 0.0f;
-      for (int k = a.band_lo[lane]; k <= a.band_hi[lane]; k++) acc += mag[k - lo];
-      a.out_band[(((size_t)t * a.n_streams + s) * C + c) * nb + lane] = acc;
+    __syncthreads();  // every wave of the stream has read its state
+    if (nt > 0) {
+      if (c == 0 && lane == 0) {
+        reinterpret_cast<int *>(stp)[st::kFramesDone] = fd0 + nt;
+        stp[st::kVolAcc] = vol;
+      }
+      if (c == C - 1) {  // synthesis memory = second half of the stream's last frame
+        const float4 *yl =
+            reinterpret_cast<const float4 *>(a.ys + ((size_t)s * V + (size_t)nt * C - 1) * kWin + kFrame);
+        float4 *dst = reinterpret_cast<float4 *>(stp + st::kSyn);
+        for (int i = lane; i < kFrame / 4; i += 64) dst[i] = yl[i];
+      }
     }
-    wfft::wsync();
   }
 }
 
@@ -558,6 +771,13 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
   static const int g_pspec = wave_resident_blocks(k_pspecw, n_cu);
   static const int g_synth = wave_resident_blocks(k_synthw, n_cu);
   static const int g_fftb = wave_resident_blocks(k_fftbw, n_cu);
+  static const int g_olafb = wave_resident_blocks(k_olafb, n_cu);
+  if (which == kWaveOlaFb) {
+    const int G = kWNW / a.n_channels;
+    hipLaunchKernelGGL(k_olafb, dim3((unsigned)std::min<long long>((a.n_streams + G - 1) / G, g_olafb)), dim3(64 * kWNW),
+                       0, stream, a);
+    return hipGetLastError();
+  }
   if (which == kWaveFftB) {
     const long long items = (long long)a.n_streams * a.wmax * a.n_channels;
     hipLaunchKernelGGL(k_fftbw, dim3((unsigned)std::min<long long>(std::max<long long>((items + kWNW - 1) / kWNW, 1), g_fftb)),

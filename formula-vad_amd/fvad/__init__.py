@@ -140,6 +140,8 @@ SYMBOLS = [
     ("fvad_engine_destroy", None, [C.c_void_p]),
     ("fvad_engine_reset", C.c_int, [C.c_void_p]),
     ("fvad_engine_push", C.c_int, [C.c_void_p, F32P, C.c_int, I32P, C.c_void_p]),
+    ("fvad_engine_push_ex", C.c_int, [C.c_void_p, F32P, C.c_int, I32P, I32P, C.c_void_p]),
+    ("fvad_engine_submit_ex", C.c_int, [C.c_void_p, F32P, C.c_int, I32P, I32P]),
     ("fvad_engine_input_slot", C.c_void_p, [C.c_void_p]),
     ("fvad_engine_submit", C.c_int, [C.c_void_p, F32P, C.c_int, I32P]),
     ("fvad_engine_collect", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]),
@@ -301,8 +303,9 @@ class Engine:
                     fptr(o["win_vad"]), fptr(o["band"]), fptr(o["denoised"]) if denoised else None)
         return o, s
 
-    def push(self, pcm, ticks_valid=None, denoised=False):
-        """pcm: [ticks][streams][channels][480] normalised f32."""
+    def push(self, pcm, ticks_valid=None, denoised=False, last_tick_samples=None):
+        """pcm: [ticks][streams][channels][480] normalised f32; last_tick_samples
+        (no-denoiser engines): real samples in each stream's last valid tick."""
         pcm = np.ascontiguousarray(pcm, np.float32)
         T = pcm.shape[0]
         assert pcm.shape[1:] == (self.B, self.C, FRAME), pcm.shape
@@ -310,8 +313,10 @@ class Engine:
         tv = None
         if ticks_valid is not None:
             tv = np.ascontiguousarray(ticks_valid, np.int32)
-        _check(lib().fvad_engine_push(self.h, fptr(pcm), T, tv.ctypes.data_as(I32P) if tv is not None else None,
-                                      C.byref(s)), "fvad_engine_push")
+        lt = np.ascontiguousarray(last_tick_samples, np.int32) if last_tick_samples is not None else None
+        _check(lib().fvad_engine_push_ex(self.h, fptr(pcm), T, tv.ctypes.data_as(I32P) if tv is not None else None,
+                                         lt.ctypes.data_as(I32P) if lt is not None else None, C.byref(s)),
+               "fvad_engine_push_ex")
         return o
 
     def input_slot(self):
@@ -503,15 +508,15 @@ def recording_channel(channel_pcm):
 class AudioPipeline:
     """src/AudioPipeline.zig for one stream (pushSamples -> VAD -> VADMachine)."""
 
-    def __init__(self, model, n_channels=2, sample_rate=48000, device=0, main_cfg=None, alt_cfgs=()):
+    def __init__(self, model, n_channels=2, sample_rate=48000, device=0, main_cfg=None, alt_cfgs=(),
+                 fft_size=2048, use_denoiser=True):
         self.model = model
-        main = main_cfg if main_cfg is not None else VadmConfig.default()
-        alts = (VadmConfig * max(1, len(alt_cfgs)))(*alt_cfgs) if alt_cfgs else None
-        self._keep = (main, alts)
+        vc = VadConfig.make(fft_size, use_denoiser, main_cfg, tuple(alt_cfgs))
+        self._keep = (vc,)
         self.n_alt = len(alt_cfgs)
         h = C.c_void_p()
-        _check(lib().fvad_pipeline_create(sample_rate, n_channels, model.h, device, C.byref(main), alts,
-                                          self.n_alt, C.byref(h)), "fvad_pipeline_create")
+        _check(lib().fvad_pipeline_create_ex(sample_rate, n_channels, model.h, device, C.byref(vc), C.byref(h)),
+               "fvad_pipeline_create_ex")
         self.h = h
 
     def push_samples(self, channel_pcm):

@@ -169,6 +169,11 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_fftb": (p["re-block + FFT B share"], 480 * 4 + 4),
         "k_vadm_hbm": (p["VADMachine share"], (4218 + 4 + 11 + 2) * 4 * FRAME / fft_size / C + 16),
     }
+    # k_olafb (fft_size 2048, <= 4 channels): k_ola + k_winmeta + k_fftbw in one
+    # kernel; the ys rows in, per-tick outputs out, the re-block window stays
+    # in LDS (only the partial window crosses pushes through the ring:
+    # <= 2047 samples each way per channel and push, ~2 x 8 KB / 50 ticks)
+    k["k_olafb"] = (960 + p["re-block + FFT B share"], 960 * 4 + 4 * 4.0 / C + 2 * 8192.0 / 50)
     k["k_gru16"] = k["k_rnn3"]  # FVAD_MODE_FP16: the same recurrence, gate sums on MFMA
     return {n: {"flops": f, "bytes": b} for n, (f, b) in k.items()}
 

@@ -151,6 +151,14 @@ typedef struct {
  * end of file; the rest of its slots are ignored).  Synchronous. */
 int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
                      fvad_outputs *out);
+/* The same with last_tick_samples (nullable): stream s's last valid tick holds
+ * only last_tick_samples[s] (1..480) real samples, the rest of its slot is
+ * ignored.  Only use_denoiser = 0 engines accept a partial tick: that path
+ * reads fft_size frames (VAD.zig:206-220) and counts samples, so a window
+ * completes as soon as its last sample is in, whatever the push sizes; with
+ * the denoiser a frame needs all 480 samples (FVAD_EINVAL otherwise). */
+int fvad_engine_push_ex(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
+                        const int32_t *last_tick_samples, fvad_outputs *out);
 
 /* Streaming ingest (the simulator's read loop, SimulationInstance.zig:194-203,
  * reads the next chunk while the pipeline works on the last one).  Two pushes
@@ -165,6 +173,8 @@ int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, const int32_
  * blocks until that slot's previous copy to the device finished; NULL on error */
 float *fvad_engine_input_slot(fvad_engine *e);
 int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid);
+int fvad_engine_submit_ex(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
+                          const int32_t *last_tick_samples);
 int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_ticks);
 
 /* Device-resident variants for benchmarking / zero-copy producers. */

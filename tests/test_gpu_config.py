@@ -101,3 +101,88 @@ def test_fused_mode_size_limits(fvad_mod, models):
         fvad_mod.Engine(m, 1, 2, fft_size=256)  # < 480: more than one window per tick
     with pytest.raises(fvad_mod.FvadError):
         fvad_mod.Engine(m, 1, 2, fft_size=1001)  # odd (FFT.zig:29-31)
+
+
+def test_without_denoiser_partial_ticks_engine(fvad_mod, oracle_mod, models):
+    """use_denoiser = false counts samples, not ticks (VAD.zig:206-220 reads
+    fft_size frames): a stream's last tick may be partial (last_tick_samples)
+    and a window whose last sample sits in it still completes.  Stream lengths
+    2048, 3 * 2048 and 5 s + 7 samples: 1, 3 and every window of the oracle,
+    bit for bit."""
+    m, om = models
+    lens = [2048, 3 * 2048, 48000 * 5 + 7]
+    streams = [fvad_mod.synth_stream(i, n, 2)[0] for i, n in zip((3, 19, 4), lens)]
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=64, bands=(speech_bins(2048),), use_denoiser=False)
+    T = max((n + 479) // 480 for n in lens)
+    wins = [[] for _ in streams]
+    for t0 in range(0, T, 64):
+        nt = min(64, T - t0)
+        pcm = np.zeros((nt, len(streams), 2, 480), np.float32)
+        valid = np.zeros(len(streams), np.int32)
+        last = np.full(len(streams), 480, np.int32)
+        for s, x in enumerate(streams):
+            a, b = t0 * 480, min(x.shape[1], (t0 + nt) * 480)
+            if b <= a:
+                continue
+            k = b - a
+            valid[s] = (k + 479) // 480
+            last[s] = k - (valid[s] - 1) * 480
+            seg = np.zeros((2, valid[s] * 480), np.float32)
+            seg[:, :k] = x[:, a:b]
+            pcm[:valid[s], s] = seg.reshape(2, valid[s], 480).transpose(1, 0, 2)
+        o = eng.push(pcm, ticks_valid=valid, last_tick_samples=last)
+        for s in range(len(streams)):
+            wf = o["win_flag"][:valid[s], s].astype(bool)
+            wins[s].append((o["band"][:valid[s], s][wf, :, 0], o["win_ratio"][:valid[s], s][wf]))
+    for s, x in enumerate(streams):
+        _, wi, _ = oracle_windows(oracle_mod, om, x, 2048, False, 48000)
+        band = np.concatenate([b for b, _ in wins[s]])
+        ratio = np.concatenate([r for _, r in wins[s]])
+        assert len(wi) == len(band) == x.shape[1] // 2048, s
+        assert np.array_equal(wi["band"][:, :2], band), s
+        assert np.array_equal(wi["ratio"], ratio), s
+
+
+def test_without_denoiser_pipeline_odd_pushes(fvad_mod, oracle_mod, models):
+    """AudioPipeline (use_denoiser = false) fed odd-sized pushes: after EVERY
+    push its segments equal the oracle's after the same push (a window is
+    taken as soon as its samples are in, never a tick later)."""
+    m, om = models
+    x = fvad_mod.synth_stream(21, 48000 * 40 + 333, 2)[0]
+    pipe = fvad_mod.AudioPipeline(m, 2, use_denoiser=False)
+    ref = oracle_mod.Pipeline(2, om, fft_size=2048, use_denoiser=False)
+    rng = np.random.default_rng(5)
+    pos, n_checks, n_segs = 0, 0, 0
+    while pos < x.shape[1]:
+        k = int(min(x.shape[1] - pos, rng.integers(1, 40000)))
+        pipe.push_samples([x[0, pos:pos + k], x[1, pos:pos + k]])
+        ref.push([x[0, pos:pos + k], x[1, pos:pos + k]])
+        pos += k
+        assert pipe.segments() == ref.segments(), pos
+        n_checks += 1
+        n_segs = len(ref.segments())
+    assert n_checks > 10 and n_segs > 0
+
+
+def test_without_denoiser_multi_ragged_tails(fvad_mod, oracle_mod, models):
+    """fvad_multi (the simulator core) with use_denoiser = false and stream
+    lengths that end inside a tick: the final partial tick is submitted, so the
+    segments equal the oracle's, the last window included."""
+    m, om = models
+    lens = [48000 * 30 + 2048 + 100, 48000 * 22 + 4095, 48000 * 31 + 1]
+    ids = (3, 19, 8)
+    streams = [fvad_mod.synth_stream(i, n, 2)[0] for i, n in zip(ids, lens)]
+    multi = fvad_mod.Multi(m, len(streams), 2, devices=(0,), ticks_per_push=50, use_denoiser=False)
+    multi.run_stream(streams, chunk=4801)
+    for s, x in enumerate(streams):
+        _, _, segs = oracle_windows(oracle_mod, om, x, 2048, False, 48000)
+        assert multi.segments(s) == segs, s
+
+
+def test_partial_tick_needs_no_denoiser(fvad_mod, models):
+    """With the denoiser a 480-sample frame is never cut (VAD.zig:219)."""
+    m, _ = models
+    eng = fvad_mod.Engine(m, 1, 2, max_ticks=4)
+    with pytest.raises(fvad_mod.FvadError):
+        eng.push(np.zeros((2, 1, 2, 480), np.float32), last_tick_samples=[100])
+    eng.push(np.zeros((2, 1, 2, 480), np.float32), last_tick_samples=[480])  # full ticks: fine
