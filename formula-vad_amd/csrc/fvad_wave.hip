@@ -603,19 +603,21 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_olafb(StagedArgs a) {
   float *mag = mg[wv];
   const int C = a.n_channels, nb = a.n_bands, B = a.n_streams, V = a.V;
   const int G = kWNW / C;  // streams per workgroup item
-  const int sw = wv / C, c = wv - sw * C;
+  // wave-uniform bookkeeping in scalar registers (the transform needs the VGPRs)
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int sw = wvu / C, c = wvu - sw * C;
   const float kInv = a.raw_s16 ? 1.0f : 1.0f / (float)32767;
   const int rl = a.ring_len;
   for (int sb = blockIdx.x * G; sb < B; sb += gridDim.x * G) {
     const int s = sb + sw;
     const bool on = sw < G && s < B;
-    const int nt = on ? ticks_of(a, s) : 0;
+    const int nt = __builtin_amdgcn_readfirstlane(on ? ticks_of(a, s) : 0);
     float *stp = a.state + (size_t)(on ? s : 0) * st::kWords;
     int fd0 = 0;
     float vol = 0;
     if (nt > 0) {
-      fd0 = reinterpret_cast<const int *>(stp)[st::kFramesDone];
-      vol = stp[st::kVolAcc];
+      fd0 = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int *>(stp)[st::kFramesDone]);
+      vol = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(stp[st::kVolAcc])));
     }
     // the partial window carried from the previous push: samples [ws, fd0 * 480)
     long long ws = (long long)fd0 * kFrame / FB * FB;
@@ -650,7 +652,23 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_olafb(StagedArgs a) {
       };
       float4 cn[2] = {}, pn[2] = {};
       load(0, cn, pn);
+      // per-tick inputs of the window bookkeeping, 64 ticks at a time: lane l
+      // holds tick t0 + l's volume ratio and vad_low (VAD.zig:284-293), read
+      // per tick with a wave-uniform readlane (no global load waits per tick)
+      float tk_ratio = 0, tk_vad = 1;
       for (int t = 0; t < nt; t++) {
+        if ((t & 63) == 0) {
+          const int tl = t + lane;
+          tk_ratio = 0;
+          tk_vad = 1;
+          if (tl < nt) {
+            tk_ratio = a.ratio[(size_t)tl * B + s];
+            for (int cc = 0; cc < C; cc++) {
+              const float vv = a.vadf[(size_t)s * V + tl * C + cc];
+              if (vv < tk_vad) tk_vad = vv;
+            }
+          }
+        }
         float4 cur[2] = {cn[0], cn[1]}, prv[2] = {pn[0], pn[1]};
         const long long p0 = (long long)(fd0 + t) * kFrame;
         const int off = (int)(p0 - ws);  // window position of the tick's first sample
@@ -679,13 +697,9 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_olafb(StagedArgs a) {
           for (int e = 0; e < 8; e++)
             if (off + q + e < FB) W[off + q + e] = o[e];
         }
-        // vad_low (VAD.zig:284-293) and the window bookkeeping (VAD.zig:298-348)
-        float vad_low = 1;
-        for (int cc = 0; cc < C; cc++) {
-          const float vv = a.vadf[(size_t)s * V + t * C + cc];
-          if (vv < vad_low) vad_low = vv;
-        }
-        const float ratio = a.ratio[ot];
+        // vad_low and the window bookkeeping (VAD.zig:298-348)
+        const float vad_low = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tk_vad), t & 63));
+        const float ratio = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tk_ratio), t & 63));
         if (complete) {
           const int r = FB - off;
           vol += ratio * ((float)r / (float)FB);
