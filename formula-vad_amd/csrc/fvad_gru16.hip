@@ -17,19 +17,18 @@
 // vector in the rnnimg term order (inputs in concatenation order, then the
 // state or r*state), 8-element chunks of a per-stream f16 operand row in LDS.
 // Each wave keeps the A fragments (weights) of its tiles in registers for the
-// whole kernel (24 slots = 96 VGPRs); the denoise z|r matrix (84 of the 192
-// fragments) sits in LDS.  A tile costs per frame one ds_read_b128
-// of B (and of A from LDS) per K-block plus the MFMA chain.
+// whole kernel (kFr = 20 slots of 8 f16); the denoise z|r matrix (84 of the
+// 192 fragments) sits in LDS.  A tile costs per frame one ds_read_b128 of B
+// (and of A from LDS) per K-block plus the MFMA chain.
 //
-// Frame t is seven phases (one barrier each) on 8 waves; features of t+1 and
-// the gains of t-1 run on waves the phase leaves idle:
-//   P0  dense(t) [w0,1]                den_out(t-1) [w2,3]
-//   P1  vad z|r(t) [w4..6]             features(t+1) [w0..3]   gains(t-1) [w7]
-//   P2  vad h(t) [w4,5]                spectral variability(t+1) [w0,1]
-//   P3  noise z|r(t) [w0..5]           vad_out(t) [w6]         fetch raw features(t+2)
-//   P4  noise h(t) [w5..7]
-//   P5  denoise z|r(t) [w0..7, w0..3 a second tile]
-//   P6  denoise h(t) [w2..7]           stage raw features(t+2)
+// Schedule: a superstep pipeline over frames (details above k_gru16).  Layer
+// L of frame t waits only for layer L - 1 of t and layer L of t - 1, so
+// superstep u runs dense(u), vad(u - 1), noise(u - 2), denoise(u - 3) and the
+// outputs of u - 2 / u - 4 side by side in two phases -- A: every z|r gate,
+// B: every candidate -- two barriers per frame; the features of u + 1 and the
+// gain smoothing of u - 4 fill the waves a phase leaves idle.  Operand
+// segments read by layers of different frames in one phase are versioned by
+// frame (OpSeg).
 #pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
 

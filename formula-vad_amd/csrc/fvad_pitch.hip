@@ -55,7 +55,10 @@ static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
 #define FVAD_Q1_B64 0
 #endif
 #ifndef FVAD_Q3_B64
-#define FVAD_Q3_B64 0
+#define FVAD_Q3_B64 1
+#endif
+#ifndef FVAD_Q5_COMPACT
+#define FVAD_Q5_COMPACT 1
 #endif
 constexpr int kPcXS = 870;  // xf row pitch: even (8-byte aligned pairs in Q5), = 6 mod 8 (conflict-free Q0 stores)
 constexpr int kPcSP = 153;  // coarse xcorr / Syy row pitch (odd; >= 147 rounded up to the scan block)
@@ -475,8 +478,29 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     // wave's serial walk carries 3 or 1 chains instead of 4.
     const bool q5b = tq >= 128;
     const int q5i = q5b ? tq - 128 : tq;
+#if FVAD_Q5_COMPACT
+    // items packed in frame order from lane 0 (window items c = 0..nv on
+    // waves 0-1, T1b items c = 1..nv on waves 2-3): ~7.6 items per frame fill
+    // one wave of each pair, the other usually has none and skips the walk
+    int q5f = 0, q5c = 0;
+    bool q5on = false;
+    {
+      int base = 0;
+#pragma unroll
+      for (int f = 0; f < kPcF; f++) {
+        const int n = fval[f] ? (q5b ? nvs[f] : 1 + nvs[f]) : 0;
+        if (!q5on && q5i >= base && q5i < base + n) {
+          q5on = true;
+          q5f = f;
+          q5c = q5i - base + (q5b ? 1 : 0);
+        }
+        base += n;
+      }
+    }
+#else
     const int q5f = q5i / 15, q5c = q5i - 15 * q5f;
     const bool q5on = q5i < 15 * kPcF && fval[q5f] && (q5c == 0 ? !q5b : q5c - 1 < nvs[q5f]);
+#endif
     float aM = 0, a0 = 0, aP = 0;
     int q5T0 = 0, q5Tc = 0, q5Tb = 0;
     if (q5on) {
