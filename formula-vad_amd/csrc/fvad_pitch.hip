@@ -120,38 +120,94 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     }
     float *Tq = a.ptile + (size_t)gq4 * ptile::kRows * ptile::kQuarter;  // the quarter's block
     const float *T = Tq + h * kPcF;
+    const long long gt = gq4 >> 2;
+    const int gqq = (int)(gq4 & 3);
+    const int gsb = (int)(gt / Vr), gv = (int)(gt - (long long)gsb * Vr);
+    const int s_first = gsb * 64 + gqq * 16 + h * kPcF;  // stream of the group's frame 0
     if (tq < kPcF) {
-      const long long t = gq4 >> 2;
-      const int q = (int)(gq4 & 3);
-      const int sb = (int)(t / Vr), v = (int)(t - (long long)sb * Vr);
-      const int s = sb * 64 + q * 16 + h * kPcF + tq;
-      fval[tq] = s < a.n_streams && v < ticks_of(a, s) * a.n_channels;
-      fidx[tq] = (long long)s * a.V + v;
+      const int s = s_first + tq;
+      fval[tq] = s < a.n_streams && gv < ticks_of(a, s) * a.n_channels;
+      fidx[tq] = (long long)s * a.V + gv;
     }
-    // Q0: each thread's float4 loads go out in batches of kQ0B before their LDS
-    // stores (a few memory latencies per group instead of one per loop trip)
-    constexpr int P4 = kPcF / 4;  // float4s per row and group
-    constexpr int kQ0N = (kXlp + 147) * P4, kQ0B = 4;
-    for (int u0 = 0; u0 < kQ0N; u0 += NT * kQ0B) {
-      float4 w4[kQ0B];
+    // Q0: xf = celt_fir5(x_lp) rebuilt here (k_plpc stores only the filter's
+    // coefficients): the frames' x_lp rows (864 values each, contiguous in
+    // the x_lp row of the stream) -> LDS, and the coarse Syy sequence; loads
+    // go out in batches of kQ0B before their LDS stores
+    {
+      constexpr int kRow4 = kXlp / 4;                    // float4 per frame's x_lp window
+      constexpr int P4 = kPcF / 4;                       // float4 per Syy row and group
+      constexpr int kN1 = kRow4 * kPcF, kQ0N = kN1 + 147 * P4, kQ0B = 4;
+      for (int u0 = 0; u0 < kQ0N; u0 += NT * kQ0B) {
+        float4 w4[kQ0B];
 #pragma unroll
-      for (int u = 0; u < kQ0B; u++) {
-        const int idx = u0 + tq + NT * u, r = idx / P4, p = idx % P4;
-        const int row = r < kXlp ? r : ptile::kSc + (r - kXlp);
-        if (idx < kQ0N) w4[u] = *reinterpret_cast<const float4 *>(T + row * ptile::kQuarter + 4 * p);
-      }
+        for (int u = 0; u < kQ0B; u++) {
+          const int idx = u0 + tq + NT * u;
+          if (idx < kN1) {
+            const int fr = idx / kRow4, j = idx - fr * kRow4;
+            const int s = min(s_first + fr, a.n_streams - 1);
+            w4[u] = *reinterpret_cast<const float4 *>(a.xlp + (size_t)s * a.LX + (size_t)gv * (kFrame / 2) + 4 * j);
+          } else if (idx < kQ0N) {
+            const int r = (idx - kN1) / P4, p = (idx - kN1) % P4;
+            w4[u] = *reinterpret_cast<const float4 *>(T + (ptile::kSc + r) * ptile::kQuarter + 4 * p);
+          }
+        }
 #pragma unroll
-      for (int u = 0; u < kQ0B; u++) {
-        const int idx = u0 + tq + NT * u, r = idx / P4, p = idx % P4;
-        if (idx < kQ0N) {
-          float *d = r < kXlp ? &xf[4 * p][r] : &scl[4 * p][r - kXlp];
-          const int pitch = r < kXlp ? kPcXS : kPcSP;
-          d[0] = w4[u].x;
-          d[pitch] = w4[u].y;
-          d[2 * pitch] = w4[u].z;
-          d[3 * pitch] = w4[u].w;
+        for (int u = 0; u < kQ0B; u++) {
+          const int idx = u0 + tq + NT * u;
+          if (idx < kN1) {
+            const int fr = idx / kRow4, j = idx - fr * kRow4;
+            float2 *d = reinterpret_cast<float2 *>(&xf[fr][4 * j]);  // rows are 8-byte aligned
+            d[0] = make_float2(w4[u].x, w4[u].y);
+            d[1] = make_float2(w4[u].z, w4[u].w);
+          } else if (idx < kQ0N) {
+            const int r = (idx - kN1) / P4, p = (idx - kN1) % P4;
+            float *d = &scl[4 * p][r];
+            d[0] = w4[u].x;
+            d[kPcSP] = w4[u].y;
+            d[2 * kPcSP] = w4[u].z;
+            d[3 * kPcSP] = w4[u].w;
+          }
         }
       }
+    }
+    {
+      // celt_fir5 in place: lane (frame, l) filters x_lp[27 l .. 27 l + 26]
+      // (history x[n-1..n-5] = 0 before n = 0; x_lp[0] = the frame's edge
+      // value), the outputs held until every lane has read its inputs
+      constexpr int kRun = kXlp / kPcL;
+      static_assert(kRun * kPcL == kXlp, "FIR runs");
+      const int fr = tq / kPcL, n0 = kRun * (tq % kPcL);
+      const float *ft = T + ptile::kFir * ptile::kQuarter + fr;
+      float l[5];
+#pragma unroll
+      for (int i = 0; i < 5; i++) l[i] = ft[i * ptile::kQuarter];
+      const float x0 = ft[5 * ptile::kQuarter];
+      __syncthreads();
+      const float *xr = xf[fr];
+      float m1 = 0, m2 = 0, m3 = 0, m4 = 0, m5 = 0;
+      if (n0 > 0) {
+        m1 = xr[n0 - 1];
+        m2 = xr[n0 - 2];
+        m3 = xr[n0 - 3];
+        m4 = xr[n0 - 4];
+        m5 = xr[n0 - 5];
+      }
+      float y[kRun];
+#pragma unroll
+      for (int k = 0; k < kRun; k++) {
+        const float x = (k == 0 && n0 == 0) ? x0 : xr[n0 + k];
+        float v = x;
+        v = v + l[0] * m1;
+        v = v + l[1] * m2;
+        v = v + l[2] * m3;
+        v = v + l[3] * m4;
+        v = v + l[4] * m5;
+        m5 = m4, m4 = m3, m3 = m2, m2 = m1, m1 = x;
+        y[k] = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kRun; k++) xf[fr][n0 + k] = y[k];
     }
     __syncthreads();
     RSTAMP(0);

@@ -15,11 +15,13 @@ constexpr int kPitchRecord = 80;  // floats per frame of the pitch record (k_pco
 
 // Pitch tile buffer (k_plpc -> k_pcorr): a tile is 64 streams at one frame
 // position; each quarter (16 streams) is one contiguous block of kRows rows of
-// 16 floats (the yy_lookup region is laid out frame-major instead).
+// 16 floats (the yy_lookup region is laid out frame-major instead).  xf (x_lp
+// after celt_fir5) is not stored: k_pcorr rebuilds it from the x_lp rows and
+// the frame's FIR coefficients (5.2 -> 1.8 KB written per frame).
 namespace ptile {
 constexpr int kTile = 64, kQuarter = 16;
-constexpr int kXf = 0;              // xf[0..863]: x_lp after celt_fir5
-constexpr int kSc = 864;            // Syy before step i of the coarse find_best_pitch, i < 147
+constexpr int kFir = 0;             // celt_fir5 coefficients lpc2[0..4], then x_lp[0] (the frame's edge value)
+constexpr int kSc = 8;              // Syy before step i of the coarse find_best_pitch, i < 147
 constexpr int kSf = kSc + 147;      // Syy of the fine find_best_pitch, i < 294
 constexpr int kYy = kSf + 294;      // yy_lookup[0..384] (remove_doubling), k_pcorr's own region:
 constexpr int kYyPitch = 388;       //   [16 frames][kYyPitch] (float4-aligned frame rows), kYyPitch rows of 16

@@ -335,44 +335,36 @@ __device__ __forceinline__ float lp_value(const float *col, int u, float x0) {
 struct Fir5State {
   float l[5];
   float m1 = 0, m2 = 0, m3 = 0, m4 = 0, m5 = 0;  // x_lp[n-1..n-5]
+  float b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0;  // x_lp[n-481..n-485]: the lagged filter (xf[n - 480])
   float x0 = 0;                                  // x_lp[0]
   float Sc = 1.0f, Sf = 1.0f, xx = 0.0f;
 };
+
+// celt_fir5 step: y = x + l0 x[n-1] + ... + l4 x[n-5] in C order, history shifted
+__device__ __forceinline__ float fir5_step(const float (&l)[5], float x, float &m1, float &m2, float &m3, float &m4,
+                                           float &m5) {
+  float y = x;
+  y = y + l[0] * m1;
+  y = y + l[1] * m2;
+  y = y + l[2] * m3;
+  y = y + l[3] * m4;
+  y = y + l[4] * m5;
+  m5 = m4, m4 = m3, m3 = m2, m2 = m1, m1 = x;
+  return y;
+}
 
 // Row stores of the tile buffer go through a per-wave LDS stage: a chunk's
 // rows (one value per lane each) are written to LDS [row][lane], then each
 // lane stores two float4 of its quarter's [row][16] block, so one store
 // instruction writes 1 KB in four 256-byte runs instead of 256 bytes in four
 // 64-byte pieces (measured: the per-step dword row stores cost k_plpc ~0.4 ms).
-// Row loads of the read-back (xf[n - 480] for the Syy recurrences)
-// take the same route backwards: two float4 per lane of the quarter's block,
-// then LDS, then each lane reads its column.
+// xf itself is not stored (k_pcorr rebuilds it from x_lp and the coefficients):
+// the Syy recurrences' xf[n - 480] comes from a second filter over the x_lp
+// chunk 480 values back, staged like the current one.
 struct OutStage {
-  float xf[kLpStep][64];      // xf rows of the chunk
   float sf[kLpStep][64];      // fine Syy rows
   float sc[kLpStep / 2][64];  // coarse Syy rows
-  float in[kLpStep][64];      // read-back rows xf[n - 480]
 };
-struct RowLd {
-  float4 v[2];
-};
-template <int NR>
-__device__ __forceinline__ void fetch_rows(const float *qbase, int row0, RowLd &r, int lane) {
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const int j = (lane & 15) + 16 * k, u = j >> 2, c4 = j & 3;
-    r.v[k] = u < NR ? *reinterpret_cast<const float4 *>(qbase + (row0 + u) * ptile::kQuarter + 4 * c4)
-                    : make_float4(0, 0, 0, 0);
-  }
-}
-__device__ __forceinline__ void stage_rows(const RowLd &r, float (*ob)[64], int lane) {
-  const int q = lane >> 4;
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const int j = (lane & 15) + 16 * k, u = j >> 2, c4 = j & 3;
-    *reinterpret_cast<float4 *>(&ob[u][16 * q + 4 * c4]) = r.v[k];
-  }
-}
 // rows row0 .. row0 + NR - 1 of the lane's quarter (qbase = its [row][16] block)
 template <int NR>
 __device__ __forceinline__ void flush_rows(float *qbase, int row0, const float (*ob)[64], int lane) {
@@ -390,31 +382,21 @@ __device__ __forceinline__ void flush_rows(float *qbase, int row0, const float (
 //   1 [0, 384)    Syy initial sums      2 [384, 480)  + xx
 //   3 [480, 774)  xx + Syy recurrences  4 the chunk holding n = 773 (guarded)
 //   5 [774, 864)  xx only
-template <bool First, int R>
-__device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, float *qbase, int n0,
-                                           const RowLd &bk, OutStage &ob, int lane) {
+// bcol: the staged x_lp column of chunk n0 - 480 (regions 3, 4; LagFirst: it
+// is chunk 0, whose x_lp[0] is the lane's x0)
+template <bool First, int R, bool LagFirst>
+__device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, const float *bcol, float *qbase, int n0,
+                                           OutStage &ob, int lane) {
   constexpr int kR4 = (480 + 294) % kLpStep;  // region 4 starts at a chunk boundary
-  if (R == 3 || R == 4) {
-    stage_rows(bk, ob.in, lane);
-    wave_sync();
-  }
 #pragma unroll
   for (int u = 0; u < kLpStep; u++) {
-    const float x = lp_value<First>(col, u, f.x0);
-    float y = x;
-    y = y + f.l[0] * f.m1;
-    y = y + f.l[1] * f.m2;
-    y = y + f.l[2] * f.m3;
-    y = y + f.l[3] * f.m4;
-    y = y + f.l[4] * f.m5;
-    f.m5 = f.m4, f.m4 = f.m3, f.m3 = f.m2, f.m2 = f.m1, f.m1 = x;
-    ob.xf[u][lane] = y;
+    const float y = fir5_step(f.l, lp_value<First>(col, u, f.x0), f.m1, f.m2, f.m3, f.m4, f.m5);
     if (R <= 2) {
       if ((u & 1) == 0) f.Sc = f.Sc + y * y;  // n0 is a multiple of 8: n even <=> u even
       f.Sf = f.Sf + y * y;
     }
     if (R == 3 || (R == 4 && u < kR4)) {
-      const float yb = ob.in[u][lane];
+      const float yb = fir5_step(f.l, lp_value<LagFirst>(bcol, u, f.x0), f.b1, f.b2, f.b3, f.b4, f.b5);
       ob.sf[u][lane] = f.Sf;
       f.Sf += y * y - yb * yb;
       f.Sf = (1 > f.Sf) ? 1 : f.Sf;
@@ -426,18 +408,20 @@ __device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, float
     }
     if (R >= 2) f.xx = f.xx + y * y;
   }
-  wave_sync();
-  flush_rows<kLpStep>(qbase, ptile::kXf + n0, ob.xf, lane);
-  if (R == 3) {
-    flush_rows<kLpStep>(qbase, ptile::kSf + n0 - 480, ob.sf, lane);
-    flush_rows<kLpStep / 2>(qbase, ptile::kSc + (n0 - 480) / 2, ob.sc, lane);
-  } else if (R == 4) {
-    flush_rows<kR4>(qbase, ptile::kSf + n0 - 480, ob.sf, lane);
-    flush_rows<(kR4 + 1) / 2>(qbase, ptile::kSc + (n0 - 480) / 2, ob.sc, lane);
+  if (R == 3 || R == 4) {
+    wave_sync();
+    if (R == 3) {
+      flush_rows<kLpStep>(qbase, ptile::kSf + n0 - 480, ob.sf, lane);
+      flush_rows<kLpStep / 2>(qbase, ptile::kSc + (n0 - 480) / 2, ob.sc, lane);
+    } else {
+      flush_rows<kR4>(qbase, ptile::kSf + n0 - 480, ob.sf, lane);
+      flush_rows<(kR4 + 1) / 2>(qbase, ptile::kSc + (n0 - 480) / 2, ob.sc, lane);
+    }
+    wave_sync();
   }
-  wave_sync();
 }
 static_assert(384 % kLpStep == 0 && 480 % kLpStep == 0 && kLpStep % 2 == 0, "pass-2 regions");
+static_assert(480 % kLpStep == 0, "the lagged chunk is a whole chunk");
 
 // Both passes walk their chunks through a register ring: the loads of the
 // next kLpPf chunks (pitch-buffer chunks and the Syy read-back) are in flight
@@ -479,10 +463,10 @@ __device__ __forceinline__ void lp_walk(const LpSrc &src, float *stg, int lane, 
 }
 
 __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
-  __shared__ float stg_all[4][kLpRows * kLpCols];
+  __shared__ float stg_all[4][2][kLpRows * kLpCols];
   __shared__ __attribute__((aligned(16))) OutStage ost_all[4];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  float *stg = stg_all[w];
+  float *stg = stg_all[w][0], *stgb = stg_all[w][1];
   OutStage &ob = ost_all[w];
   const float *col = stg + lane;
   const int Vr = a.n_ticks * a.n_channels;
@@ -573,39 +557,46 @@ __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
     lpc_fir5_coeffs(acv, l);
 
     // pass 2: x_lp again -> celt_fir5 -> xf; Syy initial sums, xx; from
-    // n = 480 on, the Syy recurrences with xf[n - 480] read back from the tile
-    // buffer (written by this lane 480 steps earlier, loaded kLpPf chunks
-    // ahead).  The chunk body is specialised per region of n, so it has no
-    // branches.
+    // n = 480 on, the Syy recurrences with xf[n - 480] from a second filter
+    // over the x_lp chunk 480 values back (loaded kLpPf chunks ahead, staged in
+    // the wave's second column).  The chunk body is specialised per region of
+    // n, so it has no branches.
     Fir5State fs;
     fs.x0 = x0;
 #pragma unroll
     for (int i = 0; i < 5; i++) fs.l[i] = l[i];
-    RowLd bk[kLpPf];
+    float4 bk[kLpPf][kLpPR];
+    const float *bcol = stgb + lane;
     lp_walk(
         src, stg, lane,
         [&](int c, int slot) {
           const int n0 = c * kLpStep;
-          if (n0 + kLpStep > 480 && n0 < 480 + 294) fetch_rows<kLpStep>(qbase, ptile::kXf + n0 - 480, bk[slot], lane);
+          if (n0 >= 480 && n0 < 480 + 294) lp_fetch(src, c - 480 / kLpStep, bk[slot]);
         },
         [&](int c, int slot) {
           const int n0 = c * kLpStep;
+          if (n0 >= 480 && n0 < 480 + 294) lp_stage(stgb, lane, bk[slot]);
           if (c == 0)
-            fir5_chunk<true, 1>(fs, col, qbase, n0, bk[slot], ob, lane);
+            fir5_chunk<true, 1, false>(fs, col, bcol, qbase, n0, ob, lane);
           else if (n0 < 384)
-            fir5_chunk<false, 1>(fs, col, qbase, n0, bk[slot], ob, lane);
+            fir5_chunk<false, 1, false>(fs, col, bcol, qbase, n0, ob, lane);
           else if (n0 < 480)
-            fir5_chunk<false, 2>(fs, col, qbase, n0, bk[slot], ob, lane);
+            fir5_chunk<false, 2, false>(fs, col, bcol, qbase, n0, ob, lane);
+          else if (n0 == 480)
+            fir5_chunk<false, 3, true>(fs, col, bcol, qbase, n0, ob, lane);
           else if (n0 + kLpStep <= 480 + 294)
-            fir5_chunk<false, 3>(fs, col, qbase, n0, bk[slot], ob, lane);
+            fir5_chunk<false, 3, false>(fs, col, bcol, qbase, n0, ob, lane);
           else if (n0 < 480 + 294)
-            fir5_chunk<false, 4>(fs, col, qbase, n0, bk[slot], ob, lane);
+            fir5_chunk<false, 4, false>(fs, col, bcol, qbase, n0, ob, lane);
           else
-            fir5_chunk<false, 5>(fs, col, qbase, n0, bk[slot], ob, lane);
+            fir5_chunk<false, 5, false>(fs, col, bcol, qbase, n0, ob, lane);
         });
     RSTAMP(1);
-    const float xx = fs.xx;
-    out[ptile::kXx * ptile::kQuarter] = xx;
+    out[ptile::kXx * ptile::kQuarter] = fs.xx;
+    // k_pcorr's xf: the FIR coefficients and x_lp[0]
+#pragma unroll
+    for (int i = 0; i < 5; i++) out[(ptile::kFir + i) * ptile::kQuarter] = l[i];
+    out[(ptile::kFir + 5) * ptile::kQuarter] = x0;
 
     // yy_lookup (remove_doubling's energy recurrence from xx) is k_pcorr's:
     // it walks it on a wave its product phase leaves idle, from xf in LDS
