@@ -17,45 +17,48 @@ namespace fvad {
 // ---------------------------------------------------------------------------
 // k_pcorr: one 256-thread workgroup per half quarter tile (8 streams at one
 // frame position; 39.8 KB of LDS, so 4 workgroups share a CU).
-//   Q0 xf (rows 0..863) and the coarse Syy sequence -> LDS
+//   Q0 the frames' x_lp windows (from the x_lp rows) and the coarse Syy
+//      sequence -> LDS; xf = celt_fir5(x_lp) with k_plpc's coefficients, in
+//      place
 //   Q1 coarse xcorr: lane = (frame, 5 consecutive lags), a register window of
 //      5 y values slides one sample per step (2 LDS reads per 5 MACs); then
 //      the coarse scan's survivors: a prefix top-2 of the lags' xcorr^2/Syy
 //      ratios over the frame's 32 lanes drops every lag that provably cannot
 //      change find_best_pitch's state, and the rest are listed in lag order
 //   Q2 coarse find_best_pitch over the survivors (exact, lane per frame; ~3 k
-//      instead of ~23 k cycles for all 147 lags); the fine Syy values at the
-//      <= 10 candidate lags are fetched here, used in Q4
-//   Q3 fine xcorr at the <= 10 lags within +-2 of 2*best (others are 0)
+//      instead of ~23 k cycles for all 147 lags)
+//   Q3 fine xcorr at the <= 10 lags within +-2 of 2*best (others are 0), on
+//      lanes split by lag parity; each lane also walks the fine Syy
+//      recurrence from k_plpc's checkpoint below its lag (<= 7 steps)
 //   Q4 fine find_best_pitch + pseudo-interpolation -> T0, candidate count
 //   Q5 remove_doubling products: lane = (frame, candidate c); candidate c's
 //      xcorr at T-1, T, T+1 share a sliding window of 3, plus xcorr(T1b);
 //      operands are read as aligned pairs (ds_read_b64: 64 banks, 2 steps
 //      per read), the lane's window parity resolved by selects
 //   Beside Q2..Q4, wave 2 (idle there) walks remove_doubling's yy_lookup
-//   recurrence (lane per frame, 384 serial steps) into the tile buffer for Q5.
+//   recurrence (lane per frame, 384 serial steps), keeping every 8th state in
+//   LDS; Q5 rebuilds the values it needs from those checkpoints.
 // ---------------------------------------------------------------------------
 #ifndef FVAD_WALK_Q2
-#define FVAD_WALK_Q2 12
+#define FVAD_WALK_Q2 6
 #endif
 #ifndef FVAD_WALK_Q3
-#define FVAD_WALK_Q3 72
+#define FVAD_WALK_Q3 36
 #endif
 #ifndef FVAD_Q5_UNROLL
 #define FVAD_Q5_UNROLL 4  // Q5 walk unroll (2 / 8 measured no better)
 #endif
 #define FVAD_PRAGMA_(x) _Pragma(#x)
 #define FVAD_UNROLL(n) FVAD_PRAGMA_(unroll n)
-constexpr int kWalkQ2 = FVAD_WALK_Q2, kWalkQ3 = FVAD_WALK_Q3;  // yy walk blocks done by the end of Q2 / Q3 (of 97)
+constexpr int kWalkQ2 = FVAD_WALK_Q2, kWalkQ3 = FVAD_WALK_Q3;  // yy walk checkpoint blocks done by the end of Q2 / Q3 (of 49)
+constexpr int kYyCk = 49;  // checkpoints yy_{8k}, 8k <= 384
+static_assert(FVAD_WALK_Q2 <= 6, "the checkpoints walked during Q2 live in the spare floats of the xf rows");
 constexpr int kPcF = 8;                // frames per workgroup (a quarter tile holds 16)
 constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
 constexpr int kPcNT = kPcL * kPcF;
 static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
 #ifndef FVAD_Q1_B64
 #define FVAD_Q1_B64 0
-#endif
-#ifndef FVAD_Q3_B64
-#define FVAD_Q3_B64 1
 #endif
 #ifndef FVAD_Q5_COMPACT
 #define FVAD_Q5_COMPACT 1
@@ -84,6 +87,10 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
   __shared__ int ncand[kPcF];
   __shared__ int best[kPcF][2], T0s[kPcF], nvs[kPcF], fval[kPcF];
   __shared__ long long fidx[kPcF];
+  // yy_lookup checkpoints yy_{8k}, k = 0..48: k < 6 (walked during Q2, while
+  // xc is still read) in the 6 spare floats of each xf row, the rest in xc
+  // rows (dead after Q2; Q5 uses only xc[fr][0..14])
+  auto yy_ck = [&](int fr, int k) -> float * { return k < 6 ? &xf[fr][kXlp + k] : &xc[fr][16 + k]; };
   const int tid = threadIdx.x;
   const int Vr = a.n_ticks * a.n_channels;
   const int n_sb = (a.n_streams + 63) >> 6;
@@ -320,56 +327,43 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(1);
     // remove_doubling's yy_lookup recurrence, lane per frame on wave 2 (idle
     // from Q2 to Q4), in three pieces beside Q2, Q3 and Q4:
-    // yy_lookup[i] = max(0, yy), yy = (yy + x[-i]^2) - x[480-i]^2 from yy =
-    // xx, x = xf + 384, into the frame's yy row of the tile buffer as float4
-    // stores (block q = i 4q .. 4q+3), read by Q5
+    // yy_lookup[i] = max(0, yy_i), yy_i = (yy_{i-1} + x[-i]^2) - x[480-i]^2
+    // from yy_0 = xx, x = xf + 384.  Only every 8th state yy_{8k} (unclamped)
+    // is kept, in LDS (yy_ck): Q5 rebuilds the two values an item needs from
+    // the checkpoint below them in at most 7 steps of the same recurrence.
     const bool walker = tq >= 128 && tq < 128 + kPcF && fval[tq - 128];
     float wyy = 0;
-    float4 *wY = nullptr;
     const float *wxr = nullptr;
+    int wfr = 0;
     if (walker) {
-      const int fr = tq - 128;
-      wY = reinterpret_cast<float4 *>(Tq + ptile::kYy * ptile::kQuarter + (h * kPcF + fr) * ptile::kYyPitch);
-      wxr = xf[fr];
-      wyy = Tq[ptile::kXx * ptile::kQuarter + h * kPcF + fr];
+      wfr = tq - 128;
+      wxr = xf[wfr];
+      wyy = Tq[ptile::kXx * ptile::kQuarter + h * kPcF + wfr];
     }
-    auto walk = [&](int q0, int q1) {
+    // walk checkpoint blocks [k0, k1): block k > 0 runs steps 8k-7 .. 8k
+    auto walk = [&](int k0, int k1) {
 #ifdef FVAD_STAMPS
       const unsigned long long w0_ = __builtin_amdgcn_s_memtime();
 #endif
-      auto step = [&](int i) -> float {
-        const float va = wxr[384 - i], vb = wxr[864 - i];
-        wyy = wyy + va * va - vb * vb;
-        return (0 > wyy) ? 0 : wyy;
-      };
-      int q = q0;
-      if (q == 0) {
-        float4 o;
-        o.x = wyy;
-        o.y = step(1);
-        o.z = step(2);
-        o.w = step(3);
-        wY[0] = o;
-        q = 1;
+      int k = k0;
+      if (k == 0) {
+        *yy_ck(wfr, 0) = wyy;
+        k = 1;
       }
-      const int qe = q1 < 96 ? q1 : 96;
-#pragma unroll 4
-      for (; q < qe; q++) {
-        float4 o;
-        o.x = step(4 * q);
-        o.y = step(4 * q + 1);
-        o.z = step(4 * q + 2);
-        o.w = step(4 * q + 3);
-        wY[q] = o;
+#pragma unroll 2
+      for (; k < k1; k++) {
+#pragma unroll
+        for (int i = 8 * k - 7; i <= 8 * k; i++) {
+          const float va = wxr[384 - i], vb = wxr[864 - i];
+          wyy = wyy + va * va - vb * vb;
+        }
+        *yy_ck(wfr, k) = wyy;
       }
-      if (q1 == 97) wY[96] = make_float4(step(384), 0.0f, 0.0f, 0.0f);
 #ifdef FVAD_STAMPS
       if (tq == 128) st_walk += __builtin_amdgcn_s_memtime() - w0_;
 #endif
     };
-    static_assert(4 * 97 == ptile::kYyPitch, "yy row");
     // Q2
-    float sfv[10];
     if (tq < kPcF) {
       const int fr = tq;
 #ifdef FVAD_STAMPS
@@ -402,11 +396,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
       }
       best[fr][0] = bst[0];
       best[fr][1] = bst[1];
-#pragma unroll
-      for (int u = 0; u < 10; u++) {
-        const int i = 2 * bst[u / 5] - 2 + (u % 5);
-        sfv[u] = (i >= 0 && i < 294) ? T[(ptile::kSf + i) * ptile::kQuarter + fr] : 0.0f;
-      }
 #ifdef FVAD_STAMPS
       if (fr == 0) st_scan += __builtin_amdgcn_s_memtime() - s0_;
 #endif
@@ -417,7 +406,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     RSTAMP(2);
     // Q3
     if (walker) walk(kWalkQ2, kWalkQ3);
-#if FVAD_Q3_B64
     // lanes by lag parity: wave 0 = the 6 even lags of each frame (u % 5 in
     // {0, 2, 4}), wave 1 = the 4 odd ones, so each wave reads its y operands
     // as aligned pairs (ds_read_b64) without per-lane parity selects; x is
@@ -433,6 +421,10 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
       const int i = (u < 5 ? 2 * bp0 : 2 * bp1) - 2 + (u % 5);
       const bool dup = u >= 5 && abs(i - 2 * bp0) <= 2;
       if (i >= 0 && i < 294 && !dup) {
+        // the fine Syy of lag i (Q4): k_plpc's checkpoint before step 8 (i / 8),
+        // loaded now, walked to i after the product
+        const int ck = i >> 3;
+        float syy = T[(ptile::kSf + ck) * ptile::kQuarter + fr];
         typedef float v2f __attribute__((ext_vector_type(2)));
         const v2f *xp = reinterpret_cast<const v2f *>(xf[fr] + (kPitchMax >> 1));
         float sum = 0.0f;
@@ -457,29 +449,20 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
           }
         }
         fine[fr][u] = (-1 > sum) ? -1 : sum;
+        for (int j = 8 * ck; j < i; j++) {
+          const float y = xf[fr][j + 480], yb = xf[fr][j];
+          syy += y * y - yb * yb;
+          syy = (1 > syy) ? 1 : syy;
+        }
+        sfl[fr][u] = syy;
       }
     }
-#else
-    if (tq < 10 * kPcF) {
-      const int fr = tq / 10, u = tq - 10 * fr;
-      const int bp0 = best[fr][0], bp1 = best[fr][1];
-      const int i = (u < 5 ? 2 * bp0 : 2 * bp1) - 2 + (u % 5);
-      const bool dup = u >= 5 && abs(i - 2 * bp0) <= 2;
-      if (i >= 0 && i < 294 && !dup) {
-        const float *xl = xf[fr] + (kPitchMax >> 1), *y = xf[fr] + i;
-        const float sum = dot_seq(0.0f, xl, 1, y, 1, 480);
-        fine[fr][u] = (-1 > sum) ? -1 : sum;
-      }
-    }
-#endif
     __syncthreads();
     RSTAMP(3);
     // Q4
-    if (walker) walk(kWalkQ3, 97);
+    if (walker) walk(kWalkQ3, kYyCk);
     if (tq < kPcF) {
       const int fr = tq;
-#pragma unroll
-      for (int u = 0; u < 10; u++) sfl[fr][u] = sfv[u];
       const int bp0 = best[fr][0], bp1 = best[fr][1];
       const int w0 = 2 * bp0 - 2, w1 = 2 * bp1 - 2;
       // lags of the first window take its values (a duplicate lag of the
@@ -623,8 +606,18 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     __syncthreads();
     if (q5on && !q5b) {
       const int fr = q5f, c = q5c;
-      const float *yrow = Tq + ptile::kYy * ptile::kQuarter + (h * kPcF + fr) * ptile::kYyPitch;
-      const float yyA = yrow[q5Tc];
+      // yy_lookup[T] from the checkpoint yy_{8 (T / 8)}: the walker's steps
+      // to T, then its clamp
+      auto yy_at = [&](int Tl) -> float {
+        const int k = Tl >> 3;
+        float w = *yy_ck(fr, k);
+        for (int i = 8 * k + 1; i <= Tl; i++) {
+          const float va = xf[fr][384 - i], vb = xf[fr][864 - i];
+          w = w + va * va - vb * vb;
+        }
+        return (0 > w) ? 0 : w;
+      };
+      const float yyA = yy_at(q5Tc);
       const float xx = T[ptile::kXx * ptile::kQuarter + fr];
       float *rg = a.rec + fidx[fr] * rec::kSize;
       const int off = pitch_offset(aP, a0, aM);
@@ -636,7 +629,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         rg[rec::kYy0] = yyA;
         rg[rec::kOff0] = __int_as_float(off);
       } else {
-        const float yyB = yrow[q5Tb];
+        const float yyB = yy_at(q5Tb);
         float *qk = rg + rec::kK + (c - 1) * rec::kKStride;
         const float xy = .5f * (a0 + xc[fr][c]), yy = .5f * (yyA + yyB);
         qk[0] = __int_as_float(q5Tc);

@@ -22,10 +22,10 @@ namespace ptile {
 constexpr int kTile = 64, kQuarter = 16;
 constexpr int kFir = 0;             // celt_fir5 coefficients lpc2[0..4], then x_lp[0] (the frame's edge value)
 constexpr int kSc = 8;              // Syy before step i of the coarse find_best_pitch, i < 147
-constexpr int kSf = kSc + 147;      // Syy of the fine find_best_pitch, i < 294
-constexpr int kYy = kSf + 294;      // yy_lookup[0..384] (remove_doubling), k_pcorr's own region:
-constexpr int kYyPitch = 388;       //   [16 frames][kYyPitch] (float4-aligned frame rows), kYyPitch rows of 16
-constexpr int kXx = kYy + kYyPitch;  // xx
+constexpr int kSf = kSc + 147;      // Syy before step 8k of the fine find_best_pitch, k < 37 (k_pcorr
+                                    //   walks the recurrence from there to the <= 10 lags it needs)
+constexpr int kSfCk = 37;
+constexpr int kXx = kSf + kSfCk;    // xx
 constexpr int kRows = kXx + 1;
 }  // namespace ptile
 

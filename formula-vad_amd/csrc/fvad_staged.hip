@@ -362,7 +362,7 @@ __device__ __forceinline__ float fir5_step(const float (&l)[5], float x, float &
 // the Syy recurrences' xf[n - 480] comes from a second filter over the x_lp
 // chunk 480 values back, staged like the current one.
 struct OutStage {
-  float sf[kLpStep][64];      // fine Syy rows
+  float sf[1][64];            // the fine Syy checkpoint of the chunk (i = n0 - 480, a multiple of 8)
   float sc[kLpStep / 2][64];  // coarse Syy rows
 };
 // rows row0 .. row0 + NR - 1 of the lane's quarter (qbase = its [row][16] block)
@@ -397,7 +397,7 @@ __device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, const
     }
     if (R == 3 || (R == 4 && u < kR4)) {
       const float yb = fir5_step(f.l, lp_value<LagFirst>(bcol, u, f.x0), f.b1, f.b2, f.b3, f.b4, f.b5);
-      ob.sf[u][lane] = f.Sf;
+      if (u == 0) ob.sf[0][lane] = f.Sf;  // k_pcorr walks from here to the lags it needs
       f.Sf += y * y - yb * yb;
       f.Sf = (1 > f.Sf) ? 1 : f.Sf;
       if ((u & 1) == 0) {
@@ -410,18 +410,17 @@ __device__ __forceinline__ void fir5_chunk(Fir5State &f, const float *col, const
   }
   if (R == 3 || R == 4) {
     wave_sync();
-    if (R == 3) {
-      flush_rows<kLpStep>(qbase, ptile::kSf + n0 - 480, ob.sf, lane);
+    flush_rows<1>(qbase, ptile::kSf + (n0 - 480) / kLpStep, ob.sf, lane);
+    if (R == 3)
       flush_rows<kLpStep / 2>(qbase, ptile::kSc + (n0 - 480) / 2, ob.sc, lane);
-    } else {
-      flush_rows<kR4>(qbase, ptile::kSf + n0 - 480, ob.sf, lane);
+    else
       flush_rows<(kR4 + 1) / 2>(qbase, ptile::kSc + (n0 - 480) / 2, ob.sc, lane);
-    }
     wave_sync();
   }
 }
 static_assert(384 % kLpStep == 0 && 480 % kLpStep == 0 && kLpStep % 2 == 0, "pass-2 regions");
 static_assert(480 % kLpStep == 0, "the lagged chunk is a whole chunk");
+static_assert(kLpStep == 8 && (294 + kLpStep - 1) / kLpStep == ptile::kSfCk, "fine Syy checkpoints every 8 lags");
 
 // Both passes walk their chunks through a register ring: the loads of the
 // next kLpPf chunks (pitch-buffer chunks and the Syy read-back) are in flight

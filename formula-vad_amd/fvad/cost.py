@@ -18,7 +18,8 @@ FRAME = 480
 # recounts them
 MEASURED = {"fine_lags_per_frame": 9.3352, "rd_cands_per_frame": 6.6061, "silent_frac": 0.004516,
             "frames_counted": 512000}
-PTILE_ROWS = 864 + 147 + 294 + 388 + 1  # k_plpc -> k_pcorr rows per frame (fvad_staged.h ptile)
+PTILE_ROWS = 8 + 147 + 37 + 1  # k_plpc -> k_pcorr rows per frame (fvad_staged.h ptile: FIR coefficients + x_lp[0],
+#   coarse Syy, fine Syy checkpoints, xx; xf is rebuilt by k_pcorr from the x_lp rows)
 
 
 def _fft960():
@@ -147,11 +148,12 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_fftAw": (p["analysis window + FFT A + scale"] + p["band energy Ex"] + 22 * 3 + dct_ly + xlp,
                    960 * 4 + spec + 22 * 4 * 2 + 4 + 240 * 4),
         # k_plpc: the frame's x_lp window (+ 2 pitch-buffer samples for x_lp[0])
-        # in; xf, the Syy sequences and xx out.
-        # k_pcorr: those in, yy_lookup (read back at <= 29 periods) and the
+        # in; the FIR coefficients, the coarse Syy sequence, the fine Syy
+        # checkpoints and xx out (r3: xf and yy_lookup no longer go through HBM).
+        # k_pcorr: the x_lp window + that tile row in (2 fine checkpoints), the
         # pitch record out
-        "k_plpc": (plpc, (864 + 2) * 4 + (PTILE_ROWS - 388) * 4),
-        "k_pcorr": (pitch - xlp - plpc - rd * 4, (864 + 147 + 10 + 1 + 385 + 29) * 4 + 80 * 4),
+        "k_plpc": (plpc, (864 + 2) * 4 + PTILE_ROWS * 4),
+        "k_pcorr": (pitch - xlp - plpc - rd * 4, (864 + 6 + 147 + 2 + 1) * 4 + 80 * 4),
         "k_select": (rd * 4 + rd * 12, 80 * 4 + 4),
         "k_pspecw": (p["pitch window + FFT + Ep + Exp"] + dct_exp, 960 * 4 + 2 * spec + 22 * 4 * 3 + 8 * 4 + 4),
         # k_rnn3: cepstral memory, spectral variability, GRU stack, gain
