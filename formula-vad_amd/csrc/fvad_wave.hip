@@ -44,6 +44,19 @@ __device__ __forceinline__ long long wave_next(const StagedArgs &a, WaveKernel k
   return wave_is_static(a, k) ? g + (long long)gridDim.x * kWNW : wave_take(a, slot, lane);
 }
 
+// A batch's frame indices, lane fr < kWB holding slot fr's frame (or -1),
+// computed once per batch: the frame loop reads them with readlane instead of
+// a per-frame ticks_valid load, whose wait also waited for every store the
+// wave still had in flight (gfx9 counts loads and stores in one vmcnt)
+__device__ __forceinline__ int batch_frames(const StagedArgs &a, long long g, int lane) {
+  return lane < kWB ? frame_of(a, g, kWB, lane) : -1;
+}
+__device__ __forceinline__ int lane_val(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// wait for v's load here, once per batch (a readlane of it inside the frame
+// loop would otherwise get a conservative wait that also drains the stores of
+// the frames before)
+__device__ __forceinline__ void settle(int v) { asm volatile("" ::"v"(v)); }
+
 // A per-iteration zero the compiler cannot see through: table reads indexed
 // with it stay inside the frame loop instead of being hoisted into registers
 // for the whole kernel (which would cost occupancy).
@@ -92,8 +105,9 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
   float *tr = reinterpret_cast<float *>(R);
   const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
   for (long long g = wave_first(a, kWaveFftA, kWorkFftA, lane); g < nb; g = wave_next(a, kWaveFftA, kWorkFftA, lane, g)) {
+    const int fl = batch_frames(a, g, lane);
     for (int fr = 0; fr < kWB; fr++) {
-      const int f = frame_of(a, g, kWB, fr);
+      const int f = lane_val(fl, fr);
       if (f < 0) continue;
       float2 v[16];
       const float *pb = frame_pb(a, f);
@@ -140,7 +154,7 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
     }
     // the Ly floor chain and the silence gate, lane per frame
     if (lane < kWB) {
-      const int f = frame_of(a, g, kWB, lane);
+      const int f = fl;
       if (f >= 0) {
         float *Ly = lyb[wv][lane];
         const float *Exl = exb[wv][lane];
@@ -163,7 +177,7 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
     wfft::wsync();
     for (int idx = lane; idx < kWB * kBands; idx += 64) {
       const int fr = idx / kBands, b = idx - fr * kBands;
-      const int f = frame_of(a, g, kWB, fr);
+      const int f = __shfl(fl, fr);
       if (f >= 0 && !silb[wv][fr]) {
         const float *Ly = lyb[wv][fr];
         float sum = 0;
@@ -192,15 +206,24 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
   float *tr = reinterpret_cast<float *>(R);
   const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
   for (long long g = wave_first(a, kWavePspec, kWorkPspec, lane); g < nb; g = wave_next(a, kWavePspec, kWorkPspec, lane, g)) {
+    // the batch's frames and their pitches, lane per frame
+    const int fl = batch_frames(a, g, lane);
+    const int pl = fl >= 0 ? a.pitch[fl] : 0;
+    settle(pl);
     for (int fr = 0; fr < kWB; fr++) {
-      const int f = frame_of(a, g, kWB, fr);
+      const int f = lane_val(fl, fr);
       if (f < 0) continue;
-      const int pit = a.pitch[f];
-      // X of bins < 400 (Exp terms), issued before the transform
+      const int pit = lane_val(pl, fr);
+      // X of bins < 400 (Exp terms) and the band's Ex, issued before the
+      // transform (Ex loaded after the P stores waited for them)
       float2 xr[7];
       const float2 *X = a.X + (size_t)f * kFreq;
 #pragma unroll
-      for (int r = 0; r < 7; r++) xr[r] = (64 * r + lane < 400) ? X[64 * r + lane] : make_float2(0, 0);
+      // (unconditional loads, lanes past the bins read bin 480 and are never
+      // used: a masked load's block would take its consumers, and their wait,
+      // right after it)
+      for (int r = 0; r < 7; r++) xr[r] = X[min(64 * r + lane, kFreq - 1)];
+      const float exl = a.Ex[(size_t)f * kBands + min(lane, kBands - 1)];
       float2 v[16];
       wave_window(frame_pb(a, f) + (kPitchBuf - kWin - pit), tb.hw, lane, v);
       wfft::run(v, tw, tb.tw, R, lane);
@@ -225,8 +248,7 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
       float e = 0;
       if (lane < kBands) {
         const size_t o = (size_t)f * kBands + lane;
-        const float ex = a.Ex[o];
-        e = (float)((double)expv / sqrt(.001 + (double)(ex * cv)));
+        e = (float)((double)expv / sqrt(.001 + (double)(exl * cv)));
         a.Ep[o] = cv;
         a.Exp[o] = e;
       }
@@ -262,22 +284,30 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
   float *rr = bp[wv][0], *nrm = bp[wv][1], *gsm = bp[wv][2];
   const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
   for (long long g = wave_first(a, kWaveSynth, kWorkSynth, lane); g < nb; g = wave_next(a, kWaveSynth, kWorkSynth, lane, g)) {
+    // the batch's frames and silence flags, lane per frame
+    const int fl = batch_frames(a, g, lane);
+    const int sl = fl >= 0 ? a.silence[fl] : 0;
+    settle(sl);
     for (int fr = 0; fr < kWB; fr++) {
-      const int f = frame_of(a, g, kWB, fr);
+      const int f = lane_val(fl, fr);
       if (f < 0) continue;
-      const bool fil = !a.silence[f];  // silent frames: X passes through
+      const bool fil = !lane_val(sl, fr);  // silent frames: X passes through
+      // every input of the frame in one batch of loads (each later load
+      // would also wait for the stores still in flight)
       const float2 *X = a.X + (size_t)f * kFreq;
       const float2 *P = a.P + (size_t)f * kFreq;
-      float2 xv[8];
+      // (unconditional: lanes past the 481 bins / 22 bands read the last
+      // one and are never used; a masked load's block would take its
+      // consumers, and their wait, right after it)
+      float2 xv[8], pv[8];
 #pragma unroll
-      for (int r = 0; r < 8; r++) xv[r] = (64 * r + lane < kFreq) ? X[64 * r + lane] : make_float2(0, 0);
+      for (int r = 0; r < 8; r++) xv[r] = X[min(64 * r + lane, kFreq - 1)];
+#pragma unroll
+      for (int r = 0; r < 8; r++) pv[r] = P[min(64 * r + lane, kFreq - 1)];
+      const size_t o = (size_t)f * kBands + min(lane, kBands - 1);
+      const float Exp = a.Exp[o], gg = a.gr[o], Ex = a.Ex[o], Ep = a.Ep[o], gs = a.gs[o];
       if (fil) {
-        float2 pv[8];
-#pragma unroll
-        for (int r = 0; r < 8; r++) pv[r] = (64 * r + lane < kFreq) ? P[64 * r + lane] : make_float2(0, 0);
         if (lane < kBands) {
-          const size_t o = (size_t)f * kBands + lane;
-          const float Exp = a.Exp[o], gg = a.gr[o], Ex = a.Ex[o], Ep = a.Ep[o];
           float r;
           if (Exp > gg)
             r = 1;
@@ -288,7 +318,7 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
           r = (float)sqrt((double)cl);
           r = (float)((double)r * sqrt((double)Ex / (1e-8 + (double)Ep)));
           rr[lane] = r;
-          gsm[lane] = a.gs[o];
+          gsm[lane] = gs;
         }
         wfft::wsync();
         // pitch filter X += r P; band terms of the filtered X
@@ -305,7 +335,7 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
         wfft::wsync();
         if (lane < kBands) {
           const float newE = band_chain(tr, tr + 400, T, lane);
-          nrm[lane] = (float)sqrt((double)a.Ex[(size_t)f * kBands + lane] / (1e-8 + (double)newE));
+          nrm[lane] = (float)sqrt((double)Ex / (1e-8 + (double)newE));
         }
         wfft::wsync();
 #pragma unroll
