@@ -422,44 +422,50 @@ static_assert(384 % kLpStep == 0 && 480 % kLpStep == 0 && kLpStep % 2 == 0, "pas
 static_assert(480 % kLpStep == 0, "the lagged chunk is a whole chunk");
 static_assert(kLpStep == 8 && (294 + kLpStep - 1) / kLpStep == ptile::kSfCk, "fine Syy checkpoints every 8 lags");
 
-// Both passes walk their chunks through a register ring: the loads of the
-// next kLpPf chunks (pitch-buffer chunks and the Syy read-back) are in flight
-// while a chunk is summed; the chunk loops are unrolled by the ring depth so
-// ring slots are static registers (depths 1-4 measured alike; 1 kept).
+// x_lp chunks in flight per pass (the ring depth)
 #ifndef FVAD_PLPC_OCC
 #define FVAD_PLPC_OCC 2
 #endif
 #ifndef FVAD_LP_PF
-#define FVAD_LP_PF 1
+#define FVAD_LP_PF 4
 #endif
 constexpr int kLpPf = FVAD_LP_PF;
 static_assert(kLpChunks % kLpPf == 0, "prefetch ring must divide the passes");
 
-// One pass over a tile's pitch-buffer chunks: chunk c is staged and handed
-// to body(c, slot) while the loads of chunks c + 1 .. c + kLpPf are in flight;
-// pre(c, slot) issues the pass's own extra loads for chunk c into ring slot
-// `slot` (kLpPf chunks ahead of its use).
-template <typename Pre, typename Body>
-__device__ __forceinline__ void lp_walk(const LpSrc &src, float *stg, int lane, Pre &&pre, Body &&body) {
-  float4 pf[kLpPf][kLpPR];
+// pass-1 state of one lane (k_plpc): _celt_autocorr's 5 lag sums, the tail
+// sums of lags 1..3 and the last 4 x_lp values
+struct AcState {
+  float acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, acc4 = 0;
+  float d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+  float h1 = 0, h2 = 0, h3 = 0, h4 = 0;
+};
+// One chunk of pass 1 (lag k: sum_{i<860} x[i] x[i+k], then the tail).
+// Kind 0: the first chunk (x_lp[0] = x0, lags start at their first term),
+// 1: a middle chunk, 2: the last (n = 856..863: term i = n - k belongs to the
+// 860-term sum while i < 860, else (n >= 860 + k) to the tail sum of x[n] x[n-k])
+template <int Kind>
+__device__ __forceinline__ void ac_chunk(AcState &s, const float *col, float x0, int c) {
 #pragma unroll
-  for (int d = 0; d < kLpPf; d++) {
-    lp_fetch(src, d, pf[d]);
-    pre(d, d);
-  }
-  for (int c0 = 0; c0 < kLpChunks; c0 += kLpPf) {
-#pragma unroll
-    for (int dd = 0; dd < kLpPf; dd++) {
-      const int c = c0 + dd;
-      lp_stage(stg, lane, pf[dd]);
-      // the ring slot is free once staged: its next chunk loads during body(c)
-      // (issued after the body instead: 0.92 vs 0.90 ms)
-      if (c + kLpPf < kLpChunks) lp_fetch(src, c + kLpPf, pf[dd]);
-      body(c, dd);
-      if (c + kLpPf < kLpChunks) pre(c + kLpPf, dd);
+  for (int u = 0; u < kLpStep; u++) {
+    const float x = lp_value<Kind == 0>(col, u, x0);
+    if (Kind == 2) {
+      const int n = c * kLpStep + u;
+      if (n < 860) s.acc0 = s.acc0 + x * x; else s.d0 = s.d0 + x * x;
+      if (n - 1 < 860) s.acc1 = s.acc1 + s.h1 * x; else s.d1 = s.d1 + x * s.h1;
+      if (n - 2 < 860) s.acc2 = s.acc2 + s.h2 * x; else s.d2 = s.d2 + x * s.h2;
+      if (n - 3 < 860) s.acc3 = s.acc3 + s.h3 * x; else s.d3 = s.d3 + x * s.h3;
+      s.acc4 = s.acc4 + s.h4 * x;  // n - 4 <= 859
+    } else {
+      s.acc0 = s.acc0 + x * x;
+      if (Kind == 1 || u >= 1) s.acc1 = s.acc1 + s.h1 * x;
+      if (Kind == 1 || u >= 2) s.acc2 = s.acc2 + s.h2 * x;
+      if (Kind == 1 || u >= 3) s.acc3 = s.acc3 + s.h3 * x;
+      if (Kind == 1 || u >= 4) s.acc4 = s.acc4 + s.h4 * x;
     }
+    s.h4 = s.h3, s.h3 = s.h2, s.h2 = s.h1, s.h1 = x;
   }
 }
+static_assert(kLpChunks * kLpStep == 864 && (kLpChunks - 1) * kLpStep == 856, "pass-1 tail chunk");
 
 __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
   __shared__ float stg_all[4][2][kLpRows * kLpCols];
@@ -505,91 +511,72 @@ __global__ void __launch_bounds__(256, FVAD_PLPC_OCC) k_plpc(StagedArgs a) {
     float *qbase = out - (lane & 15);
     RSTAMP(3);
 
-    // pass 1: x_lp -> _celt_autocorr (lag k: sum_{i<860} x[i] x[i+k], then the tail)
-    float acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, acc4 = 0;
-    float d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-    float h1 = 0, h2 = 0, h3 = 0, h4 = 0;
-    lp_walk(
-        src, stg, lane, [&](int, int) {},
-        [&](int c, int) {
-          if (c == 0) {
+    // Both passes walk the x_lp chunks through a register ring: chunk c is
+    // staged while the loads of chunks c + 1 .. c + kLpPf are in flight (the
+    // chunk loops unrolled by the ring depth, so slots are static registers)
+    float4 pf[kLpPf][kLpPR];
+    // pass 1: x_lp -> _celt_autocorr
+    AcState as;
 #pragma unroll
-            for (int u = 0; u < kLpStep; u++) {
-              const float x = lp_value<true>(col, u, x0);
-              acc0 = acc0 + x * x;
-              if (u >= 1) acc1 = acc1 + h1 * x;
-              if (u >= 2) acc2 = acc2 + h2 * x;
-              if (u >= 3) acc3 = acc3 + h3 * x;
-              if (u >= 4) acc4 = acc4 + h4 * x;
-              h4 = h3, h3 = h2, h2 = h1, h1 = x;
-            }
-          } else if (c + 1 < kLpChunks) {
+    for (int d = 0; d < kLpPf; d++) lp_fetch(src, d, pf[d]);
+    for (int c0 = 0; c0 < kLpChunks; c0 += kLpPf) {
 #pragma unroll
-            for (int u = 0; u < kLpStep; u++) {
-              const float x = lp_value<false>(col, u, x0);
-              acc0 = acc0 + x * x;
-              acc1 = acc1 + h1 * x;
-              acc2 = acc2 + h2 * x;
-              acc3 = acc3 + h3 * x;
-              acc4 = acc4 + h4 * x;
-              h4 = h3, h3 = h2, h2 = h1, h1 = x;
-            }
-          } else {
-            // n = 856..863: term i = n - k belongs to the 860-term sum while
-            // i < 860, else (n >= 860 + k) to the tail sum of x[n] x[n-k]
-#pragma unroll
-            for (int u = 0; u < kLpStep; u++) {
-              const int n = c * kLpStep + u;
-              const float x = lp_value<false>(col, u, x0);
-              if (n < 860) acc0 = acc0 + x * x; else d0 = d0 + x * x;
-              if (n - 1 < 860) acc1 = acc1 + h1 * x; else d1 = d1 + x * h1;
-              if (n - 2 < 860) acc2 = acc2 + h2 * x; else d2 = d2 + x * h2;
-              if (n - 3 < 860) acc3 = acc3 + h3 * x; else d3 = d3 + x * h3;
-              acc4 = acc4 + h4 * x;  // n - 4 <= 859
-              h4 = h3, h3 = h2, h2 = h1, h1 = x;
-            }
-          }
-        });
+      for (int dd = 0; dd < kLpPf; dd++) {
+        const int c = c0 + dd;
+        lp_stage(stg, lane, pf[dd]);
+        if (c + kLpPf < kLpChunks) lp_fetch(src, c + kLpPf, pf[dd]);
+        if (c == 0)
+          ac_chunk<0>(as, col, x0, c);
+        else if (c + 1 < kLpChunks)
+          ac_chunk<1>(as, col, x0, c);
+        else
+          ac_chunk<2>(as, col, x0, c);
+      }
+    }
     RSTAMP(0);
-    float acv[5] = {acc0 + d0, acc1 + d1, acc2 + d2, acc3 + d3, acc4 + 0.0f};
+    float acv[5] = {as.acc0 + as.d0, as.acc1 + as.d1, as.acc2 + as.d2, as.acc3 + as.d3, as.acc4 + 0.0f};
     float l[5];
     lpc_fir5_coeffs(acv, l);
 
     // pass 2: x_lp again -> celt_fir5 -> xf; Syy initial sums, xx; from
     // n = 480 on, the Syy recurrences with xf[n - 480] from a second filter
-    // over the x_lp chunk 480 values back (loaded kLpPf chunks ahead, staged in
-    // the wave's second column).  The chunk body is specialised per region of
-    // n, so it has no branches.
+    // over the x_lp chunk 480 values back (a second ring, staged in the
+    // wave's second column).  The chunk body is specialised per region of n,
+    // so it has no branches.
     Fir5State fs;
     fs.x0 = x0;
 #pragma unroll
     for (int i = 0; i < 5; i++) fs.l[i] = l[i];
-    float4 bk[kLpPf][kLpPR];
     const float *bcol = stgb + lane;
-    lp_walk(
-        src, stg, lane,
-        [&](int c, int slot) {
-          const int n0 = c * kLpStep;
-          if (n0 >= 480 && n0 < 480 + 294) lp_fetch(src, c - 480 / kLpStep, bk[slot]);
-        },
-        [&](int c, int slot) {
-          const int n0 = c * kLpStep;
-          if (n0 >= 480 && n0 < 480 + 294) lp_stage(stgb, lane, bk[slot]);
-          if (c == 0)
-            fir5_chunk<true, 1, false>(fs, col, bcol, qbase, n0, ob, lane);
-          else if (n0 < 384)
-            fir5_chunk<false, 1, false>(fs, col, bcol, qbase, n0, ob, lane);
-          else if (n0 < 480)
-            fir5_chunk<false, 2, false>(fs, col, bcol, qbase, n0, ob, lane);
-          else if (n0 == 480)
-            fir5_chunk<false, 3, true>(fs, col, bcol, qbase, n0, ob, lane);
-          else if (n0 + kLpStep <= 480 + 294)
-            fir5_chunk<false, 3, false>(fs, col, bcol, qbase, n0, ob, lane);
-          else if (n0 < 480 + 294)
-            fir5_chunk<false, 4, false>(fs, col, bcol, qbase, n0, ob, lane);
-          else
-            fir5_chunk<false, 5, false>(fs, col, bcol, qbase, n0, ob, lane);
-        });
+    constexpr int kLag = 480 / kLpStep;  // chunks between a value and its lagged partner
+    auto lagged = [](int c) { return c * kLpStep >= 480 && c * kLpStep < 480 + 294; };
+    float4 bk[kLpPf][kLpPR];
+#pragma unroll
+    for (int d = 0; d < kLpPf; d++) lp_fetch(src, d, pf[d]);
+    for (int c0 = 0; c0 < kLpChunks; c0 += kLpPf) {
+#pragma unroll
+      for (int dd = 0; dd < kLpPf; dd++) {
+        const int c = c0 + dd, n0 = c * kLpStep;
+        lp_stage(stg, lane, pf[dd]);
+        if (c + kLpPf < kLpChunks) lp_fetch(src, c + kLpPf, pf[dd]);
+        if (lagged(c)) lp_stage(stgb, lane, bk[dd]);
+        if (lagged(c + kLpPf)) lp_fetch(src, c + kLpPf - kLag, bk[dd]);
+        if (c == 0)
+          fir5_chunk<true, 1, false>(fs, col, bcol, qbase, n0, ob, lane);
+        else if (n0 < 384)
+          fir5_chunk<false, 1, false>(fs, col, bcol, qbase, n0, ob, lane);
+        else if (n0 < 480)
+          fir5_chunk<false, 2, false>(fs, col, bcol, qbase, n0, ob, lane);
+        else if (n0 == 480)
+          fir5_chunk<false, 3, true>(fs, col, bcol, qbase, n0, ob, lane);
+        else if (n0 + kLpStep <= 480 + 294)
+          fir5_chunk<false, 3, false>(fs, col, bcol, qbase, n0, ob, lane);
+        else if (n0 < 480 + 294)
+          fir5_chunk<false, 4, false>(fs, col, bcol, qbase, n0, ob, lane);
+        else
+          fir5_chunk<false, 5, false>(fs, col, bcol, qbase, n0, ob, lane);
+      }
+    }
     RSTAMP(1);
     out[ptile::kXx * ptile::kQuarter] = fs.xx;
     // k_pcorr's xf: the FIR coefficients and x_lp[0]
