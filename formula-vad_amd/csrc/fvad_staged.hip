@@ -77,6 +77,11 @@ __host__ __device__ constexpr int prep_streams(int C) { return kPrepSlots / C < 
 #define FVAD_PREP_RING 8
 #endif
 constexpr int kPrepRing = FVAD_PREP_RING;  // float4 loads in flight per lane
+// blocks per trip of the chain loop: the compiler's wait at the loop header
+// drains every load and store in flight, so it is paid once per trip
+#ifndef FVAD_PREP_UNROLL
+#define FVAD_PREP_UNROLL 4
+#endif
 static_assert((kFrame / 4) % kPrepRing == 0, "prep ring must divide a frame");
 
 // One lane walks its stream's input in blocks of kPrepRing float4 chunks: per
@@ -116,6 +121,7 @@ __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, f
   // over the stream's channels in channel order
   float sum = 0, vmin = 1, vmax = 0;
   int jt = 0, t = 0;  // chunk within the tick, tick
+#pragma unroll FVAD_PREP_UNROLL
   for (int b = 0; b < nb; b++) {
     if (rn == bpt && b + 1 < nb) {
       rn = 0;
@@ -155,29 +161,44 @@ __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, f
   }
 }
 
+typedef float f4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(64) k_prep3(StagedArgs a) {
   const int tid = threadIdx.x, lane = tid;
   const int C = a.n_channels, S = prep_streams(C), sb = blockIdx.x * S;
   const int ns = min(S, a.n_streams - sb);  // streams in this workgroup
   if (ns <= 0) return;
   // pitch history of every stream -> xs[s][0..1248), and its x_lp values
-  // (the first frame's x_lp[1..623]; k_fftAw writes the rest): one stream at a
-  // time, each lane's loads independent (unrolled), so the copies take a few
-  // memory latencies per stream rather than one per element
-  for (int s = 0; s < ns; s++) {
-    if (ticks_of(a, sb + s) == 0) continue;
-    const float *h = a.state + (size_t)(sb + s) * st::kWords + st::kPitch + kFrame;
-    float4 *x = reinterpret_cast<float4 *>(a.xs + (size_t)(sb + s) * a.L);
+  // (the first frame's x_lp[1..623]; k_fftAw writes the rest): flat over the
+  // workgroup's streams, each lane's loads in batches of 8 before their
+  // stores (a stream with no ticks gets a copy nobody reads)
+  {
+    constexpr int kH4 = kHist / 4, B = 8;
+    f4 v[B];  // (a native vector: arrays of float4 structs stayed in scratch)
+    float w[B];
+    for (int i0 = 0; i0 < ns * kH4; i0 += 64 * B) {
 #pragma unroll
-    for (int j = 0; j < (kHist / 4 + 63) / 64; j++) {
-      const int i = lane + 64 * j;
-      if (i < kHist / 4) x[i] = reinterpret_cast<const float4 *>(h)[i];
+      for (int u = 0; u < B; u++) {  // (clamped: every load unconditional)
+        const int i = min(i0 + lane + 64 * u, ns * kH4 - 1), s = i / kH4, j = i - s * kH4;
+        v[u] = reinterpret_cast<const f4 *>(a.state + (size_t)(sb + s) * st::kWords + st::kPitch + kFrame)[j];
+      }
+#pragma unroll
+      for (int u = 0; u < B; u++) {
+        const int i = i0 + lane + 64 * u, s = i / kH4, j = i - s * kH4;
+        if (i < ns * kH4) reinterpret_cast<f4 *>(a.xs + (size_t)(sb + s) * a.L)[j] = v[u];
+      }
     }
-    float *xl = a.xlp + (size_t)(sb + s) * a.LX;
+    for (int i0 = 0; i0 < ns * kXlpHist; i0 += 64 * B) {
 #pragma unroll
-    for (int j = 0; j < (kXlpHist + 63) / 64; j++) {
-      const int m = lane + 64 * j;
-      if (m > 0 && m < kXlpHist) xl[m] = xlp_value(h[2 * m - 1], h[2 * m], h[2 * m + 1]);
+      for (int u = 0; u < B; u++) {
+        const int i = min(i0 + lane + 64 * u, ns * kXlpHist - 1), s = i / kXlpHist, m = max(i - s * kXlpHist, 1);
+        const float *h = a.state + (size_t)(sb + s) * st::kWords + st::kPitch + kFrame;
+        w[u] = xlp_value(h[2 * m - 1], h[2 * m], h[2 * m + 1]);
+      }
+#pragma unroll
+      for (int u = 0; u < B; u++) {
+        const int i = i0 + lane + 64 * u, s = i / kXlpHist, m = i - s * kXlpHist;
+        if (i < ns * kXlpHist && m > 0) a.xlp[(size_t)(sb + s) * a.LX + m] = w[u];
+      }
     }
   }
   {
@@ -199,16 +220,24 @@ __global__ void __launch_bounds__(64) k_prep3(StagedArgs a) {
     }
   }
   __syncthreads();
-  // pitch_buf after the last frame = the last 1728 samples of the row
-  for (int s = 0; s < ns; s++) {
-    const int nt = ticks_of(a, sb + s);
-    if (nt == 0) continue;
-    const float4 *x = reinterpret_cast<const float4 *>(a.xs + (size_t)(sb + s) * a.L + (size_t)(nt * C - 1) * kFrame);
-    float4 *h = reinterpret_cast<float4 *>(a.state + (size_t)(sb + s) * st::kWords + st::kPitch);
+  // pitch_buf after the last frame = the last 1728 samples of the row (flat
+  // over the workgroup's streams, as the history copies)
+  {
+    constexpr int kP4 = kPitchBuf / 4, B = 8;
+    f4 v[B];
+    for (int i0 = 0; i0 < ns * kP4; i0 += 64 * B) {
 #pragma unroll
-    for (int j = 0; j < (kPitchBuf / 4 + 63) / 64; j++) {
-      const int i = lane + 64 * j;
-      if (i < kPitchBuf / 4) h[i] = x[i];
+      for (int u = 0; u < B; u++) {
+        const int i = min(i0 + lane + 64 * u, ns * kP4 - 1), s = i / kP4, j = i - s * kP4;
+        const int nt = max(ticks_of(a, sb + s), 1);
+        v[u] = reinterpret_cast<const f4 *>(a.xs + (size_t)(sb + s) * a.L + (size_t)(nt * C - 1) * kFrame)[j];
+      }
+#pragma unroll
+      for (int u = 0; u < B; u++) {
+        const int i = i0 + lane + 64 * u, s = i / kP4, j = i - s * kP4;
+        const int nt = i < ns * kP4 ? ticks_of(a, sb + s) : 0;
+        if (nt > 0) reinterpret_cast<f4 *>(a.state + (size_t)(sb + s) * st::kWords + st::kPitch)[j] = v[u];
+      }
     }
   }
 }
