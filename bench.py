@@ -420,7 +420,8 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks):
     """Roofline of the dominant kernel, per launch, from HIP events recorded
     around each kernel on the stream it runs on (fvad_engine_kernel_times; at
     N > 1 the max over ranks), plus the whole path against SURVEY.md 8(d)'s
-    ceilings."""
+    ceilings.  The engine records the events on every 4th timed push
+    (FVAD_EVENT_EVERY): on every push their markers cost it ~1 %."""
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     frames_launch = B * Ch * T
     if args.mode == "fused":
@@ -430,6 +431,9 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks):
                              "bytes": cost.frame_kernel_bytes(B, Ch, T) / frames_launch}}
     else:
         per_k = cost.staged_kernels(Ch)
+    if not any(ms > 0 for ms in kt["kernels"].values()):
+        # FVAD_NO_EVENTS=1 (diagnostic): no per-kernel events were recorded
+        return {"bound": None, "note": "no kernel timing events (FVAD_NO_EVENTS=1)", "kernels": {}}
     # bit-exact C-order sums: no product may fuse with its sum (-ffp-contract=off),
     # so a flop is one lane-op and the attainable FP32 VALU rate is half the
     # FMA-counted 157.3 TFLOP/s; a kernel is VALU-bound when its intensity
@@ -514,6 +518,7 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks):
             ", ".join("%s %s" % kv for kv in cost.MEASURED.items())),
         "kernel_ms_avg": round(kt["kernels"][dom], 4), "push_ms_avg": round(kt["total_ms"], 4),
         "timed_launches": kt["runs"],
+        "event_sampling": "events on every %s-th timed push" % os.environ.get("FVAD_EVENT_EVERY", "4"),
         "path": path,
         "kernels": kernels,
     }

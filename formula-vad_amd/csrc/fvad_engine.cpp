@@ -115,7 +115,7 @@ struct fvad_engine {
   bool slot_pending[2] = {false, false};
   double ms_sum[FVAD_MAX_TIMES] = {};
   int n_timed = 0;
-  bool timing_pending = false;  // unused (kept for layout clarity)
+  int res_count = 0;  // run_resident calls since the last clear_times (event sampling)
   int raw_s16 = 0;  // rnnoise compat mode (s16-scaled I/O)
   unsigned long long *d_stamps = nullptr;
   unsigned *d_work = nullptr;  // staged: persistent-kernel group counters  // diagnostic stamp buffer (FVAD_STAMPS builds)
@@ -1063,12 +1063,19 @@ extern "C" int fvad_engine_run_resident(fvad_engine *e, int n_ticks) {
   } else {
     e->d_pcm = e->d_pcm_b[0];
   }
-  // FVAD_NO_EVENTS=1: no timing events (diagnostic: their cost on the push)
+  // Timing events on every FVAD_EVENT_EVERY-th push (default 4: the 15
+  // event markers of a push cost it ~1 %, measured); FVAD_NO_EVENTS=1: none
   static const bool no_events = [] {
     const char *v = getenv("FVAD_NO_EVENTS");
     return v && atoi(v) == 1;
   }();
-  if ((rc = launch(e, n_ticks, false, !no_events))) return rc;
+  static const int every = [] {
+    const char *v = getenv("FVAD_EVENT_EVERY");
+    const int n = v ? atoi(v) : 4;
+    return n < 1 ? 1 : n;
+  }();
+  const bool timed = !no_events && e->res_count++ % every == 0;
+  if ((rc = launch(e, n_ticks, false, timed))) return rc;
   // a later submit / push must not overwrite buffer 0 under this run's prep
   if (e->res_pushes <= 1) {
     HIP_TRY(hipEventRecord(e->ev_in_free[0], input_reader(e)));
@@ -1113,6 +1120,7 @@ extern "C" int fvad_engine_clear_times(fvad_engine *e) {
   e->vadm_ms_sum = 0;
   e->vadm_timed = 0;
   e->n_timed = 0;
+  e->res_count = 0;
   return FVAD_OK;
 }
 
