@@ -339,6 +339,7 @@ extern "C" int fvad_engine_reset(fvad_engine *e) {
     if (rc) return rc;
   }
   HIP_TRY(hipMemsetAsync(e->d_state, 0, sizeof(float) * fvad::st::kWords * (size_t)e->cfg.n_streams, e->stream));
+  if (e->d_work) HIP_TRY(hipMemsetAsync(e->d_work, 0, sizeof(unsigned) * fvad::kWorkCounters, e->stream));
   HIP_TRY(hipMemsetAsync(e->d_ring, 0,
                          sizeof(float) * (size_t)e->ring_len * e->cfg.n_channels * e->cfg.n_streams, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));

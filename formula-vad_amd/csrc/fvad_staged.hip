@@ -660,6 +660,11 @@ __device__ __forceinline__ void sel_load(SelRec &r, const float *__restrict__ ro
 
 __global__ void __launch_bounds__(64) k_select(StagedArgs a) {
   const int lane = threadIdx.x, sl = lane >> 4, k = lane & 15;
+  // the persistent kernels' group counters: those of this push's k_fftAw /
+  // k_plpc / k_pcorr are done with (they ran before), the rest are used after
+  // this kernel; zeroed here instead of by a memset node of their own
+  static_assert(kWorkSlots * kQueues <= 64, "one lane per counter");
+  if (blockIdx.x == 0 && lane < kWorkSlots * kQueues) a.work[lane] = 0;
   const int s = blockIdx.x * kSelStreams + sl;
   const bool sok = s < a.n_streams;
   const int nf = sok ? ticks_of(a, s) * a.n_channels : 0;
@@ -1808,8 +1813,9 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   const long long frames = (long long)a.n_streams * a.V;
   auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
   (void)hipGetLastError();
+  // a.work: zero when the engine is created, then reset by every push's
+  // k_select for the next (the kernels before it) and this push (after it)
   static_assert(kWorkSlots * kQueues <= kWorkCounters, "work counters");
-  FVAD_LAUNCH_TRY(hipMemsetAsync(a.work, 0, kWorkSlots * kQueues * sizeof(unsigned), stream));
 #define REC(k) \
   if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[k], stream))
   // k_fftAw and the pitch branch (k_plpc -> k_pcorr -> k_select) both only
