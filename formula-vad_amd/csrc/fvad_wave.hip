@@ -77,14 +77,26 @@ __device__ __forceinline__ void wave_tabs_load(WaveTabs &w, const Plan *__restri
   for (int i = tid; i < kFrame; i += 64 * kWNW) w.hw[i] = P->half_window[i];
 }
 
-// layout-A input of a 960-sample analysis window at pb (x * w / 960, imag 0)
-__device__ __forceinline__ void wave_window(const float *__restrict__ pb, const float *hw, int lane,
-                                            float2 (&v)[16]) {
+// A frame's raw window samples.  k_pspecw loads them one frame ahead (the
+// transform needs them first thing: without the prefetch each frame waited a
+// memory latency on them, 0.07 ms of k_pspecw's 0.55 and 0.1 of k_fftAw's
+// 0.66, measured by a build that skipped the loads; k_fftAw, at 141 VGPRs,
+// gained nothing from the same prefetch at its 168-register limit)
+struct WinRaw {
+  float x[16];
+};
+__device__ __forceinline__ void win_load(WinRaw &w, const float *__restrict__ pb, int lane) {
+#pragma unroll
+  for (int k = 0; k < 16; k++) w.x[k] = lane < 60 ? pb[wfft::in_index(lane, k)] : 0.0f;
+}
+// layout-A input of a 960-sample analysis window from its prefetched samples
+// (x * w / 960, imag 0)
+__device__ __forceinline__ void win_apply(const WinRaw &w, const float *hw, int lane, float2 (&v)[16]) {
   hw += opaque0();
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     const int i = wfft::in_index(lane, k);
-    float val = lane < 60 ? pb[i] : 0.0f;
+    float val = w.x[k];
     val *= lane < 60 ? win960(hw, i) : 0.0f;
     v[k] = make_float2(kScale960 * val, kScale960 * 0.0f);
   }
@@ -123,7 +135,9 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
         qa = *reinterpret_cast<const float4 *>(q);
         qb = *reinterpret_cast<const float4 *>(q + 4);
       }
-      wave_window(pb + (kPitchBuf - kWin), tb.hw, lane, v);
+      WinRaw w;
+      win_load(w, pb + (kPitchBuf - kWin), lane);
+      win_apply(w, tb.hw, lane, v);
       wfft::run(v, tw, tb.tw, R, lane);
       float2 *X = a.X + (size_t)f * kFreq;
 #pragma unroll
@@ -210,9 +224,14 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
     const int fl = batch_frames(a, g, lane);
     const int pl = fl >= 0 ? a.pitch[fl] : 0;
     settle(pl);
-    for (int fr = 0; fr < kWB; fr++) {
+    auto pwin = [&](int f, int fr) { return frame_pb(a, f) + (kPitchBuf - kWin - lane_val(pl, fr)); };
+    // frames in pairs, two sets of window registers: frame fr + 1's samples
+    // load while frame fr is transformed
+    auto frame = [&](int fr, WinRaw &cur, WinRaw &nxt) __attribute__((always_inline)) {
+      const int fn = fr + 1 < kWB ? lane_val(fl, fr + 1) : -1;
+      if (fn >= 0) win_load(nxt, pwin(fn, fr + 1), lane);
       const int f = lane_val(fl, fr);
-      if (f < 0) continue;
+      if (f < 0) return;
       const int pit = lane_val(pl, fr);
       // X of bins < 400 (Exp terms) and the band's Ex, issued before the
       // transform (Ex loaded after the P stores waited for them)
@@ -225,7 +244,7 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
       for (int r = 0; r < 7; r++) xr[r] = X[min(64 * r + lane, kFreq - 1)];
       const float exl = a.Ex[(size_t)f * kBands + min(lane, kBands - 1)];
       float2 v[16];
-      wave_window(frame_pb(a, f) + (kPitchBuf - kWin - pit), tb.hw, lane, v);
+      win_apply(cur, tb.hw, lane, v);
       wfft::run(v, tw, tb.tw, R, lane);
       float2 *P = a.P + (size_t)f * kFreq;
 #pragma unroll
@@ -265,6 +284,17 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
         a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pit - 300));
       }
       wfft::wsync();
+    };
+    WinRaw wa, wb;
+    {
+      const int f0 = lane_val(fl, 0);
+      if (f0 >= 0) win_load(wa, pwin(f0, 0), lane);
+    }
+    static_assert(kWB % 2 == 0, "frame pairs");
+#pragma unroll 1
+    for (int fr = 0; fr < kWB; fr += 2) {
+      frame(fr, wa, wb);
+      frame(fr + 1, wb, wa);
     }
   }
 }
