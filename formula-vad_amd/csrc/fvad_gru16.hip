@@ -380,7 +380,8 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
   int maxnf = 0;
 #pragma unroll
   for (int s = 0; s < S; s++) maxnf = max(maxnf, L.nfs[s]);
-  // raw feature lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (as 1.0 / 0.0)
+  // raw feature lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (the flag's
+  // bits, nonzero = silent: no wait for the load where it is issued)
   const int pfs = tid / kPfW, pfi = tid - pfs * kPfW;
   const bool pf_lane = tid < S * kPfW;
   auto fetch = [&](int v) -> float {
@@ -388,14 +389,14 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     const long long f = L.fbase[pfs] + v;
     if (pfi < kBands) return a.Lyf[f * kBands + pfi];
     if (pfi < kBands + 7) return a.f34[f * 8 + (pfi - kBands)];
-    return a.silence[f] ? 1.0f : 0.0f;
+    return __int_as_float(a.silence[f]);
   };
   // features of frame f from L.pf (k_rnn3's F-C: cepstral memory, deltas,
   // 34..40, the new distance row) into feature version f % 5; item (s, i)
   auto feat_c = [&](int f, int idx) {
     const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
     const bool valid = f < L.nfs[s];
-    const bool on = valid && L.pf[s][kPfW - 1] == 0.0f;
+    const bool on = valid && __float_as_int(L.pf[s][kPfW - 1]) == 0;
     if (i == 0) {
       L.act[f & 7][s] = on;
       if (valid && !on) a.vadf[L.fbase[s] + f] = 0;  // silent: X passes through, state untouched
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
           feat_c(u + 1, (k / kLight) * kIt + k % kLight);
     }
     WSTAMP_END(0);
-    __syncthreads();
+    lds_sync();
     RSTAMP(0);
     WSTAMP_BEGIN();
     // ---- phase B: candidates of vad(u-1), noise(u-2), denoise(u-3); gains(u-4);
@@ -584,7 +585,7 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     }
     if (pf_lane) L.pf[pfs][pfi] = pf_next;  // read by the next phase A only
     WSTAMP_END(1);
-    __syncthreads();
+    lds_sync();
     RSTAMP(1);
   }
 #ifdef FVAD_STAMPS

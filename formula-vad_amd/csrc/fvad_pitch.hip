@@ -517,6 +517,11 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     // wave's serial walk carries 3 or 1 chains instead of 4.
     const bool q5b = tq >= 128;
     const int q5i = q5b ? tq - 128 : tq;
+    // the next group is taken here, so the atomic's round trip hides under
+    // the walks; published through LDS at the group's end, whose barrier then
+    // waits for LDS only (not for this group's record stores)
+    long long g_next = 0;
+    if (tq == 0) g_next = take_group(a, kWorkPcorr);
 #if FVAD_Q5_COMPACT
     // items packed in frame order from lane 0 (window items c = 0..nv on
     // waves 0-1, T1b items c = 1..nv on waves 2-3): ~7.6 items per frame fill
@@ -639,8 +644,8 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         qk[4] = __int_as_float(off);
       }
     }
-    if (tq == 0) gq = take_group(a, kWorkPcorr);
-    __syncthreads();
+    if (tq == 0) gq = g_next;
+    lds_sync();
     RSTAMP(5);
     g = gq;
   }

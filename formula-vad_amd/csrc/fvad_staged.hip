@@ -879,10 +879,15 @@ __device__ __forceinline__ void rnn_gates(const int8_t *W, const RnnIn &in, cons
 }
 
 // GRU candidate of image matrix m: sum = b + sum_j w*in[j] + sum_j (w*state[j])*r[j];
-// new[c][s] = z*state + (1-z)*act(kWs*sum) for active streams, state otherwise
-template <int m, int S, int G, int NT>
+// new[c][s] = z*state + (1-z)*act(kWs*sum) for active streams, state otherwise.
+// The sum's input prefix (b + the input terms) does not depend on the reset
+// gate, so it can run one phase early: PART 1 stores the prefix to preT
+// ([c][S]) and returns, PART 2 starts from preT and adds the recurrent terms
+// -- the same sequence of f32 adds as PART 0, split at a store.
+template <int m, int S, int G, int NT, int PART = 0>
 __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const float *stT, const float *zrT,
-                                         float *newT, const int *actv, int act, const float *tt, int tid) {
+                                         float *newT, const int *actv, int act, const float *tt, int tid,
+                                         float *preT = nullptr) {
   constexpr int SL = S / G, cols = rnnimg::kCols[m], N = cols;
   constexpr int ob = rnnimg::off_b(m), ow = rnnimg::off_w(m), ws = rnnimg::stride(m);
   constexpr int gst = (m == 2) ? 1 : 3;
@@ -890,10 +895,31 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
     const int c = t / G, s0 = (t - c * G) * SL;
     const int8_t *wc = W + ow + c * ws;
     float acc[SL];
-    const float b = (float)W[ob + c];
+    if constexpr (PART == 2) {
+      const typename VecT<SL>::T p = *reinterpret_cast<const typename VecT<SL>::T *>(preT + c * S + s0);
+      acc[0] = p.x;
+      acc[1] = p.y;
+      if constexpr (SL == 4) {
+        acc[2] = p.z;
+        acc[3] = p.w;
+      }
+    } else {
+      const float b = (float)W[ob + c];
 #pragma unroll
-    for (int q = 0; q < SL; q++) acc[q] = b;
-    rnn_inputs<m, S, SL>(wc, in, s0, acc);
+      for (int q = 0; q < SL; q++) acc[q] = b;
+      rnn_inputs<m, S, SL>(wc, in, s0, acc);
+    }
+    if constexpr (PART == 1) {
+      typename VecT<SL>::T p;
+      p.x = acc[0];
+      p.y = acc[1];
+      if constexpr (SL == 4) {
+        p.z = acc[2];
+        p.w = acc[3];
+      }
+      *reinterpret_cast<typename VecT<SL>::T *>(preT + c * S + s0) = p;
+      continue;
+    }
     mv_seg_r<rnnimg::kSegs[m][gst], S, SL>(wc + rnnimg::seg_off(m, gst), stT, zrT + N * S, s0, acc);
 #pragma unroll
     for (int q = 0; q < SL; q++) {
@@ -923,6 +949,7 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 // Two barriers per step.  Every term keeps its C order; buffers are rings
 // indexed by frame (features 8, dense/vad state 4, noise/denoise state 2).
 // ---------------------------------------------------------------------------
+
 constexpr int kR3S = 8, kR3G = 2, kR3NT = 1024;
 __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   constexpr int S = kR3S, G = kR3G, NT = kR3NT;
@@ -933,7 +960,8 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     alignas(16) float gnT[2][48 * S];
     alignas(16) float gdT[2][96 * S];
     alignas(16) float zrv[48 * S], zrn[96 * S], zrd[192 * S];
-    alignas(16) float gout[22 * S];
+    alignas(16) float dhp[96 * S];  // denoise candidate input prefixes (P1 -> P2)
+    alignas(16) float gout[2][22 * S];  // denoise_output of frame f in slot f & 1
     alignas(16) float vo[S];  // vad_output of the frame P2 computed last
     float tt[204];
     float ceps[S][kCeps * kBands];
@@ -988,7 +1016,9 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   int maxnf = 0;
 #pragma unroll
   for (int s = 0; s < S; s++) maxnf = max(maxnf, L.nfs[s]);
-  // prefetch lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (as 1.0 / 0.0)
+  // prefetch lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (the flag's bits,
+  // nonzero = silent: converting it here would wait for the load at the top of
+  // every step, before the lane's P1 role)
   const int pfs = tid / kRnnPf, pfi = tid - pfs * kRnnPf;
   const bool pf_lane = tid < S * kRnnPf;
   auto fetch = [&](int v) -> float {
@@ -996,14 +1026,14 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     const long long f = L.fbase[pfs] + v;
     if (pfi < kBands) return a.Lyf[f * kBands + pfi];
     if (pfi < kBands + 7) return a.f34[f * 8 + (pfi - kBands)];
-    return a.silence[f] ? 1.0f : 0.0f;
+    return __int_as_float(a.silence[f]);
   };
   // F-C: frame f's features from L.pf (cepstral memory, deltas, 34..40, the
   // new distance row); item (s, i), i < 37; item i == 0 records act(f)
   auto feat_c = [&](int f, int idx) {
     const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
     const bool valid = f < L.nfs[s];
-    const bool on = valid && L.pf[s][kRnnPf - 1] == 0.0f;
+    const bool on = valid && __float_as_int(L.pf[s][kRnnPf - 1]) == 0;
     if (i == 0) {
       L.act[f & 7][s] = on;
       if (valid && !on) a.vadf[L.fbase[s] + f] = 0;  // silent: X passes through, state untouched
@@ -1062,21 +1092,27 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   __syncthreads();
   // P1 wave plan (w = tid >> 6).  Waves w, w+4, w+8, w+12 share a SIMD under
   // the cyclic wave placement, so the heavy roles are spread over the four
-  // residue classes -- {den, den}, {den, den}, {den, noise, noise}, {den,
-  // noise, vad, vad} -- and no wave holds lanes of two roles (it would run
-  // both branches one after the other): denoise z|r waves 0..5 (384 tasks),
-  // noise z|r waves 6, 7, 10 (192), vad z|r waves 11, 15 (96), gain smoothing
-  // + vad_output store wave 8, spectral variability of frame t wave 9.
-  // (The constants name each role's first thread, for the stamps build.)
+  // residue classes -- {den, den, pre}, {den, den, pre}, {den, noise, noise,
+  // vad}, {den, noise, vad, pre} -- and no wave holds lanes of two roles (it
+  // would run both branches one after the other): denoise z|r waves 0..5 (384
+  // tasks), noise z|r waves 6, 7, 10 (192), vad z|r waves 11, 14 (96), the
+  // denoise candidates' input prefixes (b + the 114 input terms, which do not
+  // need the reset gate) waves 12, 13, 15 (192), gain smoothing + vad_output
+  // store wave 8, spectral variability of frame t wave 9.  (The constants
+  // name each role's first thread, for the stamps build.)  Measured and lost
+  // (DESIGN §8 r3): the noise candidates' prefixes here too (on waves 8 / 9,
+  // gains moved to P2: P1 16.0 -> 17.7 k cycles, P2 12.6 -> 10.9 k), and the
+  // heavy roles on the oldest waves of each SIMD (the young vad waves starve).
   [[maybe_unused]] constexpr int kP1Den = 0, kP1Noise = 384, kP1Vad = 704, kP1Var = 576, kP1Gain = 512;
   // P2 wave plan, balanced over the residue classes the same way (a wave
   // holding lanes of two roles set the phase at 19.6 k cycles before): denoise
-  // h waves 0..2 (192 tasks), noise h waves 3, 7 (96), denoise_output wave 4
-  // (44), vad h wave 5 (48), dense of frame t wave 6 (48), vad_output wave 8
-  // (2 lanes), features of frame t+1 waves 9..13 (296 items).  (Denoise h with
-  // 2 streams per lane on 6 waves shortened its chain to 11.1 k cycles but the
-  // extra waves stretched the other roles: 15.3 vs 14.6 k per phase.)
-  [[maybe_unused]] constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 384, kP2Out = 256, kP2VadOut = 512,
+  // h waves 0..2 (192 tasks; the 96 recurrent terms from the P1 prefix),
+  // noise h waves 3, 6 (96), denoise_output wave 4 (44), vad h wave 5 (48),
+  // dense of frame t wave 7 (48), vad_output wave 8 (2 lanes), features of
+  // frame t+1 waves 9..13 (296 items).  (Denoise h with 2 streams per lane on
+  // 6 waves shortened its chain to 11.1 k cycles but the extra waves
+  // stretched the other roles: 15.3 vs 14.6 k per phase.)
+  [[maybe_unused]] constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 448, kP2Out = 256, kP2VadOut = 512,
                 kP2Feat = 576;
   constexpr int kFeatItems = S * (kBands + 7 + kCeps);
   static_assert(kP2Feat + kFeatItems <= 14 * 64 && 96 * kR3G == 192 && 48 * kR3G <= 128 && 22 * kR3G <= 64 &&
@@ -1107,6 +1143,21 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   do {               \
   } while (0)
 #endif
+  // gain smoothing g = max(g, .6*lastg) (denoise.c) of frame f5 on lanes
+  // i0, i0 + n, ...; reads denoise_output slot f5 & 1
+  auto gains = [&](int f5, int i0, int n) {
+    for (int idx = i0; f5 >= 0 && idx < S * kBands; idx += n) {
+      const int s = idx / kBands, i = idx - s * kBands;
+      if (!L.act[f5 & 7][s]) continue;
+      const long long f = L.fbase[s] + f5;
+      const float gi = L.gout[f5 & 1][i * S + s];
+      const float al = .6f * L.lastg[s][i];
+      const float gsm = (gi > al) ? gi : al;
+      L.lastg[s][i] = gsm;
+      a.gr[f * kBands + i] = gi;
+      a.gs[f * kBands + i] = gsm;
+    }
+  };
   for (int t = 0; t <= maxnf + 4; t++) {
     // per-step opaque thread id: the roles' per-thread offsets are recomputed
     // each step instead of hoisted out of the frame loop, where they spilled
@@ -1129,54 +1180,47 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       if (fn >= 0 && fn < maxnf)
         rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
                               kActSigmoid, L.tt, (wv == 10 ? 128 : 64 * (wv - 6)) + ln);
-    } else if (wv == 11 || wv == 15) {
+    } else if (wv == 11 || wv == 14) {
       if (fv >= 0 && fv < maxnf)
         rnn_gates<1, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, kActSigmoid,
-                              L.tt, (wv == 15 ? 64 : 0) + ln);
-    } else if (wv == 8 && ln < 48) {  // gain smoothing g = max(g, .6*lastg) (denoise.c), frame t-5
-      const int f5 = t - 5;
-      for (int idx = ln; f5 >= 0 && idx < S * kBands; idx += 48) {
-        const int s = idx / kBands, i = idx - s * kBands;
-        if (!L.act[f5 & 7][s]) continue;
-        const long long f = L.fbase[s] + f5;
-        const float gi = L.gout[i * S + s];
-        const float al = .6f * L.lastg[s][i];
-        const float gsm = (gi > al) ? gi : al;
-        L.lastg[s][i] = gsm;
-        a.gr[f * kBands + i] = gi;
-        a.gs[f * kBands + i] = gsm;
-      }
-    } else if (wv == 8 && ln < 48 + S) {  // vad_output of frame t-3 (P2 of step t-1)
-      const int s = ln - 48, fw = t - 3;
-      if (fw >= 0 && fw < maxnf && L.act[fw & 7][s]) a.vadf[L.fbase[s] + fw] = L.vo[s];
+                              L.tt, (wv == 14 ? 64 : 0) + ln);
+    } else if (wv == 12 || wv == 13 || wv == 15) {  // denoise candidate input prefixes of frame t-3
+      if (fd >= 0 && fd < maxnf)
+        rnn_cand<6, S, G, 0, 1>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, nullptr, nullptr, nullptr,
+                                nullptr, 0, nullptr, (wv == 15 ? 128 : 64 * (wv - 12)) + ln, L.dhp);
+    } else if (wv == 8 && ln < 48) {  // gain smoothing of frame t-5
+      gains(t - 5, ln, 48);
     } else if (wv == 9 && ln < S) {  // spectral variability of frame t (features: P2 of step t-1)
       if (t < maxnf) feat_d(t, ln);
+    } else if (wv == 8 && ln >= 48 && ln < 48 + S) {  // vad_output of frame t-3 (P2 of step t-1)
+      const int s = ln - 48, fw = t - 3;
+      if (fw >= 0 && fw < maxnf && L.act[fw & 7][s]) a.vadf[L.fbase[s] + fw] = L.vo[s];
     }
     ROLE_END(0);
     if (pf_lane) L.pf[pfs][pfi] = pf_now;
-    __syncthreads();
+    lds_sync();
     RSTAMP(0);
     ROLE_BEGIN();
     // ---- P2
     const int fo = t - 4;
     if (wv < 3) {
       if (fd >= 0 && fd < maxnf)
-        rnn_cand<6, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, L.gdT[(fd + 1) & 1], L.zrd,
-                             L.gdT[fd & 1], L.act[fd & 7], ra[6], L.tt, tq);
-    } else if (wv == 3 || wv == 7) {
+        rnn_cand<6, S, G, 0, 2>(L.W, RnnIn{nullptr, nullptr, nullptr}, L.gdT[(fd + 1) & 1], L.zrd, L.gdT[fd & 1],
+                                L.act[fd & 7], ra[6], L.tt, tq, L.dhp);
+    } else if (wv == 3 || wv == 6) {
       if (fn >= 0 && fn < maxnf)
         rnn_cand<4, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
-                             L.gnT[fn & 1], L.act[fn & 7], ra[4], L.tt, (wv == 7 ? 64 : 0) + ln);
+                             L.gnT[fn & 1], L.act[fn & 7], ra[4], L.tt, (wv == 6 ? 64 : 0) + ln);
     } else if (wv == 5) {
       if (fv >= 0 && fv < maxnf)
         rnn_cand<2, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, L.gvT[fv & 3],
                              L.act[fv & 7], ra[2], L.tt, ln);
-    } else if (wv == 6) {
+    } else if (wv == 7) {
       if (t < maxnf)
         rnn_gates<0, S, G, 0>(L.W, RnnIn{L.featT[t & 7], nullptr, nullptr}, nullptr, L.doutT[t & 3], ra[0], L.tt, ln);
     } else if (wv == 4) {
       if (fo >= 0 && fo < maxnf)
-        rnn_gates<7, S, G, 0>(L.W, RnnIn{L.gdT[fo & 1], nullptr, nullptr}, nullptr, L.gout, ra[7], L.tt, ln);
+        rnn_gates<7, S, G, 0>(L.W, RnnIn{L.gdT[fo & 1], nullptr, nullptr}, nullptr, L.gout[fo & 1], ra[7], L.tt, ln);
     } else if (wv == 8 && ln < G) {
       // vad_output(t-2) -> L.vo, stored by the next step's P1
       if (fn >= 0 && fn < maxnf)
@@ -1185,7 +1229,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       if (t + 1 < maxnf) feat_c(t + 1, tq - kP2Feat);
     }
     ROLE_END(1);
-    __syncthreads();
+    lds_sync();
     RSTAMP(1);
   }
   STAMP_FLUSH(0, 2);

@@ -66,6 +66,17 @@ __device__ __forceinline__ int frame_of(const StagedArgs &a, long long g, int F,
   return v < ticks_of(a, s) * a.n_channels ? (int)f : -1;
 }
 
+// Workgroup barrier for LDS traffic only: __syncthreads() also waits for the
+// wave's outstanding global stores (vmcnt(0)), so a wave that stores results
+// late in a phase holds every wave at the barrier for the stores' round trip.
+// Use only where no thread of the workgroup reads back, in the same kernel,
+// global data another thread wrote before the barrier.
+#ifndef FVAD_FULL_SYNC
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#else
+__device__ __forceinline__ void lds_sync() { __syncthreads(); }
+#endif
+
 // Diagnostic build only (-DFVAD_STAMPS): per-phase s_memtime totals of
 // thread 0 (it joins every barrier, so a phase's stamp is its critical path),
 // accumulated into a.stamps[base + id]; no other code reads them.
