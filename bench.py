@@ -260,18 +260,27 @@ def host_rate(eng, args, rank, dist, torch, base):
     two pushes of the resident synthetic audio, alternating.  pinned: the
     producer writes each push into the engine's pinned slot (the copy cost of
     the producer itself is not counted); pageable: submit from an ordinary
-    host array (plus a threaded copy into the slot)."""
+    host array (plus a threaded copy into the slot); pinned_i16: the same
+    audio as 16-bit samples through fvad_engine_input_slot_i16 /
+    submit_i16 (half the PCIe bytes, converted on the device)."""
     import fvad
+    import numpy as np
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     src = fvad.synth_ticks(base, B, Ch, args.resident_pushes * T, 0, 2 * T)
     halves = (src[:T], src[T:])
+    q16 = [np.clip(np.round(h * 32768.0), -32768, 32767).astype(np.int16) for h in halves]
     res = {}
-    for kind in ("pinned", "pageable"):
-        if kind == "pinned":
+    for kind in ("pinned", "pageable", "pinned_i16"):
+        if kind.startswith("pinned"):
             for k in range(2):  # each slot holds one of the two pushes
-                sl = eng.input_slot()
-                sl[:T] = halves[k]
-                eng.submit(sl[:T])
+                if kind == "pinned":
+                    sl = eng.input_slot()
+                    sl[:T] = halves[k]
+                    eng.submit(sl[:T])
+                else:
+                    sl = eng.input_slot_i16()
+                    sl[:T] = q16[k]
+                    eng.submit_i16(sl[:T])
             eng.collect(want=False)
             eng.collect(want=False)
         eng.sync()
@@ -282,7 +291,10 @@ def host_rate(eng, args, rank, dist, torch, base):
             if inflight == 2:
                 eng.collect(want=True)
                 inflight -= 1
-            eng.submit(eng.input_slot()[:T] if kind == "pinned" else halves[k & 1])
+            if kind == "pinned_i16":
+                eng.submit_i16(eng.input_slot_i16()[:T])
+            else:
+                eng.submit(eng.input_slot()[:T] if kind == "pinned" else halves[k & 1])
             inflight += 1
         while inflight:
             eng.collect(want=True)
@@ -294,11 +306,13 @@ def host_rate(eng, args, rank, dist, torch, base):
                      1000.0 * sec / args.steps)
     return {"value": round(res["pinned"][0], 1), "unit": "frames/s", "ms_per_step": round(res["pinned"][1], 3),
             "pageable_value": round(res["pageable"][0], 1), "pageable_ms_per_step": round(res["pageable"][1], 3),
-            "input_bytes_per_step": int(halves[0].nbytes),
+            "i16_value": round(res["pinned_i16"][0], 1), "i16_ms_per_step": round(res["pinned_i16"][1], 3),
+            "input_bytes_per_step": int(halves[0].nbytes), "i16_input_bytes_per_step": int(q16[0].nbytes),
             "note": "streaming submit/collect, 2 pushes in flight, input = the first two pushes of the synthetic "
                     "streams alternating: from pinned host slots (value) or pageable host memory (pageable_value), "
                     "H2D over PCIe inside the timed region and overlapped with the previous push; per-tick "
-                    "outputs copied back every push"}
+                    "outputs copied back every push; i16_value: the same audio as 16-bit samples from the pinned "
+                    "16-bit slot (fvad_engine_submit_i16, k / 32768 converted on the device)"}
 
 
 def gather_kernel_tables(kt, dist, torch, rank):
@@ -405,6 +419,7 @@ def main():
     if host is not None:
         line["host_buffers"] = host
         line["realtime_streams_host"] = round(host["value"] / (100.0 * Ch), 1)
+        line["realtime_streams_host_i16"] = round(host["i16_value"] / (100.0 * Ch), 1)
     if args.cpu_baseline:  # rank 0 only, at any N (the other ranks have finished)
         try:
             line["cpu_baseline"] = cpu_baseline(args, base)

@@ -136,6 +136,7 @@ struct fvad_engine {
   hipStream_t cstream = nullptr;
   struct Slot {
     float *in = nullptr;                 // pinned [max_ticks][B][C][480]
+    int16_t *in16 = nullptr;             // pinned 16-bit input slot (fvad_engine_input_slot_i16; on first use)
     int32_t *ticks = nullptr;            // pinned [B]
     float *vad = nullptr, *ratio = nullptr, *wratio = nullptr, *wvad = nullptr, *band = nullptr, *den = nullptr;
     int32_t *wflag = nullptr;            // pinned outputs of the push that used this slot
@@ -145,6 +146,7 @@ struct fvad_engine {
   } slots[2];
   bool slots_ready = false;
   int sub_next = 0, col_next = 0;
+  int16_t *d_pcm16 = nullptr;  // device staging of a 16-bit submit (converted into d_pcm on the copy stream)
 };
 
 // Diagnostic builds: per-phase cycle totals of k_frame (thread 0 of every workgroup).
@@ -305,11 +307,12 @@ void free_all(fvad_engine *e) {
                       e->ev_vt[1][0], e->ev_vt[1][1], e->ev_vadm_b[0], e->ev_vadm_b[1]};
   for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
+  if (e->d_pcm16) (void)hipFree(e->d_pcm16);
   if (e->side) (void)hipStreamDestroy(e->side);
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
   if (e->cstream) (void)hipStreamDestroy(e->cstream);
   for (auto &sl : e->slots) {
-    void *hp[] = {sl.in, sl.ticks, sl.vad, sl.ratio, sl.wratio, sl.wvad, sl.band, sl.den, sl.wflag};
+    void *hp[] = {sl.in, sl.in16, sl.ticks, sl.vad, sl.ratio, sl.wratio, sl.wvad, sl.band, sl.den, sl.wflag};
     for (void *q : hp)
       if (q) (void)hipHostFree(q);
     if (sl.h2d) (void)hipEventDestroy(sl.h2d);
@@ -844,6 +847,19 @@ int ensure_slots(fvad_engine *e) {
   return FVAD_OK;
 }
 
+// the 16-bit ingest's pinned slots and device staging buffer, on first use
+int ensure_slots16(fvad_engine *e) {
+  if (e->d_pcm16) return FVAD_OK;
+  const fvad_engine_config &c = e->cfg;
+  const size_t n = (size_t)c.max_ticks * c.n_streams * c.n_channels * fvad::kFrame;
+  for (auto &sl : e->slots)
+    if (hipHostMalloc(reinterpret_cast<void **>(&sl.in16), n * sizeof(int16_t), 0) != hipSuccess)
+      return fail(FVAD_ENOMEM, "hipHostMalloc failed (16-bit input slots)");
+  if (hipMalloc(reinterpret_cast<void **>(&e->d_pcm16), n * sizeof(int16_t)) != hipSuccess)
+    return fail(FVAD_ENOMEM, "hipMalloc failed (16-bit input staging)");
+  return FVAD_OK;
+}
+
 }  // namespace
 
 extern "C" int fvad_engine_push(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
@@ -907,8 +923,16 @@ extern "C" int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks,
   return fvad_engine_submit_ex(e, pcm, n_ticks, ticks_valid, nullptr);
 }
 
-extern "C" int fvad_engine_submit_ex(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
-                                     const int32_t *last_tick_samples) {
+namespace {
+
+// fvad_engine_submit_ex / fvad_engine_submit_i16: pcm is float or int16_t
+// (16-bit samples k, pushed as k / 32768.0f -- libsndfile's short -> float
+// normalisation, exact in f32: half the host-to-device bytes, converted by
+// k_pcm16 on the copy stream before the push's kernels read d_pcm)
+template <typename Sample>
+int submit_any(fvad_engine *e, const Sample *pcm, int n_ticks, const int32_t *ticks_valid,
+               const int32_t *last_tick_samples) {
+  constexpr bool k16 = sizeof(Sample) == 2;
   if (!e || !pcm) return fail(FVAD_EINVAL, "null argument");
   const fvad_engine_config &c = e->cfg;
   if (n_ticks < 1 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range [1, max_ticks]");
@@ -918,14 +942,21 @@ extern "C" int fvad_engine_submit_ex(fvad_engine *e, const float *pcm, int n_tic
   if ((rc = tail_ticks(e, ticks_valid, last_tick_samples, n_ticks, tt))) return rc;
   HIP_TRY(hipSetDevice(c.device));
   if ((rc = ensure_slots(e))) return rc;
+  if constexpr (k16)
+    if ((rc = ensure_slots16(e))) return rc;
   const int si = e->sub_next;
   auto &sl = e->slots[si];
   if (sl.pending) return fail(FVAD_EINVAL, "two pushes in flight: collect the older one first");
   const size_t B = c.n_streams, TB = (size_t)n_ticks * B;
-  const size_t bytes = TB * c.n_channels * fvad::kFrame * sizeof(float);
-  if (pcm != sl.in) {  // otherwise the producer wrote into the slot (fvad_engine_input_slot)
+  const size_t n_samples = TB * c.n_channels * fvad::kFrame, bytes = n_samples * sizeof(float);
+  Sample *slot_in;
+  if constexpr (k16)
+    slot_in = sl.in16;
+  else
+    slot_in = sl.in;
+  if (pcm != slot_in) {  // otherwise the producer wrote into the slot (fvad_engine_input_slot[_i16])
     if (sl.h2d_busy) HIP_TRY(hipEventSynchronize(sl.h2d));
-    par_copy(sl.in, pcm, bytes);
+    par_copy(slot_in, pcm, n_samples * sizeof(Sample));
   }
   if (!tt.empty())
     std::memcpy(sl.ticks, tt.data(), tt.size() * sizeof(int32_t));
@@ -938,7 +969,14 @@ extern "C" int fvad_engine_submit_ex(fvad_engine *e, const float *pcm, int n_tic
   const bool staged = c.mode != FVAD_MODE_FUSED;
   hipStream_t cs = staged ? e->cstream : e->stream;
   if ((rc = input_buffer(e, cs))) return rc;
-  HIP_TRY(hipMemcpyAsync(e->d_pcm, sl.in, bytes, hipMemcpyHostToDevice, cs));
+  if constexpr (k16) {
+    // d_pcm16 is reused by the next 16-bit submit only after this conversion
+    // (both on cs, in order)
+    HIP_TRY(hipMemcpyAsync(e->d_pcm16, sl.in16, n_samples * sizeof(int16_t), hipMemcpyHostToDevice, cs));
+    HIP_TRY(fvad::launch_pcm16(e->d_pcm16, e->d_pcm, n_samples, cs));
+  } else {
+    HIP_TRY(hipMemcpyAsync(e->d_pcm, sl.in, bytes, hipMemcpyHostToDevice, cs));
+  }
   if (use_ticks) {
     int *dticks = e->d_ticks;
     if (staged) {
@@ -969,6 +1007,35 @@ extern "C" int fvad_engine_submit_ex(fvad_engine *e, const float *pcm, int n_tic
   sl.n_ticks = n_ticks;
   e->sub_next = si ^ 1;
   return FVAD_OK;
+}
+
+}  // namespace
+
+extern "C" int fvad_engine_submit_ex(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
+                                     const int32_t *last_tick_samples) {
+  return submit_any(e, pcm, n_ticks, ticks_valid, last_tick_samples);
+}
+
+extern "C" int16_t *fvad_engine_input_slot_i16(fvad_engine *e) {
+  if (!e) {
+    fail(FVAD_EINVAL, "null engine");
+    return nullptr;
+  }
+  if (hipSetDevice(e->cfg.device) != hipSuccess || ensure_slots(e) || ensure_slots16(e)) return nullptr;
+  auto &sl = e->slots[e->sub_next];
+  if (sl.h2d_busy) {
+    if (hipEventSynchronize(sl.h2d) != hipSuccess) {
+      fail(FVAD_EDEVICE, "hipEventSynchronize failed");
+      return nullptr;
+    }
+    sl.h2d_busy = false;
+  }
+  return sl.in16;
+}
+
+extern "C" int fvad_engine_submit_i16(fvad_engine *e, const int16_t *pcm, int n_ticks, const int32_t *ticks_valid,
+                                      const int32_t *last_tick_samples) {
+  return submit_any(e, pcm, n_ticks, ticks_valid, last_tick_samples);
 }
 
 extern "C" int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_ticks) {

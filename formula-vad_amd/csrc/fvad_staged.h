@@ -134,6 +134,8 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
 hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream);
 // use_denoiser = 0 (VAD.zig:206-212,239-249): k_ndring, k_ndmeta, FFT B
 hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream);
+// 16-bit ingest: dst[i] = src[i] / 32768.0f (exact), n a multiple of 8
+hipError_t launch_pcm16(const int16_t *src, float *dst, size_t n, hipStream_t stream);
 // fp16 / MFMA recurrence (fvad_gru16.hip), run in k_rnn3's place when a.gru16_frags is set
 hipError_t launch_gru16(const StagedArgs &a, hipStream_t stream);
 int gru16_frag_count();   // A fragments of 64 lanes x 8 f16

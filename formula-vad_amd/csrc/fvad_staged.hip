@@ -1941,4 +1941,35 @@ hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream) {
   return hipSuccess;
 }
 
+// ---------------------------------------------------------------------------
+// k_pcm16: the 16-bit ingest's conversion (fvad_engine_submit_i16), samples
+// k -> k / 32768.0f, libsndfile's short -> float normalisation (the simulator's
+// WAV reader does the same), exact in f32.  HBM-bound streaming: 16 B in and
+// 32 B out per thread and step, grid-stride over the push.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pcm16(const int4 *__restrict__ src, float4 *__restrict__ dst, size_t n8) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    const int4 v = src[i];
+    const int w[4] = {v.x, v.y, v.z, v.w};
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      o[2 * k] = (float)(short)(w[k] & 0xffff) * (1.0f / 32768.0f);
+      o[2 * k + 1] = (float)(short)(w[k] >> 16) * (1.0f / 32768.0f);
+    }
+    dst[2 * i] = make_float4(o[0], o[1], o[2], o[3]);
+    dst[2 * i + 1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
+hipError_t launch_pcm16(const int16_t *src, float *dst, size_t n, hipStream_t stream) {
+  if (n % 8) return hipErrorInvalidValue;
+  const size_t n8 = n / 8;
+  const unsigned grid = (unsigned)std::min<size_t>((n8 + 255) / 256, 256 * 16);
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pcm16, dim3(grid), dim3(256), 0, stream, reinterpret_cast<const int4 *>(src),
+                     reinterpret_cast<float4 *>(dst), n8);
+  return hipGetLastError();
+}
+
 }  // namespace fvad

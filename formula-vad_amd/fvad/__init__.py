@@ -145,6 +145,8 @@ SYMBOLS = [
     ("fvad_engine_input_slot", C.c_void_p, [C.c_void_p]),
     ("fvad_engine_submit", C.c_int, [C.c_void_p, F32P, C.c_int, I32P]),
     ("fvad_engine_collect", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]),
+    ("fvad_engine_input_slot_i16", C.c_void_p, [C.c_void_p]),
+    ("fvad_engine_submit_i16", C.c_int, [C.c_void_p, C.POINTER(C.c_int16), C.c_int, I32P, I32P]),
     ("fvad_engine_load_synthetic", C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
     ("fvad_engine_load_synthetic_ex", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32]),
     ("fvad_engine_resident_seek", C.c_int, [C.c_void_p, C.c_int]),
@@ -338,6 +340,29 @@ class Engine:
         self._sub_keep = tv
         _check(lib().fvad_engine_submit(self.h, fptr(pcm), pcm.shape[0],
                                         tv.ctypes.data_as(I32P) if tv is not None else None), "fvad_engine_submit")
+
+    def input_slot_i16(self):
+        """The pinned 16-bit input slot for the next submit_i16, as a
+        [max_ticks][streams][channels][480] int16 view."""
+        p = lib().fvad_engine_input_slot_i16(self.h)
+        if not p:
+            raise FvadError("fvad_engine_input_slot_i16: %s" % last_error())
+        n = self.max_ticks * self.B * self.C * FRAME
+        arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int16)), shape=(n,))
+        return arr.reshape(self.max_ticks, self.B, self.C, FRAME)
+
+    def submit_i16(self, pcm, ticks_valid=None, last_tick_samples=None):
+        """Asynchronous push of 16-bit samples k (fvad_engine_submit_i16): the
+        same outputs as submit() of k / 32768.0f, half the PCIe bytes."""
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        assert pcm.shape[1:] == (self.B, self.C, FRAME), pcm.shape
+        tv = np.ascontiguousarray(ticks_valid, np.int32) if ticks_valid is not None else None
+        lt = np.ascontiguousarray(last_tick_samples, np.int32) if last_tick_samples is not None else None
+        self._sub_keep = (tv, lt)
+        _check(lib().fvad_engine_submit_i16(self.h, pcm.ctypes.data_as(C.POINTER(C.c_int16)), pcm.shape[0],
+                                            tv.ctypes.data_as(I32P) if tv is not None else None,
+                                            lt.ctypes.data_as(I32P) if lt is not None else None),
+               "fvad_engine_submit_i16")
 
     def collect(self, denoised=False, want=True):
         """Outputs of the oldest submitted push (fvad_engine_collect)."""

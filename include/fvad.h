@@ -176,6 +176,17 @@ int fvad_engine_submit(fvad_engine *e, const float *pcm, int n_ticks, const int3
 int fvad_engine_submit_ex(fvad_engine *e, const float *pcm, int n_ticks, const int32_t *ticks_valid,
                           const int32_t *last_tick_samples);
 int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_ticks);
+/* 16-bit PCM ingest (onboard WAV audio is 16-bit): the same push as
+ * fvad_engine_submit_ex on the samples k / 32768.0f (libsndfile's short ->
+ * float normalisation, as the reference's sf_read_float gives
+ * AudioPipeline.pushSamples, src/AudioPipeline.zig:86-120; exact in f32), so
+ * the outputs are bit-identical to a float submit of those samples.  Half the
+ * host-to-device bytes; the conversion runs on the device, on the copy
+ * stream.  The slot and the submit/collect rules are fvad_engine_input_slot's
+ * and fvad_engine_submit's. */
+int16_t *fvad_engine_input_slot_i16(fvad_engine *e);
+int fvad_engine_submit_i16(fvad_engine *e, const int16_t *pcm, int n_ticks, const int32_t *ticks_valid,
+                           const int32_t *last_tick_samples);
 
 /* Device-resident variants for benchmarking / zero-copy producers. */
 /* allocate a device input of n_ticks and fill it with the synthetic generator */

@@ -75,6 +75,79 @@ def test_submit_collect_equals_push(fvad_mod, models, mode):
         assert np.array_equal(a["band"][wf], b["band"][wf])
 
 
+@pytest.mark.parametrize("mode", ["staged", "fused", "fp16"])
+def test_submit_i16_equals_float_push(fvad_mod, models, mode):
+    """16-bit ingest (fvad_engine_submit_i16, k_pcm16): samples k give the
+    outputs of a float push of k / 32768.0f (libsndfile's short -> float),
+    bit for bit -- through the zero-copy 16-bit slot and caller buffers, two
+    pushes in flight, ragged ticks, full-scale and clipped samples."""
+    m, _ = models
+    secs = [5.0, 3.37, 4.2, 0.9]
+    streams = []
+    for i, sec in zip((5, 21, 44, 9), secs):
+        x = fvad_mod.synth_stream(i, int(48000 * sec), 2)[0]
+        q = np.clip(np.round(x * 32768.0 * (1 + 3 * (i == 44))), -32768, 32767).astype(np.int16)
+        streams.append(q)
+    q_pushes = _chunks([q.astype(np.float32) for q in streams], 30)  # sample values k, as f32
+    ref_eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=30, want_denoised=True, mode=mode)
+    ref = [ref_eng.push(p / np.float32(32768.0), ticks_valid=v, denoised=True) for p, v in q_pushes]
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=30, want_denoised=True, mode=mode)
+    got, in_flight = [], 0
+    for k, (p, v) in enumerate(q_pushes):
+        p16 = p.astype(np.int16)
+        if in_flight == 2:
+            got.append(eng.collect(denoised=True))
+            in_flight -= 1
+        if k % 2:
+            slot = eng.input_slot_i16()
+            slot[: p16.shape[0]] = p16
+            eng.submit_i16(slot[: p16.shape[0]], ticks_valid=v)
+        else:
+            eng.submit_i16(p16, ticks_valid=v)
+        in_flight += 1
+    while in_flight:
+        got.append(eng.collect(denoised=True))
+        in_flight -= 1
+    assert len(got) == len(ref)
+    for a, b in zip(ref, got):
+        for key in ("vad", "ratio", "win_flag", "win_ratio", "win_vad", "denoised"):
+            assert np.array_equal(a[key], b[key]), key
+        wf = a["win_flag"].astype(bool)
+        assert np.array_equal(a["band"][wf], b["band"][wf])
+
+
+def test_submit_i16_no_denoiser_partial_tick(fvad_mod, models):
+    """use_denoiser = 0 with a partial last tick through the 16-bit ingest."""
+    m, _ = models
+    n = [2048 * 3 + 100, 480 * 9 + 17]
+    streams = [np.clip(np.round(fvad_mod.synth_stream(7 + i, k, 2)[0] * 32768.0), -32768, 32767).astype(np.int16)
+               for i, k in enumerate(n)]
+    T = max((k + FRAME - 1) // FRAME for k in n)
+    pcm = np.zeros((T, 2, 2, FRAME), np.int16)
+    valid = np.zeros(2, np.int32)
+    last = np.zeros(2, np.int32)
+    for s, x in enumerate(streams):
+        nt = (x.shape[1] + FRAME - 1) // FRAME
+        pad = np.zeros((2, nt * FRAME), np.int16)
+        pad[:, : x.shape[1]] = x
+        pcm[:nt, s] = pad.reshape(2, nt, FRAME).transpose(1, 0, 2)
+        valid[s] = nt
+        last[s] = x.shape[1] - (nt - 1) * FRAME
+    ref_eng = fvad_mod.Engine(m, 2, 2, max_ticks=T, use_denoiser=False)
+    ref = ref_eng.push(pcm.astype(np.float32) / np.float32(32768.0), ticks_valid=valid, last_tick_samples=last)
+    eng = fvad_mod.Engine(m, 2, 2, max_ticks=T, use_denoiser=False)
+    eng.submit_i16(pcm, ticks_valid=valid, last_tick_samples=last)
+    got = eng.collect()
+    n_win = 0
+    for s in range(2):  # outputs are defined on each stream's valid ticks, windows where win_flag is set
+        wf = ref["win_flag"][: valid[s], s].astype(bool)
+        assert np.array_equal(wf, got["win_flag"][: valid[s], s].astype(bool)), s
+        for key in ("win_ratio", "win_vad", "band"):
+            assert np.array_equal(ref[key][: valid[s], s][wf], got[key][: valid[s], s][wf]), (key, s)
+        n_win += int(wf.sum())
+    assert n_win == sum(k // 2048 for k in n)
+
+
 def test_submit_limits(fvad_mod, models):
     m, _ = models
     eng = fvad_mod.Engine(m, 2, 2, max_ticks=8)
