@@ -146,7 +146,8 @@ struct fvad_engine {
   } slots[2];
   bool slots_ready = false;
   int sub_next = 0, col_next = 0;
-  int16_t *d_pcm16 = nullptr;  // device staging of a 16-bit submit (converted into d_pcm on the copy stream)
+  int16_t *d_pcm16 = nullptr;  // device staging of a 16-bit submit (converted into d_pcm by k_pcm16)
+
 };
 
 // Diagnostic builds: per-phase cycle totals of k_frame (thread 0 of every workgroup).
@@ -308,6 +309,7 @@ void free_all(fvad_engine *e) {
   for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
   if (e->d_pcm16) (void)hipFree(e->d_pcm16);
+
   if (e->side) (void)hipStreamDestroy(e->side);
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
   if (e->cstream) (void)hipStreamDestroy(e->cstream);
@@ -825,7 +827,12 @@ int ensure_slots(fvad_engine *e) {
   const fvad_engine_config &c = e->cfg;
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t TB = T * B, frames = TB * C * fvad::kFrame;
-  if (!e->cstream && hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) != hipSuccess)
+  // the copy stream at the highest priority: its own hardware queue, so the
+  // 16-bit ingest's k_pcm16 does not queue behind a long kernel of a stream
+  // sharing its queue (it waited for k_vadm_hbm at the default priority)
+  int lo_prio = 0, hi_prio = 0;
+  if (!e->cstream && (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
+                      hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, hi_prio) != hipSuccess))
     return fail(FVAD_EDEVICE, "copy stream creation failed");
   auto host = [&](auto **p, size_t count) -> int {
     if (hipHostMalloc(reinterpret_cast<void **>(p), std::max<size_t>(count, 1) * 4, 0) != hipSuccess)
@@ -928,7 +935,7 @@ namespace {
 // fvad_engine_submit_ex / fvad_engine_submit_i16: pcm is float or int16_t
 // (16-bit samples k, pushed as k / 32768.0f -- libsndfile's short -> float
 // normalisation, exact in f32: half the host-to-device bytes, converted by
-// k_pcm16 on the copy stream before the push's kernels read d_pcm)
+// k_pcm16 on the copy stream right after the copy)
 template <typename Sample>
 int submit_any(fvad_engine *e, const Sample *pcm, int n_ticks, const int32_t *ticks_valid,
                const int32_t *last_tick_samples) {
@@ -970,8 +977,8 @@ int submit_any(fvad_engine *e, const Sample *pcm, int n_ticks, const int32_t *ti
   hipStream_t cs = staged ? e->cstream : e->stream;
   if ((rc = input_buffer(e, cs))) return rc;
   if constexpr (k16) {
-    // d_pcm16 is reused by the next 16-bit submit only after this conversion
-    // (both on cs, in order)
+    // d_pcm16 is overwritten by the next 16-bit submit only after this
+    // conversion read it (both on cs, in order)
     HIP_TRY(hipMemcpyAsync(e->d_pcm16, sl.in16, n_samples * sizeof(int16_t), hipMemcpyHostToDevice, cs));
     HIP_TRY(fvad::launch_pcm16(e->d_pcm16, e->d_pcm, n_samples, cs));
   } else {
