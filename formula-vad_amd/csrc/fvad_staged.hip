@@ -1741,10 +1741,8 @@ __global__ void __launch_bounds__(256) k_ndring(StagedArgs a) {
 }
 
 // k_ndmeta: window completion per tick (a window completes in the tick that
-// brings its last sample); a completed window's volume ratio is
-// preAnalyzeSegment over its fft_size input samples (VAD.zig:253-272:
-// rmsVolume per channel = sqrt(sum x^2 / n), the sum in sample order; min /
-// max over channels); lane per stream.
+// brings its last sample), lane per stream; the completed windows' volume
+// ratios are k_ndvol's.
 __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
   const int s = blockIdx.x * 64 + threadIdx.x;
   if (s >= a.n_streams) return;
@@ -1763,21 +1761,6 @@ __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
       const bool complete = a0 + (unsigned)nd_real(a, s, t, nt) >= next_end;
       if (complete) {
         const unsigned long long ws = wdone * (unsigned)FB;
-        float vol_min = 1, vol_max = 0;
-        for (int c = 0; c < C; c++) {
-          const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
-          long long ri = (long long)(ws % (unsigned long long)a.ring_len);
-          float sum = 0.0f;
-          for (int n = 0; n < FB; n++) {
-            const float x = ring[ri];
-            sum += x * x;
-            if (++ri == a.ring_len) ri = 0;
-          }
-          const float vol = sqrtf(sum / (float)FB);
-          if (vol < vol_min) vol_min = vol;
-          if (vol > vol_max) vol_max = vol;
-        }
-        a.out_win_ratio[o] = vol_max == 0 ? 0.0f : vol_min / vol_max;
         a.out_win_vad[o] = -1.0f;
         wt[j] = t;
         wsx[j] = (long long)ws;
@@ -1792,6 +1775,37 @@ __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
     *cnt = sd0 + (unsigned long long)(nt - 1) * kFrame + (unsigned)nd_real(a, s, nt - 1, nt);
   }
   for (; j < a.wmax; j++) wt[j] = -1;
+}
+
+// k_ndvol: a completed window's volume ratio, preAnalyzeSegment over its
+// fft_size input samples (VAD.zig:253-272: rmsVolume per channel =
+// sqrt(sum x^2 / n) with the sum in sample order, audio_utils.zig:14-24; min /
+// max over channels in channel order).  The sum is one serial f32 chain per
+// channel, so the parallelism is across windows: lane per (stream, window of
+// this push) -- ~fft_size / 480 times k_ndmeta's lanes.
+__global__ void __launch_bounds__(64) k_ndvol(StagedArgs a) {
+  const long long item = (long long)blockIdx.x * 64 + threadIdx.x;
+  if (item >= (long long)a.n_streams * a.wmax) return;
+  const int s = (int)(item / a.wmax), j = (int)(item - (long long)s * a.wmax);
+  const int t = a.win_tick[(size_t)s * a.wmax + j];
+  if (t < 0) return;
+  const int C = a.n_channels, FB = a.nfft_b;
+  const unsigned long long ws = (unsigned long long)a.win_start[(size_t)s * a.wmax + j];
+  float vol_min = 1, vol_max = 0;
+  for (int c = 0; c < C; c++) {
+    const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
+    long long ri = (long long)(ws % (unsigned long long)a.ring_len);
+    float sum = 0.0f;
+    for (int n = 0; n < FB; n++) {
+      const float x = ring[ri];
+      sum += x * x;
+      if (++ri == a.ring_len) ri = 0;
+    }
+    const float vol = sqrtf(sum / (float)FB);
+    if (vol < vol_min) vol_min = vol;
+    if (vol > vol_max) vol_max = vol;
+  }
+  a.out_win_ratio[(size_t)t * a.n_streams + s] = vol_max == 0 ? 0.0f : vol_min / vol_max;
 }
 
 // every launch is checked where it is issued: a failed launch in the middle of
@@ -1931,6 +1945,7 @@ hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream) {
   const long long frames = (long long)a.n_streams * a.V;
   FVAD_KERNEL_TRY(k_ndring, dim3((unsigned)((frames + 1) / 2)), dim3(256), 0, stream, a);
   FVAD_KERNEL_TRY(k_ndmeta, dim3((a.n_streams + 63) / 64), dim3(64), 0, stream, a);
+  FVAD_KERNEL_TRY(k_ndvol, dim3((unsigned)(((long long)a.n_streams * a.wmax + 63) / 64)), dim3(64), 0, stream, a);
   return launch_fftb(a, n_cu, stream);
 }
 

@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 BENCH=(bench.py --cpu-baseline 0 --host-rate 0 --variants 0 "$@")
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" --steps 5 --warmup 2 \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" --steps 20 --warmup 10 \
   > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run -- python3 "${BENCH[@]}" --steps 2 --warmup 1 \
   > "$OUT/fetch.log" 2>&1
