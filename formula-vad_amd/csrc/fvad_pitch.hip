@@ -45,6 +45,11 @@ namespace fvad {
 #ifndef FVAD_WALK_Q3
 #define FVAD_WALK_Q3 36
 #endif
+// Q5's walking waves at s_setprio 2 (the group ends with them; 1.20 -> 1.19
+// ms); the yy walker at priority 2 beside Q2..Q4 measured no better
+#ifndef FVAD_PC_PRIO
+#define FVAD_PC_PRIO 1
+#endif
 #ifndef FVAD_Q5_UNROLL
 #define FVAD_Q5_UNROLL 4  // Q5 walk unroll (2 / 8 measured no better)
 #endif
@@ -547,6 +552,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
 #endif
     float aM = 0, a0 = 0, aP = 0;
     int q5T0 = 0, q5Tc = 0, q5Tb = 0;
+    if ((FVAD_PC_PRIO & 1) && q5on) __builtin_amdgcn_s_setprio(2);
     if (q5on) {
       const int fr = q5f, c = q5c;
       q5T0 = T0s[fr];
@@ -608,6 +614,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         }
       }
     }
+    if (FVAD_PC_PRIO & 1) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     if (q5on && !q5b) {
       const int fr = q5f, c = q5c;

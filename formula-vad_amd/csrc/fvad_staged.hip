@@ -950,6 +950,14 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 // indexed by frame (features 8, dense/vad state 4, noise/denoise state 2).
 // ---------------------------------------------------------------------------
 
+// P2 wave priorities (s_setprio while the role runs): bit 2 the noise h
+// waves, bit 4 denoise_output (kept: k_rnn3 1.19 -> 1.16 ms; both are young
+// waves that set P2's end), bit 8 vad h + dense (no gain).  Raising P1's
+// noise or vad z|r waves above the denoise waves lost (1.16 -> 1.19 / 1.21 ms),
+// as did the denoise prefix waves (1.23 ms).
+#ifndef FVAD_PRIO
+#define FVAD_PRIO 6
+#endif
 constexpr int kR3S = 8, kR3G = 2, kR3NT = 1024;
 __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   constexpr int S = kR3S, G = kR3G, NT = kR3NT;
@@ -1208,19 +1216,27 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
         rnn_cand<6, S, G, 0, 2>(L.W, RnnIn{nullptr, nullptr, nullptr}, L.gdT[(fd + 1) & 1], L.zrd, L.gdT[fd & 1],
                                 L.act[fd & 7], ra[6], L.tt, tq, L.dhp);
     } else if (wv == 3 || wv == 6) {
+      if (FVAD_PRIO & 2) __builtin_amdgcn_s_setprio(3);
       if (fn >= 0 && fn < maxnf)
         rnn_cand<4, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
                              L.gnT[fn & 1], L.act[fn & 7], ra[4], L.tt, (wv == 6 ? 64 : 0) + ln);
+      if (FVAD_PRIO & 2) __builtin_amdgcn_s_setprio(0);
     } else if (wv == 5) {
+      if (FVAD_PRIO & 8) __builtin_amdgcn_s_setprio(2);
       if (fv >= 0 && fv < maxnf)
         rnn_cand<2, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, L.gvT[fv & 3],
                              L.act[fv & 7], ra[2], L.tt, ln);
+      if (FVAD_PRIO & 8) __builtin_amdgcn_s_setprio(0);
     } else if (wv == 7) {
+      if (FVAD_PRIO & 8) __builtin_amdgcn_s_setprio(2);
       if (t < maxnf)
         rnn_gates<0, S, G, 0>(L.W, RnnIn{L.featT[t & 7], nullptr, nullptr}, nullptr, L.doutT[t & 3], ra[0], L.tt, ln);
+      if (FVAD_PRIO & 8) __builtin_amdgcn_s_setprio(0);
     } else if (wv == 4) {
+      if (FVAD_PRIO & 4) __builtin_amdgcn_s_setprio(2);
       if (fo >= 0 && fo < maxnf)
         rnn_gates<7, S, G, 0>(L.W, RnnIn{L.gdT[fo & 1], nullptr, nullptr}, nullptr, L.gout[fo & 1], ra[7], L.tt, ln);
+      if (FVAD_PRIO & 4) __builtin_amdgcn_s_setprio(0);
     } else if (wv == 8 && ln < G) {
       // vad_output(t-2) -> L.vo, stored by the next step's P1
       if (fn >= 0 && fn < maxnf)
