@@ -952,7 +952,8 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 
 // P2 wave priorities (s_setprio while the role runs): bit 2 the noise h
 // waves, bit 4 denoise_output (kept: k_rnn3 1.19 -> 1.16 ms; both are young
-// waves that set P2's end), bit 8 vad h + dense (no gain).  Raising P1's
+// waves that set P2's end), bit 8 vad h + dense (no gain; nor vad_output or
+// the feature waves raised: 1.17 -> 1.18 ms).  Raising P1's
 // noise or vad z|r waves above the denoise waves lost (1.16 -> 1.19 / 1.21 ms),
 // as did the denoise prefix waves (1.23 ms).
 #ifndef FVAD_PRIO
