@@ -941,11 +941,13 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 // for one term are one 16-byte LDS read (ds_read_b128, full LDS rate; the
 // float2 reads of G = 4 were paired into half-rate ds_read2_b64) and one
 // int8 -> f32 conversion serves 4 streams.  Step t:
-//   P1  z|r gates of vad(t-1), noise(t-2), denoise(t-3); features of t+1
-//       (cepstral memory, deltas, distance row); gain smoothing of t-5
-//   P2  candidates of vad(t-1), noise(t-2), denoise(t-3); dense(t);
-//       denoise_output(t-4); vad_output(t-2); spectral variability of t+1;
-//       next features -> LDS
+//   P1  z|r gates of vad(t-1), noise(t-2), denoise(t-3); the denoise
+//       candidates' input prefixes of t-3; spectral variability of t; gain
+//       smoothing of t-5
+//   P2  candidates of vad(t-1), noise(t-2), denoise(t-3) (denoise: its 96
+//       recurrent terms after the P1 prefix); dense(t); denoise_output(t-4);
+//       vad_output(t-2); features of t+1 (cepstral memory, deltas, distance
+//       row) -> LDS
 // Two barriers per step.  Every term keeps its C order; buffers are rings
 // indexed by frame (features 8, dense/vad state 4, noise/denoise state 2).
 // ---------------------------------------------------------------------------
