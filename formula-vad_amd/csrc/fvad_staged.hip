@@ -855,12 +855,46 @@ __device__ __forceinline__ void rnn_inputs(const int8_t *wc, const RnnIn &in, in
   }
 }
 
+// input segments [G0, G1) of matrix m (a sum split across phases continues
+// where the stored partial sum stopped: the same adds in the same order)
+template <int m, int S, int SL, int G0, int G1>
+__device__ __forceinline__ void rnn_segs(const int8_t *wc, const RnnIn &in, int s0, float (&acc)[SL]) {
+  if constexpr (G0 <= 0 && G1 > 0) mv_seg<rnnimg::kSegs[m][0], S, SL>(wc, in.v0, s0, acc);
+  if constexpr (m == 3 || m == 4 || m == 5 || m == 6) {
+    if constexpr (G0 <= 1 && G1 > 1) mv_seg<rnnimg::kSegs[m][1], S, SL>(wc + rnnimg::seg_off(m, 1), in.v1, s0, acc);
+    if constexpr (G0 <= 2 && G1 > 2) mv_seg<rnnimg::kSegs[m][2], S, SL>(wc + rnnimg::seg_off(m, 2), in.v2, s0, acc);
+  }
+}
+template <int SL>
+__device__ __forceinline__ void acc_load(float (&acc)[SL], const float *p) {
+  const typename VecT<SL>::T v = *reinterpret_cast<const typename VecT<SL>::T *>(p);
+  acc[0] = v.x;
+  acc[1] = v.y;
+  if constexpr (SL == 4) {
+    acc[2] = v.z;
+    acc[3] = v.w;
+  }
+}
+template <int SL>
+__device__ __forceinline__ void acc_store(const float (&acc)[SL], float *p) {
+  typename VecT<SL>::T v;
+  v.x = acc[0];
+  v.y = acc[1];
+  if constexpr (SL == 4) {
+    v.z = acc[2];
+    v.w = acc[3];
+  }
+  *reinterpret_cast<typename VecT<SL>::T *>(p) = v;
+}
+
 // dense layer / GRU z|r gates of image matrix m:
 //   out[c][s] = act(kWs * (b[c] + sum_j w[c][j] * [in ; state][j][s]))
 // (tasks t = tid, tid + NT, ...; NT = 0: the single task tid)
-template <int m, int S, int G, int NT>
+// (PART 3: b + input segment 0 only, stored to preT [c][S]; PART 5: from
+// preT, the remaining input segments and the state)
+template <int m, int S, int G, int NT, int PART = 0>
 __device__ __forceinline__ void rnn_gates(const int8_t *W, const RnnIn &in, const float *stT, float *outT, int act,
-                                          const float *tt, int tid) {
+                                          const float *tt, int tid, float *preT = nullptr) {
   constexpr int SL = S / G, cols = rnnimg::kCols[m];
   constexpr int ob = rnnimg::off_b(m), ow = rnnimg::off_w(m), ws = rnnimg::stride(m);
   constexpr int gst = (m == 1) ? 1 : (m == 3 || m == 5) ? 3 : -1;  // state segment of z|r matrices
@@ -868,10 +902,21 @@ __device__ __forceinline__ void rnn_gates(const int8_t *W, const RnnIn &in, cons
     const int c = t / G, s0 = (t - c * G) * SL;
     const int8_t *wc = W + ow + c * ws;
     float acc[SL];
-    const float b = (float)W[ob + c];
+    if constexpr (PART == 5) {
+      acc_load<SL>(acc, preT + c * S + s0);
+      rnn_segs<m, S, SL, 1, 3>(wc, in, s0, acc);
+    } else {
+      const float b = (float)W[ob + c];
 #pragma unroll
-    for (int q = 0; q < SL; q++) acc[q] = b;
-    rnn_inputs<m, S, SL>(wc, in, s0, acc);
+      for (int q = 0; q < SL; q++) acc[q] = b;
+      if constexpr (PART == 3) {
+        rnn_segs<m, S, SL, 0, 1>(wc, in, s0, acc);
+        acc_store<SL>(acc, preT + c * S + s0);
+        continue;
+      } else {
+        rnn_inputs<m, S, SL>(wc, in, s0, acc);
+      }
+    }
     if constexpr (gst >= 0) mv_seg<rnnimg::kSegs[m][gst], S, SL>(wc + rnnimg::seg_off(m, gst), stT, s0, acc);
 #pragma unroll
     for (int q = 0; q < SL; q++) outT[c * S + s0 + q] = activate(tt, act, kWs * acc[q]);
@@ -895,29 +940,20 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
     const int c = t / G, s0 = (t - c * G) * SL;
     const int8_t *wc = W + ow + c * ws;
     float acc[SL];
-    if constexpr (PART == 2) {
-      const typename VecT<SL>::T p = *reinterpret_cast<const typename VecT<SL>::T *>(preT + c * S + s0);
-      acc[0] = p.x;
-      acc[1] = p.y;
-      if constexpr (SL == 4) {
-        acc[2] = p.z;
-        acc[3] = p.w;
-      }
+    if constexpr (PART == 2 || PART == 4) {
+      acc_load<SL>(acc, preT + c * S + s0);
+      if constexpr (PART == 4) rnn_segs<m, S, SL, 1, 3>(wc, in, s0, acc);
     } else {
       const float b = (float)W[ob + c];
 #pragma unroll
       for (int q = 0; q < SL; q++) acc[q] = b;
-      rnn_inputs<m, S, SL>(wc, in, s0, acc);
+      if constexpr (PART == 3)
+        rnn_segs<m, S, SL, 0, 1>(wc, in, s0, acc);
+      else
+        rnn_inputs<m, S, SL>(wc, in, s0, acc);
     }
-    if constexpr (PART == 1) {
-      typename VecT<SL>::T p;
-      p.x = acc[0];
-      p.y = acc[1];
-      if constexpr (SL == 4) {
-        p.z = acc[2];
-        p.w = acc[3];
-      }
-      *reinterpret_cast<typename VecT<SL>::T *>(preT + c * S + s0) = p;
+    if constexpr (PART == 1 || PART == 3 || PART == 4) {
+      acc_store<SL>(acc, preT + c * S + s0);
       continue;
     }
     mv_seg_r<rnnimg::kSegs[m][gst], S, SL>(wc + rnnimg::seg_off(m, gst), stT, zrT + N * S, s0, acc);
@@ -961,6 +997,9 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 #ifndef FVAD_PRIO
 #define FVAD_PRIO 6
 #endif
+#ifndef FVAD_GVPRE
+#define FVAD_GVPRE 1
+#endif
 constexpr int kR3S = 8, kR3G = 2, kR3NT = 1024;
 __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   constexpr int S = kR3S, G = kR3G, NT = kR3NT;
@@ -971,7 +1010,8 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     alignas(16) float gnT[2][48 * S];
     alignas(16) float gdT[2][96 * S];
     alignas(16) float zrv[48 * S], zrn[96 * S], zrd[192 * S];
-    alignas(16) float dhp[96 * S];  // denoise candidate input prefixes (P1 -> P2)
+    alignas(16) float dhp[2][96 * S];  // denoise candidate input prefixes of frame f in slot f & 1
+    alignas(16) float zpre[192 * S];   // denoise z|r: b + the vad-state segment (P2 -> next P1)
     alignas(16) float gout[2][22 * S];  // denoise_output of frame f in slot f & 1
     alignas(16) float vo[S];  // vad_output of the frame P2 computed last
     float tt[204];
@@ -1185,8 +1225,8 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     const int wv = tq >> 6, ln = tq & 63;
     if (wv < 6) {
       if (fd >= 0 && fd < maxnf)
-        rnn_gates<5, S, G, 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, L.gdT[(fd + 1) & 1], L.zrd,
-                              kActSigmoid, L.tt, tq);
+        rnn_gates<5, S, G, 0, FVAD_GVPRE ? 5 : 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]},
+                                                  L.gdT[(fd + 1) & 1], L.zrd, kActSigmoid, L.tt, tq, L.zpre);
     } else if (wv == 6 || wv == 7 || wv == 10) {
       if (fn >= 0 && fn < maxnf)
         rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
@@ -1197,8 +1237,9 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
                               L.tt, (wv == 14 ? 64 : 0) + ln);
     } else if (wv == 12 || wv == 13 || wv == 15) {  // denoise candidate input prefixes of frame t-3
       if (fd >= 0 && fd < maxnf)
-        rnn_cand<6, S, G, 0, 1>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, nullptr, nullptr, nullptr,
-                                nullptr, 0, nullptr, (wv == 15 ? 128 : 64 * (wv - 12)) + ln, L.dhp);
+        rnn_cand<6, S, G, 0, FVAD_GVPRE ? 4 : 1>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, nullptr,
+                                                 nullptr, nullptr, nullptr, 0, nullptr,
+                                                 (wv == 15 ? 128 : 64 * (wv - 12)) + ln, L.dhp[fd & 1]);
     } else if (wv == 8 && ln < 48) {  // gain smoothing of frame t-5
       gains(t - 5, ln, 48);
     } else if (wv == 9 && ln < S) {  // spectral variability of frame t (features: P2 of step t-1)
@@ -1217,7 +1258,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     if (wv < 3) {
       if (fd >= 0 && fd < maxnf)
         rnn_cand<6, S, G, 0, 2>(L.W, RnnIn{nullptr, nullptr, nullptr}, L.gdT[(fd + 1) & 1], L.zrd, L.gdT[fd & 1],
-                                L.act[fd & 7], ra[6], L.tt, tq, L.dhp);
+                                L.act[fd & 7], ra[6], L.tt, tq, L.dhp[fd & 1]);
     } else if (wv == 3 || wv == 6) {
       if (FVAD_PRIO & 2) __builtin_amdgcn_s_setprio(3);
       if (fn >= 0 && fn < maxnf)
@@ -1244,9 +1285,25 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       // vad_output(t-2) -> L.vo, stored by the next step's P1
       if (fn >= 0 && fn < maxnf)
         rnn_gates<8, S, G, 0>(L.W, RnnIn{L.gvT[fn & 3], nullptr, nullptr}, nullptr, L.vo, ra[8], L.tt, ln);
+#if FVAD_GVPRE
+    } else if (tq >= kP2Feat && tq < kP2Feat + 192) {  // features of t+1 on waves 9..11
+      for (int idx = tq - kP2Feat; t + 1 < maxnf && idx < kFeatItems; idx += 192) feat_c(t + 1, idx);
+    } else if (wv >= 12 && wv <= 14) {  // denoise z|r of frame t-2: b + the vad-state segment
+      const int fz = t - 2;
+      if (fz >= 0 && fz < maxnf)
+        rnn_gates<5, S, G, 192, 3>(L.W, RnnIn{L.gvT[fz & 3], nullptr, nullptr}, nullptr, nullptr, kActSigmoid, L.tt,
+                                   tq - 768, L.zpre);
+    } else if (wv == 15) {  // denoise candidates of frame t-2: b + the vad-state segment
+      const int fz = t - 2;
+      if (fz >= 0 && fz < maxnf)
+        rnn_cand<6, S, G, 64, 3>(L.W, RnnIn{L.gvT[fz & 3], nullptr, nullptr}, nullptr, nullptr, nullptr, nullptr, 0,
+                                 nullptr, ln, L.dhp[fz & 1]);
+    }
+#else
     } else if (tq >= kP2Feat && tq < kP2Feat + kFeatItems) {
       if (t + 1 < maxnf) feat_c(t + 1, tq - kP2Feat);
     }
+#endif
     ROLE_END(1);
     lds_sync();
     RSTAMP(1);
