@@ -983,7 +983,8 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 //   P2  candidates of vad(t-1), noise(t-2), denoise(t-3) (denoise: its 96
 //       recurrent terms after the P1 prefix); dense(t); denoise_output(t-4);
 //       vad_output(t-2); features of t+1 (cepstral memory, deltas, distance
-//       row) -> LDS
+//       row) -> LDS; the denoise z|r gates' and candidates' first segment
+//       (b + the 24 vad-state terms) of frame t-2, continued by the next P1
 // Two barriers per step.  Every term keeps its C order; buffers are rings
 // indexed by frame (features 8, dense/vad state 4, noise/denoise state 2).
 // ---------------------------------------------------------------------------
@@ -1160,7 +1161,10 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   // h waves 0..2 (192 tasks; the 96 recurrent terms from the P1 prefix),
   // noise h waves 3, 6 (96), denoise_output wave 4 (44), vad h wave 5 (48),
   // dense of frame t wave 7 (48), vad_output wave 8 (2 lanes), features of
-  // frame t+1 waves 9..13 (296 items).  (Denoise h with 2 streams per lane on
+  // frame t+1 waves 9..11 (296 items, two per lane on the first 104), the
+  // denoise z|r first segments of frame t-2 waves 12..14 (384 tasks, two per
+  // lane), the denoise candidates' wave 15 (192, three per lane); without
+  // FVAD_GVPRE the features take waves 9..13.  (Denoise h with 2 streams per lane on
   // 6 waves shortened its chain to 11.1 k cycles but the extra waves
   // stretched the other roles: 15.3 vs 14.6 k per phase.)
   [[maybe_unused]] constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 448, kP2Out = 256, kP2VadOut = 512,
