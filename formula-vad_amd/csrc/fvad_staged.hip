@@ -991,12 +991,14 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 
 // P2 wave priorities (s_setprio while the role runs): bit 2 the noise h
 // waves, bit 4 denoise_output (kept: k_rnn3 1.19 -> 1.16 ms; both are young
-// waves that set P2's end), bit 8 vad h + dense (no gain; nor vad_output or
+// waves that set P2's end), bit 128 the denoise candidates' vad-state
+// segment wave 15 (kept: 1.141 -> 1.128 ms; the z|r segment waves 12-14
+// raised lost, 1.17), bit 8 vad h + dense (no gain; nor vad_output or
 // the feature waves raised: 1.17 -> 1.18 ms).  Raising P1's
 // noise or vad z|r waves above the denoise waves lost (1.16 -> 1.19 / 1.21 ms),
 // as did the denoise prefix waves (1.23 ms).
 #ifndef FVAD_PRIO
-#define FVAD_PRIO 6
+#define FVAD_PRIO 134
 #endif
 #ifndef FVAD_GVPRE
 #define FVAD_GVPRE 1
@@ -1299,9 +1301,11 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
                                    tq - 768, L.zpre);
     } else if (wv == 15) {  // denoise candidates of frame t-2: b + the vad-state segment
       const int fz = t - 2;
+      if (FVAD_PRIO & 128) __builtin_amdgcn_s_setprio(2);
       if (fz >= 0 && fz < maxnf)
         rnn_cand<6, S, G, 64, 3>(L.W, RnnIn{L.gvT[fz & 3], nullptr, nullptr}, nullptr, nullptr, nullptr, nullptr, 0,
                                  nullptr, ln, L.dhp[fz & 1]);
+      if (FVAD_PRIO & 128) __builtin_amdgcn_s_setprio(0);
     }
 #else
     } else if (tq >= kP2Feat && tq < kP2Feat + kFeatItems) {
