@@ -18,6 +18,7 @@
 // identical results.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -104,6 +105,12 @@ struct fvad_engine {
   int rnn_act[fvad::rnnimg::kMats] = {};
   long long *d_wstart = nullptr;
   int V = 0, L = 0, LX = 0, wmax = 0, grid_frames = 0;
+  int wpt = 1;  // window slots per (tick, stream): windows_per_tick(fft_size)
+  // FFT B above kMaxFftB: tables [tw | sup | hann | perm] and k_fftb's scratch
+  float *d_fbtab = nullptr;
+  float2 *d_fbwork = nullptr;
+  int fb_work_blocks = 0;
+  long long fb_work_stride = 0;
   int resident_ticks = 0;
   int n_kernels = 0;
   bool olafb = false;  // staged: k_olafb in place of k_ola, k_winmeta, k_fftbw (kernel 8)
@@ -298,7 +305,8 @@ void free_all(fvad_engine *e) {
                   e->d_model, e->d_stamps, e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->d_gru16, e->d_gru16_bias, e->vadm.st, e->vadm.buf,
-                  e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband};
+                  e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband,
+                  e->d_fbtab, e->d_fbwork};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &set : e->evs)
@@ -351,23 +359,40 @@ extern "C" int fvad_engine_reset(fvad_engine *e) {
   return FVAD_OK;
 }
 
+namespace {
+void fill_bands(const fvad_engine_config &c, int *band_lo, int *band_hi, int *lo_all, int *hi_all) {
+  int lo = 1 << 30, hi = -1;
+  for (int b = 0; b < fvad::kMaxBandCfg; b++) {
+    band_lo[b] = b < c.n_bands ? c.band_lo[b] : 0;
+    band_hi[b] = b < c.n_bands ? c.band_hi[b] : -1;
+    if (b < c.n_bands) {
+      lo = std::min(lo, c.band_lo[b]);
+      hi = std::max(hi, c.band_hi[b]);
+    }
+  }
+  *lo_all = lo;
+  *hi_all = hi;
+}
+
+}  // namespace
+
 extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_model *model, fvad_engine **out) {
   if (!cfg || !model || !out) return fail(FVAD_EINVAL, "null argument");
   const fvad_engine_config &c = *cfg;
   if (c.sample_rate != 48000) return fail(FVAD_ERATE, "only 48 kHz is supported (VAD.zig:101-104)");
   if (c.n_streams < 1 || c.n_channels < 1 || c.n_channels > FVAD_MAX_CHANNELS)
     return fail(FVAD_EINVAL, "n_streams >= 1 and 1 <= n_channels <= 8 required");
-  // FFT.zig:29-31 needs an even size; the engine's per-tick window outputs
-  // hold at most one window per 480-sample tick (fft_size >= 480), and one
-  // transform's work arrays stay in LDS (<= kMaxFftB)
-  if (c.fft_size < fvad::kFrame || (c.fft_size & 1) || c.fft_size > fvad::kMaxFftB)
-    return fail(FVAD_EINVAL, "fft_size must be even, 480 <= fft_size <= 16384");
+  // FFT.zig:29-31: any even, non-zero size.  fft_size < 480 completes several
+  // windows per tick (VAD.zig:307-347; fvad_engine_windows_per_tick slots per
+  // tick in the window outputs); kMaxFftSize keeps window indices in 32 bits
+  if (c.fft_size < 2 || (c.fft_size & 1) || c.fft_size > fvad::kMaxFftSize)
+    return fail(FVAD_EINVAL, "fft_size must be even, 2 <= fft_size <= 4194304 (FFT.zig:29-31)");
   if (c.mode == FVAD_MODE_FUSED) {
     int n = c.fft_size / 2;
     for (int p : {4, 2, 3, 5})
       while (n % p == 0) n /= p;
-    if (n != 1 || c.fft_size > 2048)
-      return fail(FVAD_EINVAL, "fused mode: fft_size <= 2048 with radices 2, 3, 4, 5 (use the staged mode)");
+    if (n != 1 || c.fft_size > 2048 || c.fft_size < fvad::kFrame)
+      return fail(FVAD_EINVAL, "fused mode: 480 <= fft_size <= 2048 with radices 2, 3, 4, 5 (use the staged mode)");
   }
   if (!c.use_denoiser && c.mode == FVAD_MODE_FUSED)
     return fail(FVAD_EINVAL, "use_denoiser = 0 runs on the staged engine");
@@ -426,7 +451,19 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
       return bail(fail(FVAD_EDEVICE, "hipEventCreate failed"));
   fvad::Plan *plan = new fvad::Plan();
   fvad::build_plan(plan, c.fft_size);
-  int rc = dalloc(&e->d_plan, 1);
+  e->wpt = fvad::windows_per_tick(c.fft_size);
+  int rc = FVAD_OK;
+  if (c.fft_size > fvad::kMaxFftB) {  // FFT B's tables outside the plan: [tw | sup | hann | perm]
+    const size_t n = c.fft_size;
+    std::vector<float> tab(n + n / 2 + n + n / 2);
+    int *perm = reinterpret_cast<int *>(tab.data() + n + n / 2 + n);
+    plan->norm_b = fvad::build_fftb_tables(c.fft_size, plan->fac_b, tab.data(), tab.data() + n, perm,
+                                           tab.data() + n + n / 2);
+    rc = dalloc(&e->d_fbtab, tab.size());
+    if (!rc && hipMemcpy(e->d_fbtab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail(FVAD_EDEVICE, "FFT-B table upload failed");
+  }
+  if (!rc) rc = dalloc(&e->d_plan, 1);
   if (!rc && hipMemcpy(e->d_plan, plan, sizeof(fvad::Plan), hipMemcpyHostToDevice) != hipSuccess)
     rc = fail(FVAD_EDEVICE, "plan upload failed");
   delete plan;
@@ -434,11 +471,12 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   if ((rc = upload_model(e, *fvad_model_host(model)))) return bail(rc);
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t frames = T * B * C * fvad::kFrame;
+  const size_t TBW = T * B * e->wpt;  // window slots
   if ((rc = dalloc(&e->d_state, B * fvad::st::kWords)) || (rc = dalloc(&e->d_ring, B * C * e->ring_len)) ||
       (rc = dalloc(&e->d_pcm_b[0], frames)) || (rc = dalloc(&e->d_pcm_b[1], frames)) ||
       (rc = dalloc(&e->d_ratio_b[0], T * B)) ||
-      (rc = dalloc(&e->d_vad, T * B)) || (rc = dalloc(&e->d_wratio, T * B)) || (rc = dalloc(&e->d_wvad, T * B)) ||
-      (rc = dalloc(&e->d_wflag, T * B)) || (rc = dalloc(&e->d_band, T * B * C * c.n_bands)) ||
+      (rc = dalloc(&e->d_vad, T * B)) || (rc = dalloc(&e->d_wratio, TBW)) || (rc = dalloc(&e->d_wvad, TBW)) ||
+      (rc = dalloc(&e->d_wflag, T * B)) || (rc = dalloc(&e->d_band, TBW * C * c.n_bands)) ||
       (rc = dalloc(&e->d_ticks_b[0], 2 * B)) || (c.want_denoised && (rc = dalloc(&e->d_den, frames))))
     return bail(rc);
   e->d_pcm = e->d_pcm_b[0];
@@ -476,6 +514,18 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "device query failed"));
     e->grid_frames = prop.multiProcessorCount;  // CUs; persistent grids are sized per kernel
+    // k_fftb's device scratch when a transform does not fit in LDS: a slice per
+    // workgroup, at most two per CU and 1 GiB
+    int lo = 0, hi = 0, band_lo[fvad::kMaxBandCfg], band_hi[fvad::kMaxBandCfg];
+    fill_bands(c, band_lo, band_hi, &lo, &hi);
+    e->fb_work_stride = fvad::fftb_work_stride(c.fft_size, lo, hi, fvad::fftb_generic(c.fft_size / 2));
+    if (e->fb_work_stride > 0) {
+      const long long per = e->fb_work_stride * (long long)sizeof(float2);
+      const long long units = (long long)B * e->wmax;
+      e->fb_work_blocks = (int)std::max<long long>(
+          1, std::min<long long>({units, 2LL * e->grid_frames, (1LL << 30) / per}));
+      if ((rc = dalloc(&e->d_fbwork, (size_t)e->fb_work_blocks * e->fb_work_stride))) return bail(rc);
+    }
   }
   if ((rc = fvad_engine_reset(e))) return bail(rc);
   *out = e;
@@ -494,20 +544,6 @@ extern "C" void fvad_engine_destroy(fvad_engine *e) {
 }
 
 namespace {
-
-void fill_bands(const fvad_engine_config &c, int *band_lo, int *band_hi, int *lo_all, int *hi_all) {
-  int lo = 1 << 30, hi = -1;
-  for (int b = 0; b < fvad::kMaxBandCfg; b++) {
-    band_lo[b] = b < c.n_bands ? c.band_lo[b] : 0;
-    band_hi[b] = b < c.n_bands ? c.band_hi[b] : -1;
-    if (b < c.n_bands) {
-      lo = std::min(lo, c.band_lo[b]);
-      hi = std::max(hi, c.band_hi[b]);
-    }
-  }
-  *lo_all = lo;
-  *hi_all = hi;
-}
 
 int launch_fused(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   const fvad_engine_config &c = e->cfg;
@@ -603,6 +639,23 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   a.win_tick = e->d_wtick;
   a.win_start = e->d_wstart;
   a.wmax = e->wmax;
+  a.wpt = e->wpt;
+  if (e->d_fbtab) {  // fft_size > kMaxFftB: [tw | sup | hann | perm] (fvad_engine_create)
+    const size_t n = c.fft_size;
+    a.fb_tw = reinterpret_cast<const float2 *>(e->d_fbtab);
+    a.fb_sup = reinterpret_cast<const float2 *>(e->d_fbtab + n);
+    a.fb_hann = e->d_fbtab + n + n / 2;
+    a.fb_perm = reinterpret_cast<const int *>(e->d_fbtab + n + n / 2 + n);
+  } else {  // the plan's own tables (device addresses inside d_plan)
+    const char *pb = reinterpret_cast<const char *>(e->d_plan);
+    a.fb_tw = reinterpret_cast<const float2 *>(pb + offsetof(fvad::Plan, twb));
+    a.fb_sup = reinterpret_cast<const float2 *>(pb + offsetof(fvad::Plan, superb));
+    a.fb_hann = reinterpret_cast<const float *>(pb + offsetof(fvad::Plan, hannb));
+    a.fb_perm = reinterpret_cast<const int *>(pb + offsetof(fvad::Plan, permb));
+  }
+  a.fb_work = e->d_fbwork;
+  a.fb_work_blocks = e->fb_work_blocks;
+  a.fb_work_stride = e->fb_work_stride;
   a.plan = e->d_plan;
   a.model = e->d_model;
   a.n_bands = c.n_bands;
@@ -724,7 +777,7 @@ int collect_vadm_timing(fvad_engine *e) {
 int fetch(fvad_engine *e, int n_ticks, fvad_outputs *o) {
   if (!o) return FVAD_OK;
   const fvad_engine_config &c = e->cfg;
-  const size_t TB = (size_t)n_ticks * c.n_streams;
+  const size_t TB = (size_t)n_ticks * c.n_streams, TBW = TB * e->wpt;
   auto cp = [&](void *dst, const void *src, size_t bytes) -> int {
     if (!dst) return FVAD_OK;
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
@@ -732,8 +785,8 @@ int fetch(fvad_engine *e, int n_ticks, fvad_outputs *o) {
   };
   int rc;
   if ((rc = cp(o->vad, e->d_vad, TB * 4)) || (rc = cp(o->ratio, e->d_ratio, TB * 4)) ||
-      (rc = cp(o->win_flag, e->d_wflag, TB * 4)) || (rc = cp(o->win_ratio, e->d_wratio, TB * 4)) ||
-      (rc = cp(o->win_vad, e->d_wvad, TB * 4)) || (rc = cp(o->band, e->d_band, TB * c.n_channels * c.n_bands * 4)))
+      (rc = cp(o->win_flag, e->d_wflag, TB * 4)) || (rc = cp(o->win_ratio, e->d_wratio, TBW * 4)) ||
+      (rc = cp(o->win_vad, e->d_wvad, TBW * 4)) || (rc = cp(o->band, e->d_band, TBW * c.n_channels * c.n_bands * 4)))
     return rc;
   if (o->denoised) {
     if (!e->d_den) return fail(FVAD_EINVAL, "engine created without want_denoised");
@@ -826,7 +879,7 @@ int ensure_slots(fvad_engine *e) {
   if (e->slots_ready) return FVAD_OK;
   const fvad_engine_config &c = e->cfg;
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
-  const size_t TB = T * B, frames = TB * C * fvad::kFrame;
+  const size_t TB = T * B, TBW = TB * e->wpt, frames = TB * C * fvad::kFrame;
   // the copy stream at the highest priority: its own hardware queue, so the
   // 16-bit ingest's k_pcm16 does not queue behind a long kernel of a stream
   // sharing its queue (it waited for k_vadm_hbm at the default priority)
@@ -842,8 +895,8 @@ int ensure_slots(fvad_engine *e) {
   for (auto &sl : e->slots) {
     int rc;
     if ((rc = host(&sl.in, frames)) || (rc = host(&sl.ticks, 2 * B)) || (rc = host(&sl.vad, TB)) ||
-        (rc = host(&sl.ratio, TB)) || (rc = host(&sl.wflag, TB)) || (rc = host(&sl.wratio, TB)) ||
-        (rc = host(&sl.wvad, TB)) || (rc = host(&sl.band, TB * C * c.n_bands)) ||
+        (rc = host(&sl.ratio, TB)) || (rc = host(&sl.wflag, TB)) || (rc = host(&sl.wratio, TBW)) ||
+        (rc = host(&sl.wvad, TBW)) || (rc = host(&sl.band, TBW * C * c.n_bands)) ||
         (c.want_denoised && (rc = host(&sl.den, frames))))
       return rc;
     if (hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) != hipSuccess ||
@@ -954,7 +1007,7 @@ int submit_any(fvad_engine *e, const Sample *pcm, int n_ticks, const int32_t *ti
   const int si = e->sub_next;
   auto &sl = e->slots[si];
   if (sl.pending) return fail(FVAD_EINVAL, "two pushes in flight: collect the older one first");
-  const size_t B = c.n_streams, TB = (size_t)n_ticks * B;
+  const size_t B = c.n_streams, TB = (size_t)n_ticks * B, TBW = TB * e->wpt;
   const size_t n_samples = TB * c.n_channels * fvad::kFrame, bytes = n_samples * sizeof(float);
   Sample *slot_in;
   if constexpr (k16)
@@ -1005,8 +1058,8 @@ int submit_any(fvad_engine *e, const Sample *pcm, int n_ticks, const int32_t *ti
     return FVAD_OK;
   };
   if ((rc = d2h(sl.vad, e->d_vad, TB * 4)) || (rc = d2h(sl.ratio, e->d_ratio, TB * 4)) ||
-      (rc = d2h(sl.wflag, e->d_wflag, TB * 4)) || (rc = d2h(sl.wratio, e->d_wratio, TB * 4)) ||
-      (rc = d2h(sl.wvad, e->d_wvad, TB * 4)) || (rc = d2h(sl.band, e->d_band, TB * c.n_channels * c.n_bands * 4)) ||
+      (rc = d2h(sl.wflag, e->d_wflag, TB * 4)) || (rc = d2h(sl.wratio, e->d_wratio, TBW * 4)) ||
+      (rc = d2h(sl.wvad, e->d_wvad, TBW * 4)) || (rc = d2h(sl.band, e->d_band, TBW * c.n_channels * c.n_bands * 4)) ||
       (c.want_denoised && (rc = d2h(sl.den, e->d_den, bytes))))
     return rc;
   HIP_TRY(hipEventRecord(sl.done, e->stream));
@@ -1052,7 +1105,7 @@ extern "C" int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_tic
   const fvad_engine_config &c = e->cfg;
   HIP_TRY(hipSetDevice(c.device));
   HIP_TRY(hipEventSynchronize(sl.done));
-  const size_t TB = (size_t)sl.n_ticks * c.n_streams;
+  const size_t TB = (size_t)sl.n_ticks * c.n_streams, TBW = TB * e->wpt;
   if (out) {
     if (out->denoised && !c.want_denoised) return fail(FVAD_EINVAL, "engine created without want_denoised");
     auto cp = [](void *dst, const void *src, size_t n) {
@@ -1061,9 +1114,9 @@ extern "C" int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_tic
     cp(out->vad, sl.vad, TB * 4);
     cp(out->ratio, sl.ratio, TB * 4);
     cp(out->win_flag, sl.wflag, TB * 4);
-    cp(out->win_ratio, sl.wratio, TB * 4);
-    cp(out->win_vad, sl.wvad, TB * 4);
-    cp(out->band, sl.band, TB * c.n_channels * c.n_bands * 4);
+    cp(out->win_ratio, sl.wratio, TBW * 4);
+    cp(out->win_vad, sl.wvad, TBW * 4);
+    cp(out->band, sl.band, TBW * c.n_channels * c.n_bands * 4);
     if (out->denoised) par_copy(out->denoised, sl.den, TB * c.n_channels * fvad::kFrame * 4);
   }
   if (n_ticks) *n_ticks = sl.n_ticks;
@@ -1206,6 +1259,8 @@ extern "C" int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out)
   return fetch(e, n_ticks, out);
 }
 
+extern "C" int fvad_engine_windows_per_tick(const fvad_engine *e) { return e ? e->wpt : FVAD_EINVAL; }
+
 extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
   if (e && i == e->n_kernels && e->vadm.n > 0) return "k_vadm_hbm";
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
@@ -1299,9 +1354,9 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
   e->vadm = v;
   e->vadm_init = std::move(init);
   e->vadm_buf_len = (size_t)off;
-  const size_t TB = (size_t)e->cfg.max_ticks * B;
-  if ((rc = dalloc(&e->d_vflag, TB)) || (rc = dalloc(&e->d_vwratio, TB)) || (rc = dalloc(&e->d_vwvad, TB)) ||
-      (rc = dalloc(&e->d_vband, TB * e->cfg.n_channels * e->cfg.n_bands)) || (rc = dalloc(&e->d_vticks, (size_t)B)))
+  const size_t TB = (size_t)e->cfg.max_ticks * B, TBW = TB * e->wpt;
+  if ((rc = dalloc(&e->d_vflag, TB)) || (rc = dalloc(&e->d_vwratio, TBW)) || (rc = dalloc(&e->d_vwvad, TBW)) ||
+      (rc = dalloc(&e->d_vband, TBW * e->cfg.n_channels * e->cfg.n_bands)) || (rc = dalloc(&e->d_vticks, (size_t)B)))
     return rc;
   if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_copy, hipEventDisableTiming) != hipSuccess ||

@@ -249,54 +249,10 @@ extern "C" size_t fvad_vadm_segments(const fvad_vadm *v, fvad_segment *out, size
   return segs.size();
 }
 
-// ---------------------------------------------------------------------------
-// Tick driver shared by the single-stream pipeline and the multi-stream core:
-// consumes engine outputs of n_ticks and feeds each stream's machines.
-// ---------------------------------------------------------------------------
 namespace {
 struct StreamMachines {
-  std::vector<VADMachine> machines;  // [0] = main
-  uint64_t windows_done = 0;
+  std::vector<VADMachine> machines;  // [0] = main; they run on the device (k_vadm_hbm)
 };
-
-struct TickBuffers {
-  std::vector<float> vad, ratio, win_ratio, win_vad, band;
-  std::vector<int32_t> win_flag;
-  void resize(size_t tb, int C, int nb) {
-    vad.resize(tb);
-    ratio.resize(tb);
-    win_ratio.resize(tb);
-    win_vad.resize(tb);
-    win_flag.resize(tb);
-    band.resize(tb * C * nb);
-  }
-  fvad_outputs outputs() {
-    fvad_outputs o;
-    std::memset(&o, 0, sizeof(o));
-    o.vad = vad.data();
-    o.ratio = ratio.data();
-    o.win_flag = win_flag.data();
-    o.win_ratio = win_ratio.data();
-    o.win_vad = win_vad.data();
-    o.band = band.data();
-    return o;
-  }
-};
-
-void consume(std::vector<StreamMachines *> &sm, const TickBuffers &tb, int n_ticks, int n_streams, int C, int nb,
-             int fft_size, const int32_t *ticks_valid) {
-  for (int s = 0; s < n_streams; s++) {
-    const int nt = ticks_valid ? ticks_valid[s] : n_ticks;
-    for (int t = 0; t < nt; t++) {
-      const size_t o = (size_t)t * n_streams + s;
-      if (!tb.win_flag[o]) continue;
-      const uint64_t index = sm[s]->windows_done * (uint64_t)fft_size;
-      for (auto &m : sm[s]->machines)
-        m.run(index, &tb.band[(o * C) * nb + m.band_slot], C, nb, tb.win_vad[o], tb.win_ratio[o]);
-      sm[s]->windows_done++;
-    }
-  }
-}
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -309,7 +265,6 @@ struct fvad_pipeline {
   StreamMachines sm;
   std::vector<std::vector<float>> pending;  // samples not yet forming a full 480 frame
   uint64_t total_write_count = 0;
-  TickBuffers tb;
   std::vector<float> pcm;
   // Recorder: raw input history [hist0, total_write_count) per channel, kept
   // from the earliest sample a capture that may still complete can start at
@@ -381,7 +336,6 @@ extern "C" int fvad_pipeline_create_ex(int sample_rate, int n_channels, const fv
     return rc;
   }
   p->pending.assign(n_channels, {});
-  p->tb.resize(p->ec.max_ticks, n_channels, p->ec.n_bands);
   p->pcm.resize((size_t)p->ec.max_ticks * n_channels * fvad::kFrame);
   *out = p;
   return FVAD_OK;

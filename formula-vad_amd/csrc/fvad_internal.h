@@ -22,11 +22,23 @@ constexpr int kMaxNeurons = 128;
 constexpr int kMaxCh = 8;
 constexpr int kMaxBandCfg = 4;
 
-// FFT B (FFT.zig) is a real FFT of fft_size: any even fft_size up to
-// kMaxFftB on the device (kissfft's mixed-radix factorisation; one transform's
-// work array, twice that with a radix > 5, stays in LDS).
+// FFT B (FFT.zig) is a real FFT of fft_size: any even fft_size (FFT.zig:29-31)
+// from 2 up to kMaxFftSize on the device (kissfft's mixed-radix
+// factorisation).  Up to kMaxFftB the tables live in the Plan and one
+// transform's work array (twice that with a radix > 5) stays in LDS; above it
+// the tables are separate device arrays and the work arrays device scratch.
+// kMaxFftSize keeps every per-window index in 32 bits (a 87 s window); the
+// real limit is memory: the re-block ring holds B * C * (fft_size + T * 480)
+// floats.
 constexpr int kMaxFftB = 16384;
+constexpr int kMaxFftSize = 1 << 22;
 constexpr int kMaxFactors = 32;
+
+// FFT-B windows that can complete in one 480-sample tick: one for fft_size >=
+// 480, else up to floor((fft_size - 1 + 480) / fft_size) -- the reference
+// splits one denoiser frame over several FFT-buffer writes (VAD.zig:307-347).
+// The engine's window outputs hold that many slots per (tick, stream).
+constexpr int windows_per_tick(int fft_size) { return fft_size >= kFrame ? 1 : (fft_size - 1 + kFrame) / fft_size; }
 
 // ---------------------------------------------------------------------------
 // Per-stream persistent state, one contiguous record per stream (the kernels
@@ -146,6 +158,12 @@ struct HostModel {
   std::size_t blob_size = 0;
 };
 
+// Every table of the plan; for nfft_b > kMaxFftB only FFT B's metadata
+// (sizes, factors, norm_b), the tables then come from build_fftb_tables.
 void build_plan(Plan *p, int nfft_b);
+// FFT B's tables for any even nfft_b into caller arrays: twb[nfft_b]
+// (nfft_b / 2 complex), superb[nfft_b / 2], permb[nfft_b / 2], hannb[nfft_b];
+// fac = kf_factor(nfft_b / 2) pairs.  Returns norm_b.
+float build_fftb_tables(int nfft_b, const int *fac, float *twb, float *superb, int *permb, float *hannb);
 
 }  // namespace fvad

@@ -121,18 +121,24 @@ void build_plan(Plan *p, int nfft_b) {
     if (p->fac_b[2 * i] > 5) p->generic_b = 1;
   }
   p->stages_b = st == p->nfac_b ? st : 0;
+  if (nfft_b <= kMaxFftB) p->norm_b = build_fftb_tables(nfft_b, p->fac_b, p->twb, p->superb, p->permb, p->hannb);
+}
+
+float build_fftb_tables(int nfft_b, const int *fac, float *twb, float *superb, int *permb, float *hannb) {
+  const double pi = 3.14159265358979323846;
+  const int nc = nfft_b / 2;
   for (int i = 0; i < nc; i++) {
     const double kpi = 3.141592653589793238462643383279502884197169399375105820974944;
     const double phase = -2 * kpi * i / nc;
-    p->twb[2 * i] = (float)std::cos(phase);
-    p->twb[2 * i + 1] = (float)std::sin(phase);
+    twb[2 * i] = (float)std::cos(phase);
+    twb[2 * i + 1] = (float)std::sin(phase);
   }
   for (int i = 0; i < nc / 2; i++) {
     const double phase = -3.14159265358979323846264338327 * ((double)(i + 1) / nc + .5);
-    p->superb[2 * i] = (float)std::cos(phase);
-    p->superb[2 * i + 1] = (float)std::sin(phase);
+    superb[2 * i] = (float)std::cos(phase);
+    superb[2 * i + 1] = (float)std::sin(phase);
   }
-  kiss_leaf_perm(p->permb, 0, 0, 1, p->fac_b);
+  kiss_leaf_perm(permb, 0, 0, 1, fac);
   // hannWindowPeriodic in f32 (2*pi coerced to f32, (2*pi*k*n)/N in f32, f32 cos)
   const float N = (float)nfft_b;
   const float two_pi = (float)(2.0 * pi);
@@ -145,12 +151,12 @@ void build_plan(Plan *p, int nfft_b) {
       const float arg = ((two_pi * kk) * nn) / N;
       acc += (sgn * 0.5f) * (float)std::cos((double)arg);
     }
-    p->hannb[i] = acc;
+    hannb[i] = acc;
   }
   float sum = 0;
-  for (int i = 0; i < nfft_b; i++) sum += p->hannb[i];
+  for (int i = 0; i < nfft_b; i++) sum += hannb[i];
   const float window_norm = (float)nfft_b / sum;
-  p->norm_b = window_norm / (float)(nfft_b / 2);
+  return window_norm / (float)(nfft_b / 2);
 }
 
 }  // namespace fvad

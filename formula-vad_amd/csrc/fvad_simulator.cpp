@@ -11,7 +11,7 @@
 //   48 kHz) — libsndfile/ogg are not available, see DESIGN.md.
 //   Instances run in lock-step on the GPU(s) (simulator.zig:217-228 spawns one
 //   thread per instance instead), streamed from their files push by push
-//   (preload_audio: read whole first); any even fft_size >= 480,
+//   (preload_audio: read whole first); any even fft_size (FFT.zig:29-31),
 //   use_denoiser, alternative machines (run on the device; like the
 //   reference, only the main machine's segments are reported); instances may
 //   differ in channel count.  audio_read_frame_count does not change results

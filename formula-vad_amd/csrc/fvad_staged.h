@@ -89,9 +89,19 @@ struct StagedArgs {
   float *ys;               // [f][960] windowed synthesis output
   float *ring;             // [s][c][ring_len]
   int ring_len;
-  int *win_tick;           // [s][wmax] tick at which window j completes (-1: none)
+  int *win_tick;           // [s][wmax] output slot of window j: tick * wpt + (its rank in the tick); -1: none
   long long *win_start;    // [s][wmax] absolute sample index of window j
   int wmax;
+  int wpt;                 // window slots per (tick, stream) of the outputs: windows_per_tick(fft_size)
+  // FFT B's tables (the Plan's up to kMaxFftB, separate device arrays above)
+  // and, when a transform does not fit in LDS, k_fftb's device scratch:
+  // fb_work_blocks workgroups, fb_work_stride float2 each
+  const float2 *fb_tw, *fb_sup;
+  const int *fb_perm;
+  const float *fb_hann;
+  float2 *fb_work;
+  int fb_work_blocks;
+  long long fb_work_stride;
   const Plan *plan;
   const DevModel *model;
   int n_bands;
@@ -100,6 +110,9 @@ struct StagedArgs {
   int wave_static;             // wave kernels with static batch striding: bit 1 << WaveKernel
   int band_lo[kMaxBandCfg], band_hi[kMaxBandCfg];
   int bin_lo_all, bin_hi_all;
+  // per (tick, stream): out_vad, out_win_flag (windows completed in the tick,
+  // 0..wpt); per window slot [t][s][wpt]: out_win_ratio, out_win_vad, and
+  // out_band [t][s][wpt][c][band]
   float *out_vad, *out_win_ratio, *out_win_vad, *out_band, *out_den;
   int *out_win_flag;
   int raw_s16;
@@ -134,6 +147,9 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
 hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream);
 // use_denoiser = 0 (VAD.zig:206-212,239-249): k_ndring, k_ndmeta, FFT B
 hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream);
+// k_fftb's scratch need: 0 when a transform fits in LDS, else float2 per workgroup
+long long fftb_work_stride(int nfft_b, int bin_lo_all, int bin_hi_all, int generic);
+bool fftb_generic(int nc);  // kf_factor(nc) has a radix > 5
 // 16-bit ingest: dst[i] = src[i] / 32768.0f (exact), n a multiple of 8
 hipError_t launch_pcm16(const int16_t *src, float *dst, size_t n, hipStream_t stream);
 // fp16 / MFMA recurrence (fvad_gru16.hip), run in k_rnn3's place when a.gru16_frags is set

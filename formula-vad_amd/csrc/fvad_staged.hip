@@ -1419,7 +1419,7 @@ __global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
       int *istp = reinterpret_cast<int *>(stp);
       int fd = istp[st::kFramesDone];
       float vol = stp[st::kVolAcc];
-      const int FB = a.plan->nfft_b;
+      const int FB = a.plan->nfft_b, wpt = a.wpt;
       // the per-tick inputs (ratio, vad) of 8 ticks load before any of their
       // outputs is stored (stores between the loads would serialise them)
       constexpr int kWmT = 8;
@@ -1435,31 +1435,38 @@ __global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
         for (int u = 0; u < kWmT; u++) {
           const int t = t0 + u;
           if (t < nt) {
-          const size_t o = (size_t)t * a.n_streams + s;
-          const float ratio = rr[u];
-          const long long a0 = (long long)fd * kFrame;
-          const long long wdone = a0 / FB;
-          const long long next_end = (wdone + 1) * FB;
-          const bool complete = a0 + kFrame >= next_end;
-          if (complete) {
-            const int r = (int)(next_end - a0);
-            vol += ratio * ((float)r / (float)FB);
-            a.out_win_ratio[o] = vol;
-            a.out_win_vad[o] = vv[u];
-            vol = 0;
-            if (kFrame - r > 0) vol += ratio * ((float)(kFrame - r) / (float)FB);
-            wt[j] = t;
-            wsx[j] = wdone * FB;
-            j++;
-          } else {
-            vol += ratio * ((float)kFrame / (float)FB);
-            a.out_win_ratio[o] = 0.0f;
-            a.out_win_vad[o] = 0.0f;
-            // no window completes in this tick: band sums are defined as 0
-            for (int i = 0; i < a.n_channels * a.n_bands; i++) a.out_band[o * a.n_channels * a.n_bands + i] = 0.0f;
-          }
-          a.out_win_flag[o] = complete ? 1 : 0;
-          fd++;
+            const size_t o = (size_t)t * a.n_streams + s, ow = o * wpt;
+            const float ratio = rr[u];
+            // fftBufferStep (VAD.zig:307-347): the frame goes into the FFT
+            // buffer in pieces of min(room left, samples left); each piece
+            // adds ratio * written / fft_size, a full buffer is a window
+            // (vad = this frame's); fft_size < 480 completes several per tick
+            const long long a0 = (long long)fd * kFrame;
+            int off = 0, nw = 0;
+            while (off < kFrame) {
+              const long long pos = a0 + off, wdone = pos / FB, next_end = (wdone + 1) * FB;
+              const int written = (int)min((long long)(kFrame - off), next_end - pos);
+              vol += ratio * ((float)written / (float)FB);
+              off += written;
+              if (pos + written == next_end) {
+                a.out_win_ratio[ow + nw] = vol;
+                a.out_win_vad[ow + nw] = vv[u];
+                vol = 0;
+                wt[j] = t * wpt + nw;
+                wsx[j] = wdone * FB;
+                j++;
+                nw++;
+              }
+            }
+            // slots without a window: band sums, ratio and vad defined as 0
+            for (int w = nw; w < wpt; w++) {
+              a.out_win_ratio[ow + w] = 0.0f;
+              a.out_win_vad[ow + w] = 0.0f;
+              for (int i = 0; i < a.n_channels * a.n_bands; i++)
+                a.out_band[(ow + w) * a.n_channels * a.n_bands + i] = 0.0f;
+            }
+            a.out_win_flag[o] = nw;
+            fd++;
           }
         }
       }
@@ -1500,69 +1507,82 @@ __global__ void __launch_bounds__(64) k_winmeta(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_fftb: one workgroup per (stream, completed window): FFT B per channel
+// k_fftb: one workgroup per (stream, completed window): FFT B per channel.
+// kLds: the transform's work arrays in dynamic LDS (fft_size <= kMaxFftB);
+// otherwise each of the grid's workgroups owns a slice of device scratch and
+// walks the (stream, window) units grid-stride.  Output index of a window:
+// its slot (tick * wpt + rank in the tick, k_winmeta / k_ndmeta).
 // ---------------------------------------------------------------------------
-template <int NT>
+__device__ __forceinline__ size_t win_out(const StagedArgs &a, int s, int slot) {
+  const int t = slot / a.wpt;
+  return ((size_t)t * a.n_streams + s) * a.wpt + (slot - t * a.wpt);
+}
+
+template <int NT, bool kLds>
 __global__ void __launch_bounds__(NT) k_fftb(StagedArgs a) {
-  // dynamic LDS: W[nc] (+ S[nc] with a radix > 5), then the magnitudes of
-  // the reported bins
-  extern __shared__ __attribute__((aligned(16))) float2 W[];
+  // W[nc] (+ S[nc] with a radix > 5), then the magnitudes of the reported bins
+  extern __shared__ __attribute__((aligned(16))) float2 Wl[];
   const Plan *__restrict__ P = a.plan;
   const int nc = P->ncfft_b, C = a.n_channels;
+  float2 *W = kLds ? Wl : a.fb_work + (size_t)blockIdx.x * a.fb_work_stride;
   float2 *S = W + nc;
   float *mag = reinterpret_cast<float *>(W + (P->generic_b ? 2 * nc : nc));
   const int tid = threadIdx.x;
-  const int s = blockIdx.x / a.wmax, j = blockIdx.x - s * a.wmax;
-  if (s >= a.n_streams) return;
-  const int t = a.win_tick[(size_t)s * a.wmax + j];
-  if (t < 0) return;
-  const long long wstart = a.win_start[(size_t)s * a.wmax + j];
-  const float2 *__restrict__ twb = reinterpret_cast<const float2 *>(P->twb);
-  const float2 *__restrict__ sup = reinterpret_cast<const float2 *>(P->superb);
-  const size_t o = (size_t)t * a.n_streams + s;
-  for (int c = 0; c < C; c++) {
-    const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
-    for (int k = tid; k < nc; k += NT) {
-      const int n = P->permb[k];
-      const float t0 = ring[(wstart + 2 * n) % a.ring_len] * P->hannb[2 * n];
-      const float t1 = ring[(wstart + 2 * n + 1) % a.ring_len] * P->hannb[2 * n + 1];
-      W[k] = make_float2(t0, t1);
-    }
-    __syncthreads();
-    kiss_stages(W, S, P->fac_b, P->nfac_b, nc, twb, tid, NT);
-    const int lo = a.bin_lo_all, hi = a.bin_hi_all;
-    for (int k = lo + tid; k <= hi; k += NT) {
-      float re, imv;
-      if (k == 0) {
-        re = W[0].x + W[0].y;
-        imv = 0;
-      } else if (k == nc) {
-        re = W[0].x - W[0].y;
-        imv = 0;
-      } else {
-        const int kk = (2 * k < nc) ? k : nc - k;
-        const float2 fpk = W[kk];
-        const float2 fpnk = make_float2(W[nc - kk].x, -W[nc - kk].y);
-        const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
-        const float2 tw2 = cmul(f2k, sup[kk - 1]);
-        if (2 * k < nc) {
-          re = (f1k.x + tw2.x) * ((float).5);
-          imv = (f1k.y + tw2.y) * ((float).5);
-        } else {
-          re = (f1k.x - tw2.x) * ((float).5);
-          imv = (tw2.y - f1k.y) * ((float).5);
-        }
+  const float2 *__restrict__ twb = a.fb_tw;
+  const float2 *__restrict__ sup = a.fb_sup;
+  const int *__restrict__ perm = a.fb_perm;
+  const float *__restrict__ hann = a.fb_hann;
+  const long long units = (long long)a.n_streams * a.wmax;
+  for (long long unit = blockIdx.x; unit < units; unit += gridDim.x) {
+    const int s = (int)(unit / a.wmax), j = (int)(unit - (long long)s * a.wmax);
+    const int slot = a.win_tick[(size_t)s * a.wmax + j];
+    if (slot < 0) continue;  // uniform over the workgroup
+    const long long wstart = a.win_start[(size_t)s * a.wmax + j];
+    const size_t o = win_out(a, s, slot);
+    for (int c = 0; c < C; c++) {
+      const float *ring = a.ring + ((size_t)s * C + c) * a.ring_len;
+      for (int k = tid; k < nc; k += NT) {
+        const int n = perm[k];
+        const float t0 = ring[(wstart + 2 * n) % a.ring_len] * hann[2 * n];
+        const float t1 = ring[(wstart + 2 * n + 1) % a.ring_len] * hann[2 * n + 1];
+        W[k] = make_float2(t0, t1);
       }
-      const float r2 = re * re, i2 = imv * imv;
-      mag[k - lo] = sqrtf(r2 + i2) * P->norm_b;
+      __syncthreads();
+      kiss_stages(W, S, P->fac_b, P->nfac_b, nc, twb, tid, NT);
+      const int lo = a.bin_lo_all, hi = a.bin_hi_all;
+      for (int k = lo + tid; k <= hi; k += NT) {
+        float re, imv;
+        if (k == 0) {
+          re = W[0].x + W[0].y;
+          imv = 0;
+        } else if (k == nc) {
+          re = W[0].x - W[0].y;
+          imv = 0;
+        } else {
+          const int kk = (2 * k < nc) ? k : nc - k;
+          const float2 fpk = W[kk];
+          const float2 fpnk = make_float2(W[nc - kk].x, -W[nc - kk].y);
+          const float2 f1k = cadd(fpk, fpnk), f2k = csub(fpk, fpnk);
+          const float2 tw2 = cmul(f2k, sup[kk - 1]);
+          if (2 * k < nc) {
+            re = (f1k.x + tw2.x) * ((float).5);
+            imv = (f1k.y + tw2.y) * ((float).5);
+          } else {
+            re = (f1k.x - tw2.x) * ((float).5);
+            imv = (tw2.y - f1k.y) * ((float).5);
+          }
+        }
+        const float r2 = re * re, i2 = imv * imv;
+        mag[k - lo] = sqrtf(r2 + i2) * P->norm_b;
+      }
+      __syncthreads();
+      if (tid < a.n_bands) {
+        float acc = 0.0f;
+        for (int k = a.band_lo[tid]; k <= a.band_hi[tid]; k++) acc += mag[k - lo];
+        a.out_band[(o * C + c) * a.n_bands + tid] = acc;
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    if (tid < a.n_bands) {
-      float acc = 0.0f;
-      for (int k = a.band_lo[tid]; k <= a.band_hi[tid]; k++) acc += mag[k - lo];
-      a.out_band[(o * C + c) * a.n_bands + tid] = acc;
-    }
-    __syncthreads();
   }
 }
 
@@ -1672,9 +1692,11 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
   VadmState S = a.vadm.st[(size_t)m * B + s];
   float *st = a.vadm.buf + K.st_off + s, *rb = a.vadm.buf + K.r_off + s;
   VadmSeg *seg = a.vadm.seg + ((size_t)m * B + s) * a.vadm.seg_cap;
-  for (int t = 0; t < nt; t++) {
-    const size_t o = (size_t)t * B + s;
-    if (!a.out_win_flag[o]) continue;
+  // every window of the push in order: ticks, then a tick's slots (several
+  // when fft_size < 480)
+  for (int t = 0; t < nt; t++)
+    for (int w = 0, nw = a.out_win_flag[(size_t)t * B + s]; w < nw; w++) {
+    const size_t o = ((size_t)t * B + s) * a.wpt + w;
     const unsigned long long index = S.windows_done * fft;
     S.windows_done++;
     float min_v = 999, max_v = 0;
@@ -1825,8 +1847,8 @@ __global__ void __launch_bounds__(256) k_ndring(StagedArgs a) {
 }
 
 // k_ndmeta: window completion per tick (a window completes in the tick that
-// brings its last sample), lane per stream; the completed windows' volume
-// ratios are k_ndvol's.
+// brings its last sample; fft_size < 480: several per tick), lane per stream;
+// the completed windows' volume ratios are k_ndvol's.
 __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
   const int s = blockIdx.x * 64 + threadIdx.x;
   if (s >= a.n_streams) return;
@@ -1838,23 +1860,25 @@ __global__ void __launch_bounds__(64) k_ndmeta(StagedArgs a) {
     unsigned long long *cnt = nd_count(a, s);
     const unsigned long long sd0 = *cnt;
     for (int t = 0; t < nt; t++) {
-      const size_t o = (size_t)t * a.n_streams + s;
+      const size_t o = (size_t)t * a.n_streams + s, ow = o * a.wpt;
+      // the tick's samples [a0, end) complete every window ending in (a0, end]
+      // (fft_size < 480: several)
       const unsigned long long a0 = sd0 + (unsigned long long)t * kFrame;
-      const unsigned long long wdone = a0 / (unsigned)FB;
-      const unsigned long long next_end = (wdone + 1) * (unsigned)FB;
-      const bool complete = a0 + (unsigned)nd_real(a, s, t, nt) >= next_end;
-      if (complete) {
-        const unsigned long long ws = wdone * (unsigned)FB;
-        a.out_win_vad[o] = -1.0f;
-        wt[j] = t;
-        wsx[j] = (long long)ws;
+      const unsigned long long end = a0 + (unsigned)nd_real(a, s, t, nt);
+      unsigned long long next_end = (a0 / (unsigned)FB + 1) * (unsigned)FB;
+      int nw = 0;
+      for (; next_end <= end; next_end += (unsigned)FB, nw++) {
+        a.out_win_vad[ow + nw] = -1.0f;
+        wt[j] = t * a.wpt + nw;
+        wsx[j] = (long long)(next_end - (unsigned)FB);
         j++;
-      } else {
-        a.out_win_ratio[o] = 0.0f;
-        a.out_win_vad[o] = 0.0f;
-        for (int i = 0; i < C * a.n_bands; i++) a.out_band[o * C * a.n_bands + i] = 0.0f;
       }
-      a.out_win_flag[o] = complete ? 1 : 0;
+      for (int w = nw; w < a.wpt; w++) {
+        a.out_win_ratio[ow + w] = 0.0f;
+        a.out_win_vad[ow + w] = 0.0f;
+        for (int i = 0; i < C * a.n_bands; i++) a.out_band[(ow + w) * C * a.n_bands + i] = 0.0f;
+      }
+      a.out_win_flag[o] = nw;
     }
     *cnt = sd0 + (unsigned long long)(nt - 1) * kFrame + (unsigned)nd_real(a, s, nt - 1, nt);
   }
@@ -1889,7 +1913,7 @@ __global__ void __launch_bounds__(64) k_ndvol(StagedArgs a) {
     if (vol < vol_min) vol_min = vol;
     if (vol > vol_max) vol_max = vol;
   }
-  a.out_win_ratio[(size_t)t * a.n_streams + s] = vol_max == 0 ? 0.0f : vol_min / vol_max;
+  a.out_win_ratio[win_out(a, s, t)] = vol_max == 0 ? 0.0f : vol_min / vol_max;
 }
 
 // every launch is checked where it is issued: a failed launch in the middle of
@@ -1905,29 +1929,48 @@ __global__ void __launch_bounds__(64) k_ndvol(StagedArgs a) {
     FVAD_LAUNCH_TRY(hipGetLastError());        \
   } while (0)
 
-// k_fftb's dynamic LDS: the transform (twice with a radix > 5) + reported bins
-size_t fftb_lds_bytes(const StagedArgs &a) {
-  const int nc = a.nfft_b / 2;
-  int n = nc, generic = 0;
-  for (int p = 2; p * p <= n; p++)
-    while (n % p == 0) {
-      generic |= p > 5;
-      n /= p;
-    }
-  generic |= n > 5;
-  return sizeof(float2) * (size_t)nc * (generic ? 2 : 1) + sizeof(float) * (a.bin_hi_all - a.bin_lo_all + 1);
+// FFT B of every completed window: the wave-per-window kernel for 2048 points
+// (one window per tick at most), the block kernel k_fftb (mixed radix) for
+// every other size -- work arrays in LDS up to kMaxFftB and 160 KB, else in
+// device scratch (the engine sizes a.fb_work by fftb_work_stride)
+bool fftb_generic(int nc) {  // kf_factor(nc) has a radix > 5
+  int n = nc;
+  for (int p : {4, 2, 3, 5})
+    while (n % p == 0) n /= p;
+  return n > 1;
 }
 
-// FFT B: the wave-per-window kernel for 2048 points, the block kernel
-// (mixed radix, dynamic LDS) for every other size
+long long fftb_work_stride(int nfft_b, int bin_lo_all, int bin_hi_all, int generic) {
+  const long long nc = nfft_b / 2, bins = bin_hi_all - bin_lo_all + 1;
+  const long long lds = (long long)sizeof(float2) * nc * (generic ? 2 : 1) + (long long)sizeof(float) * bins;
+  if (nfft_b <= kMaxFftB && lds <= 160 * 1024) return 0;
+  return (nc * (generic ? 2 : 1) + (bins + 1) / 2 + 1) & ~1LL;  // float2 units, 16-byte aligned slices
+}
+
 hipError_t launch_fftb(const StagedArgs &a, int n_cu, hipStream_t stream) {
   if (a.nfft_b == 2048) return launch_wave(kWaveFftB, a, n_cu, stream);
   static const bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fftb<256>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    bool ok = true;
+    for (const void *k : {reinterpret_cast<const void *>(&k_fftb<256, true>),
+                          reinterpret_cast<const void *>(&k_fftb<64, true>)})
+      ok &= hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    return ok;
   }();
   (void)attr;
-  FVAD_KERNEL_TRY(k_fftb<256>, dim3(a.n_streams * a.wmax), dim3(256), fftb_lds_bytes(a), stream, a);
+  const long long units = (long long)a.n_streams * a.wmax;
+  if (a.fb_work) {
+    const unsigned grid = (unsigned)std::min<long long>(units, a.fb_work_blocks);
+    FVAD_KERNEL_TRY((k_fftb<256, false>), dim3(grid), dim3(256), 0, stream, a);
+    return hipSuccess;
+  }
+  const int nc = a.nfft_b / 2;
+  const size_t lds = sizeof(float2) * (size_t)nc * (fftb_generic(nc) ? 2 : 1) +
+                     sizeof(float) * (size_t)(a.bin_hi_all - a.bin_lo_all + 1);
+  const unsigned grid = (unsigned)std::min<long long>(units, 1 << 16);
+  if (nc <= 64)  // fft_size <= 128: a wave per window
+    FVAD_KERNEL_TRY((k_fftb<64, true>), dim3(grid), dim3(64), lds, stream, a);
+  else
+    FVAD_KERNEL_TRY((k_fftb<256, true>), dim3(grid), dim3(256), lds, stream, a);
   return hipSuccess;
 }
 

@@ -154,6 +154,7 @@ SYMBOLS = [
     ("fvad_engine_sync", C.c_int, [C.c_void_p]),
     ("fvad_engine_kernel_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("fvad_engine_kernel_name", C.c_char_p, [C.c_void_p, C.c_int]),
+    ("fvad_engine_windows_per_tick", C.c_int, [C.c_void_p]),
     ("fvad_engine_attach_vadm", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     ("fvad_engine_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
     ("fvad_engine_segments_range", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_size_t]),
@@ -293,12 +294,16 @@ class Engine:
         self.h = h
         self.B, self.C, self.nb = n_streams, n_channels, len(bands)
         self.max_ticks = max_ticks
+        # window slots per (tick, stream): 1 for fft_size >= 480, else several
+        # (VAD.zig:307-347); with W > 1 the window outputs get a slot axis
+        self.wpt = lib().fvad_engine_windows_per_tick(h)
 
     def _alloc_out(self, n_ticks, denoised):
-        T, B, Ch, nb = n_ticks, self.B, self.C, self.nb
+        T, B, Ch, nb, W = n_ticks, self.B, self.C, self.nb, self.wpt
+        ws = (T, B) if W == 1 else (T, B, W)
         o = {"vad": np.zeros((T, B), np.float32), "ratio": np.zeros((T, B), np.float32),
-             "win_flag": np.zeros((T, B), np.int32), "win_ratio": np.zeros((T, B), np.float32),
-             "win_vad": np.zeros((T, B), np.float32), "band": np.zeros((T, B, Ch, nb), np.float32)}
+             "win_flag": np.zeros((T, B), np.int32), "win_ratio": np.zeros(ws, np.float32),
+             "win_vad": np.zeros(ws, np.float32), "band": np.zeros(ws + (Ch, nb), np.float32)}
         if denoised:
             o["denoised"] = np.zeros((T, B, Ch, FRAME), np.float32)
         s = Outputs(fptr(o["vad"]), fptr(o["ratio"]), o["win_flag"].ctypes.data_as(I32P), fptr(o["win_ratio"]),

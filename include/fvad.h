@@ -104,7 +104,9 @@ typedef struct {
   int n_channels;       /* channels per stream (2 = onboard stereo) */
   int device;           /* HIP device ordinal */
   int sample_rate;      /* must be 48000 */
-  int fft_size;         /* VAD.Config.fft_size: even, 480..16384 (fused mode: radices 2..5, <= 2048) */
+  int fft_size;         /* VAD.Config.fft_size: even, 2..4194304 (FFT.zig:29-31; fused mode: 480..2048,
+                         * radices 2..5).  Below 480 one tick completes several windows (VAD.zig:307-347):
+                         * see fvad_engine_windows_per_tick */
   int max_ticks;        /* largest n_ticks per push */
   int n_bands;          /* band sums to report per window, 1..4 */
   int band_lo[FVAD_MAX_BANDS]; /* inclusive FFT-B bin ranges (FFT.freqToBin) */
@@ -135,16 +137,26 @@ void fvad_engine_destroy(fvad_engine *e);
 int fvad_engine_reset(fvad_engine *e);
 
 /* Per-tick outputs, host arrays owned by the caller, indexed [tick][stream]...
- * Any pointer may be NULL to skip that output. */
+ * Any pointer may be NULL to skip that output.  The window outputs have W =
+ * fvad_engine_windows_per_tick(e) slots per (tick, stream): W = 1 for fft_size
+ * >= 480 (the layout is then [ticks][streams]...), more below 480, where one
+ * 480-sample frame fills several FFT buffers (VAD.zig:307-347); slot w < the
+ * tick's win_flag holds the tick's w-th completed window, in sample order. */
 typedef struct {
   float *vad;          /* [ticks][streams]  min over channels of rnnoise vad (VAD.zig:284-293) */
   float *ratio;        /* [ticks][streams]  preAnalyzeSegment volume ratio (VAD.zig:253-272) */
-  int32_t *win_flag;   /* [ticks][streams]  1 if an FFT-B window completed in this tick */
-  float *win_ratio;    /* [ticks][streams]  share-weighted window volume ratio (VAD.zig:319-325) */
-  float *win_vad;      /* [ticks][streams]  window vad = last frame's vad (VAD.zig:330) */
-  float *band;         /* [ticks][streams][channels][n_bands] band sums (PipelineFFT.zig:99-112); 0 where win_flag is 0 */
+  int32_t *win_flag;   /* [ticks][streams]  FFT-B windows completed in this tick (0..W; 0 or 1 when W = 1) */
+  float *win_ratio;    /* [ticks][streams][W]  share-weighted window volume ratio (VAD.zig:319-325) */
+  float *win_vad;      /* [ticks][streams][W]  window vad = last frame's vad (VAD.zig:330) */
+  float *band;         /* [ticks][streams][W][channels][n_bands] band sums (PipelineFFT.zig:99-112); 0 in
+                        * slots without a window */
   float *denoised;     /* [ticks][streams][channels][480] normalised denoised PCM (want_denoised) */
 } fvad_outputs;
+
+/* W, the window slots per (tick, stream) of fvad_outputs: 1 for fft_size >=
+ * 480, else floor((fft_size - 1 + 480) / fft_size) -- the most windows one
+ * tick can complete */
+int fvad_engine_windows_per_tick(const fvad_engine *e);
 
 /* pcm: host [ticks][streams][channels][480] normalised f32.  ticks_valid
  * (nullable): stream s only consumes its first ticks_valid[s] ticks (ragged
@@ -266,7 +278,7 @@ int fvad_engine_vadm_state(fvad_engine *e, int stream, int machine, int *speech_
 
 /* VAD.Config (VAD.zig:17-23) */
 typedef struct {
-  int fft_size;                                     /* even, 480..16384 (FFT.zig:28-31) */
+  int fft_size;                                     /* even, 2..4194304 (FFT.zig:28-31) */
   int use_denoiser;                                 /* 0: fft_size frames of raw input to FFT B */
   fvad_vadm_config vad_machine_config;              /* main machine */
   const fvad_vadm_config *alt_vad_machine_configs;  /* alternative machines (training), nullable */

@@ -46,28 +46,38 @@ def engine_run(fvad, engine, streams, chunk_ticks, denoised=True):
                 seg = x[:, t0 * FRAME:(t0 + v) * FRAME].reshape(Ch, v, FRAME)
                 pcm[:v, s] = seg.transpose(1, 0, 2)
         outs.append((engine.push(pcm, ticks_valid=valid, denoised=denoised), valid))
+    W = getattr(engine, "wpt", 1)
     per = []
     for s in range(B):
         vad, ratio, wf, wr, wv, band, den = [], [], [], [], [], [], []
         for o, valid in outs:
             v = valid[s]
+            cnt = o["win_flag"][:v, s]
             vad.append(o["vad"][:v, s])
             ratio.append(o["ratio"][:v, s])
-            wf.append(o["win_flag"][:v, s])
-            wr.append(o["win_ratio"][:v, s])
-            wv.append(o["win_vad"][:v, s])
-            band.append(o["band"][:v, s])
+            wf.append(cnt)
+            wr.append(tick_windows(o["win_ratio"][:v, s], cnt, W))
+            wv.append(tick_windows(o["win_vad"][:v, s], cnt, W))
+            band.append(tick_windows(o["band"][:v, s], cnt, W))
             if denoised:
                 den.append(o["denoised"][:v, s])
-        wf = np.concatenate(wf).astype(bool)
-        r = {"vad": np.concatenate(vad), "ratio": np.concatenate(ratio), "win_flag": wf,
-             "win_ratio": np.concatenate(wr)[wf], "win_vad": np.concatenate(wv)[wf],
-             "band": np.concatenate(band)[wf]}
+        r = {"vad": np.concatenate(vad), "ratio": np.concatenate(ratio), "win_flag": np.concatenate(wf),
+             "win_ratio": np.concatenate(wr), "win_vad": np.concatenate(wv), "band": np.concatenate(band)}
         if denoised:
             d = np.concatenate(den)  # [T][Ch][480]
             r["denoised"] = d.transpose(1, 0, 2).reshape(Ch, -1)
         per.append(r)
     return per
+
+
+def tick_windows(x, counts, W):
+    """The completed windows of one stream's ticks, in sample order: x is
+    [ticks]... (W == 1) or [ticks][W]... (window slots), counts the ticks'
+    win_flag (windows completed per tick)."""
+    counts = np.asarray(counts)
+    if W == 1:
+        return x[counts.astype(bool)]
+    return x[np.arange(W)[None, :] < counts[:, None]]
 
 
 def first_mismatch(a, b):

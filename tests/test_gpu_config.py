@@ -1,6 +1,7 @@
 """VAD.Config beyond the defaults on the device path, bit-exact against the
-oracle: any even fft_size (FFT.zig:28-31; kissfft mixed radix on the GPU) and
-use_denoiser = false (VAD.zig:206-212,239-249: fft_size frames of raw input
+oracle: any even fft_size (FFT.zig:28-31; kissfft mixed radix on the GPU) --
+below 480 one denoiser frame fills several FFT buffers (VAD.zig:307-347), above
+16384 FFT B works in device scratch -- and use_denoiser = false (VAD.zig:206-212,239-249: fft_size frames of raw input
 straight to FFT B, window ratio = preAnalyzeSegment over the frame, no vad).
 """
 import numpy as np
@@ -22,9 +23,9 @@ def speech_bins(fft_size):
     return tuple(int(np.floor(np.float32(f) / step + np.float32(0.5))) for f in (100.0, 1500.0))
 
 
-def oracle_windows(oracle_mod, om, x, fft_size, use_denoiser, chunk):
+def oracle_windows(oracle_mod, om, x, fft_size, use_denoiser, chunk, main_cfg=None):
     Ch, n = x.shape
-    p = oracle_mod.Pipeline(Ch, om, fft_size=fft_size, use_denoiser=use_denoiser,
+    p = oracle_mod.Pipeline(Ch, om, fft_size=fft_size, use_denoiser=use_denoiser, main_cfg=main_cfg,
                             trace_frames=n // 480 + 1, trace_windows=n // fft_size + 2)
     for k in range(0, n, chunk):
         p.push([x[c, k:k + chunk] for c in range(Ch)])
@@ -98,9 +99,13 @@ def test_fused_mode_size_limits(fvad_mod, models):
     with pytest.raises(fvad_mod.FvadError):
         fvad_mod.Engine(m, 1, 2, use_denoiser=False, mode="fused")
     with pytest.raises(fvad_mod.FvadError):
-        fvad_mod.Engine(m, 1, 2, fft_size=256)  # < 480: more than one window per tick
+        fvad_mod.Engine(m, 1, 2, fft_size=256, mode="fused")  # < 480: the staged engine's window slots
     with pytest.raises(fvad_mod.FvadError):
         fvad_mod.Engine(m, 1, 2, fft_size=1001)  # odd (FFT.zig:29-31)
+    with pytest.raises(fvad_mod.FvadError):
+        fvad_mod.Engine(m, 1, 2, fft_size=0, bands=((0, 0),))
+    with pytest.raises(fvad_mod.FvadError):
+        fvad_mod.Engine(m, 1, 2, fft_size=1 << 23)  # beyond kMaxFftSize (32-bit window indices)
 
 
 def test_without_denoiser_partial_ticks_engine(fvad_mod, oracle_mod, models):
@@ -186,3 +191,153 @@ def test_partial_tick_needs_no_denoiser(fvad_mod, models):
     with pytest.raises(fvad_mod.FvadError):
         eng.push(np.zeros((2, 1, 2, 480), np.float32), last_tick_samples=[100])
     eng.push(np.zeros((2, 1, 2, 480), np.float32), last_tick_samples=[480])  # full ticks: fine
+
+
+def windows_per_tick(fft_size):
+    return 1 if fft_size >= 480 else (fft_size - 1 + 480) // fft_size
+
+
+# stream lengths (s) per size.  fft_size 2 completes 24 000 windows per
+# second, and every window re-sums the whole long-term average
+# (RollingAverage.zig:45-56: the default initial value makes all 180 s of
+# entries count from the start, 4.3 M at fft_size 2), so that case is short and
+# its machine averages 0.2 s
+SMALL_SECS = {2: (0.6, 0.37), 64: (12.0, 7.3), 256: (20.0, 13.3), 478: (20.0, 13.3)}
+
+
+def machine_cfgs(fvad_mod, oracle_mod, fft_size):
+    cf, co = fvad_mod.VadmConfig.default(), oracle_mod.VadmConfig.default()
+    if fft_size == 2:
+        cf.long_term_speech_avg_sec = co.long_term_speech_avg_sec = 0.2
+    return cf, co
+
+
+@pytest.mark.parametrize("fft_size", [2, 64, 256, 478])
+def test_engine_small_fft_sizes(fvad_mod, oracle_mod, models, fft_size):
+    """fft_size < 480 (VAD.zig:307-347): a 480-sample denoiser frame is split
+    over several FFT-buffer writes, each piece adding ratio * written /
+    fft_size; every full buffer is a window whose vad is the frame's.  The
+    engine reports them in windows_per_tick slots per tick; per-frame vad /
+    ratio, every window's band sums, ratio and vad, and the device
+    VADMachine's segments equal the oracle's."""
+    m, om = models
+    streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip((0, 19), SMALL_SECS[fft_size])]
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=50, fft_size=fft_size, bands=(speech_bins(fft_size),))
+    assert eng.wpt == windows_per_tick(fft_size)
+    cf, co = machine_cfgs(fvad_mod, oracle_mod, fft_size)
+    eng.attach_vadm([cf])
+    got = engine_windows(fvad_mod, eng, streams, 50)
+    for s, x in enumerate(streams):
+        fr, wi, segs = oracle_windows(oracle_mod, om, x, fft_size, True, 48000, co)
+        g = got[s]
+        assert np.array_equal(fr["vad"], g["vad"]) and np.array_equal(fr["ratio"], g["ratio"])
+        assert len(wi) == int(g["win_flag"].sum()) == (x.shape[1] // 480 * 480) // fft_size
+        assert g["win_flag"].max() <= eng.wpt
+        assert np.array_equal(wi["band"][:, :2], g["band"][:, :, 0])
+        assert np.array_equal(wi["ratio"], g["win_ratio"]) and np.array_equal(wi["vad"], g["win_vad"])
+        assert eng.segments(s) == segs
+
+
+def run_partial_ticks(fvad_mod, eng, streams, chunk):
+    """Push streams of any length (the last tick partial: last_tick_samples,
+    use_denoiser = 0) in chunk-tick pushes; per stream the completed windows'
+    band sums [n][C] and ratios, in order."""
+    B, Ch = len(streams), streams[0].shape[0]
+    lens = [x.shape[1] for x in streams]
+    T = max((n + 479) // 480 for n in lens)
+    bands = [[] for _ in streams]
+    ratios = [[] for _ in streams]
+    for t0 in range(0, T, chunk):
+        nt = min(chunk, T - t0)
+        pcm = np.zeros((nt, B, Ch, 480), np.float32)
+        valid = np.zeros(B, np.int32)
+        last = np.full(B, 480, np.int32)
+        for s, x in enumerate(streams):
+            a, b = t0 * 480, min(x.shape[1], (t0 + nt) * 480)
+            if b <= a:
+                continue
+            k = b - a
+            valid[s] = (k + 479) // 480
+            last[s] = k - (valid[s] - 1) * 480
+            seg = np.zeros((Ch, valid[s] * 480), np.float32)
+            seg[:, :k] = x[:, a:b]
+            pcm[:valid[s], s] = seg.reshape(Ch, valid[s], 480).transpose(1, 0, 2)
+        o = eng.push(pcm, ticks_valid=valid, last_tick_samples=last)
+        for s in range(B):
+            cnt = o["win_flag"][:valid[s], s]
+            bands[s].append(pu.tick_windows(o["band"][:valid[s], s], cnt, eng.wpt)[:, :, 0])
+            ratios[s].append(pu.tick_windows(o["win_ratio"][:valid[s], s], cnt, eng.wpt))
+    return [np.concatenate(b) for b in bands], [np.concatenate(r) for r in ratios]
+
+
+@pytest.mark.parametrize("fft_size", [2, 64, 256, 478])
+def test_engine_small_fft_without_denoiser(fvad_mod, oracle_mod, models, fft_size):
+    """use_denoiser = false with fft_size < 480: the pipeline reads fft_size
+    frames (VAD.zig:206-220), so one 480-sample tick holds several windows;
+    stream ends mid-tick (last_tick_samples).  Band sums and window ratios of
+    every window equal the oracle's; the device VADMachine's segments too."""
+    m, om = models
+    secs = SMALL_SECS[fft_size]
+    lens = [int(48000 * secs[0]) + 7, int(48000 * secs[1]) + 333]
+    streams = [fvad_mod.synth_stream(i, n, 2)[0] for i, n in zip((3, 19), lens)]
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=40, fft_size=fft_size, bands=(speech_bins(fft_size),),
+                          use_denoiser=False)
+    cf, co = machine_cfgs(fvad_mod, oracle_mod, fft_size)
+    eng.attach_vadm([cf])
+    band, ratio = run_partial_ticks(fvad_mod, eng, streams, 40)
+    for s, x in enumerate(streams):
+        _, wi, segs = oracle_windows(oracle_mod, om, x, fft_size, False, 48000, co)
+        assert len(wi) == len(band[s]) == x.shape[1] // fft_size
+        assert np.array_equal(wi["band"][:, :2], band[s])
+        assert np.array_equal(wi["ratio"], ratio[s])
+        assert eng.segments(s) == segs
+
+
+@pytest.mark.parametrize("fft_size,use_denoiser", [(20480, True), (22528, True), (22528, False)])
+def test_engine_large_fft_sizes(fvad_mod, oracle_mod, models, fft_size, use_denoiser):
+    """fft_size > 16384: FFT B's tables outside the plan and the transform in
+    device scratch (20480 = 2 * 4^5 * 2 * 5; 22528 = 2 * 4^5 * 11, a generic
+    radix).  Band sums, ratios, vad and the device VADMachine's segments equal
+    the oracle's.  (Up to 24000: above it VADMachine.init's channel-ratio
+    average has length 0, VADMachine.zig:73,89-93.)"""
+    m, om = models
+    streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip((0, 19), (16.0, 11.3))]
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=50, fft_size=fft_size, bands=(speech_bins(fft_size),),
+                          use_denoiser=use_denoiser)
+    eng.attach_vadm()
+    got = engine_windows(fvad_mod, eng, streams, 50)
+    for s, x in enumerate(streams):
+        fr, wi, segs = oracle_windows(oracle_mod, om, x, fft_size, use_denoiser, 48000)
+        g = got[s]
+        if use_denoiser:
+            assert np.array_equal(fr["vad"], g["vad"]) and np.array_equal(fr["ratio"], g["ratio"])
+        assert len(wi) == int(g["win_flag"].sum()) > 0
+        assert np.array_equal(wi["band"][:, :2], g["band"][:, :, 0])
+        assert np.array_equal(wi["ratio"], g["win_ratio"])
+        if use_denoiser:
+            assert np.array_equal(wi["vad"], g["win_vad"])
+        assert eng.segments(s) == segs
+
+
+def test_engine_fft_65536(fvad_mod, oracle_mod, models):
+    """fft_size 65536 (4^7 * 2 complex points, 512 KB of scratch per
+    transform), with a VADMachine whose channel-ratio average spans 2 s: the
+    reference's default 0.5 s gives that average length 0 above fft_size 24000
+    (VADMachine.zig:73,89-93).  Window outputs and segments equal the
+    oracle's."""
+    m, om = models
+    x = fvad_mod.synth_stream(4, 48000 * 9, 2)[0]
+    fft = 65536
+    cfg_f, cfg_o = fvad_mod.VadmConfig.default(), oracle_mod.VadmConfig.default()
+    cfg_f.channel_vol_ratio_avg_sec = cfg_o.channel_vol_ratio_avg_sec = 2.0
+    eng = fvad_mod.Engine(m, 1, 2, max_ticks=64, fft_size=fft, bands=(speech_bins(fft), (0, 4000)))
+    eng.attach_vadm([cfg_f])
+    got = engine_windows(fvad_mod, eng, [x], 64)[0]
+    p = oracle_mod.Pipeline(2, om, fft_size=fft, main_cfg=cfg_o, trace_frames=901, trace_windows=8)
+    p.push([x[0], x[1]])
+    fr, wi = p.trace()
+    assert np.array_equal(fr["vad"], got["vad"])
+    assert len(wi) == int(got["win_flag"].sum()) == 6
+    assert np.array_equal(wi["band"][:, :2], got["band"][:, :, 0])
+    assert np.array_equal(wi["ratio"], got["win_ratio"]) and np.array_equal(wi["vad"], got["win_vad"])
+    assert eng.segments(0) == p.segments()

@@ -112,7 +112,8 @@ def test_simulator_bad_plan(tmp_path):
 
 
 @pytest.mark.parametrize("fft_size,use_denoiser,preload", [(1000, True, False), (2048, False, True),
-                                                           (3000, False, False)])
+                                                           (3000, False, False), (256, True, False),
+                                                           (256, False, True)])
 def test_simulator_vad_config(fvad_mod, oracle_mod, tmp_path, fft_size, use_denoiser, preload):
     """plan.json with a non-default VAD.Config (VAD.zig:17-23): fft_size,
     use_denoiser, alternative machines; instances of different channel counts
