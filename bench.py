@@ -62,8 +62,10 @@ def parse():
                     help="staged (bit-exact, default), fused (bit-exact), fp16 (configs[4]: GRU on MFMA, tolerance)")
     ap.add_argument("--no-vadm", action="store_true", help="staged: do not run the device VADMachine (k_vadm)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on this host (rank 0)")
-    ap.add_argument("--cpu-streams", type=int, default=64)
-    ap.add_argument("--cpu-ticks", type=int, default=100)
+    ap.add_argument("--cpu-streams", type=int, default=48,
+                    help="CPU sample: streams 0..N-1 of this rank's partition (every 20th has digital silence)")
+    ap.add_argument("--cpu-ticks", type=int, default=0,
+                    help="CPU sample: ticks per stream (0: the whole resident cycle the GPU times)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="measure each CPU sample (single-core, all-core) for about this long")
     ap.add_argument("--pmc-json", default=None,
@@ -164,9 +166,10 @@ def cpu_baseline(args, base=0):
     group of streams (simulator.zig:217-228 runs one per instance).  Timed
     single-core and on every CPU this process may use, capped at 16: the GPU
     box allots 16 of its host's hardware threads to one GPU and asks worker
-    pools to stay within that share.  Bounded sample: the first CPU_TICKS
-    ticks of the same synthetic streams as the GPU run's resident input, pushed
-    in 50-tick chunks like the GPU step, repeated for about --cpu-seconds each.
+    pools to stay within that share.  Bounded sample: the whole resident cycle
+    the GPU times (10 s: burst onsets, speech, the every-20th-stream digital
+    silence at t = 5 s) of the partition's first CPU_STREAMS streams, pushed in
+    50-tick chunks like the GPU step, repeated for about --cpu-seconds each.
     A whole-host figure (per-thread rate x the host's hardware threads) is
     reported as an extrapolation, never as `value`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -179,13 +182,12 @@ def cpu_baseline(args, base=0):
     except AttributeError:
         avail = os.cpu_count() or 1
     threads = max(1, min(16, avail))
-    S, T, Ch = args.cpu_streams, args.cpu_ticks, args.channels
-    n = T * 480
     total = args.resident_pushes * args.ticks
-    stride = max(1, args.streams_per_gpu // S)
+    S, T, Ch = min(args.cpu_streams, args.streams_per_gpu), args.cpu_ticks or total, args.channels
+    n = T * 480
     pcm = np.zeros((S, Ch, n), np.float32)
     for s in range(S):
-        x, _ = fvad.synth_stream(base + s * stride, total * 480, Ch)  # the resident input's generator length
+        x, _ = fvad.synth_stream(base + s, total * 480, Ch)  # the resident input's generator length
         pcm[s] = x[:, :n]
 
     def timed(nthr, streams):
@@ -206,10 +208,11 @@ def cpu_baseline(args, base=0):
             "sample": "oracle whole path (rnnoise, FFT B band sums, VADMachine), -O3 -march=native "
                       "-ffp-contract=off on %s; %d threads = this GPU's CPU allotment on a host of %d hardware "
                       "threads (%d usable by this process; whole_host_extrapolated = per-thread rate x %d, not "
-                      "measured); sample: the first %d ticks (%.1f s) of %d of the %d streams (every %dth) x %d ch, "
+                      "measured); sample: %d ticks (%.1f s%s) of streams %d..%d of the %d x %d ch, "
                       "%d passes in %.1f s; single-core: %d streams, %d passes, %.1f s" % (
-                          cpu_model, threads, hw, avail, hw, T, T * 0.01, S, args.streams_per_gpu, stride, Ch,
-                          all_r, all_s, max(1, S // 16), one_r, one_s)}
+                          cpu_model, threads, hw, avail, hw, T, T * 0.01,
+                          ", the GPU's whole resident cycle" if T == total else "", base, base + S - 1,
+                          args.streams_per_gpu, Ch, all_r, all_s, max(1, S // 16), one_r, one_s)}
 
 
 class StubEngine:
@@ -385,7 +388,8 @@ def main():
             "ms_per_step": round(1000.0 * el16 / args.steps, 3),
             "dtype": "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
             "k_gru16_ms": round(kt16["kernels"].get("k_gru16", 0.0), 4),
-            "parity": "tolerance (SURVEY.md 8(c): vad |d| <= 2e-2, segments identical; tests/test_gpu_fp16.py)",
+            "parity": "tolerance (SURVEY.md 8(c): vad |d| <= 2e-2, segments identical or reported -- 1238 of "
+                      "1239 segment lists identical on this workload; tests/test_gpu_fp16.py, test_gpu_fullsize.py)",
             "note": "BASELINE configs[4]'s fp16-GRU variant on the same workload and clock (bench.py --mode fp16 "
                     "gives its full line)"}}
     fvad.synth_cache_clear()

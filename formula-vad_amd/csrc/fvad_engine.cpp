@@ -352,6 +352,7 @@ extern "C" int fvad_engine_reset(fvad_engine *e) {
     if (rc) return rc;
   }
   HIP_TRY(hipMemsetAsync(e->d_state, 0, sizeof(float) * fvad::st::kWords * (size_t)e->cfg.n_streams, e->stream));
+  e->res_next = 0;  // fresh streams start at the resident cycle's first push (t = 0)
   if (e->d_work) HIP_TRY(hipMemsetAsync(e->d_work, 0, sizeof(unsigned) * fvad::kWorkCounters, e->stream));
   HIP_TRY(hipMemsetAsync(e->d_ring, 0,
                          sizeof(float) * (size_t)e->ring_len * e->cfg.n_channels * e->cfg.n_streams, e->stream));
@@ -912,9 +913,11 @@ int ensure_slots16(fvad_engine *e) {
   if (e->d_pcm16) return FVAD_OK;
   const fvad_engine_config &c = e->cfg;
   const size_t n = (size_t)c.max_ticks * c.n_streams * c.n_channels * fvad::kFrame;
-  for (auto &sl : e->slots)
-    if (hipHostMalloc(reinterpret_cast<void **>(&sl.in16), n * sizeof(int16_t), 0) != hipSuccess)
+  for (auto &sl : e->slots)  // a slot allocated by an earlier, partly failed call is kept
+    if (!sl.in16 && hipHostMalloc(reinterpret_cast<void **>(&sl.in16), n * sizeof(int16_t), 0) != hipSuccess) {
+      sl.in16 = nullptr;
       return fail(FVAD_ENOMEM, "hipHostMalloc failed (16-bit input slots)");
+    }
   if (hipMalloc(reinterpret_cast<void **>(&e->d_pcm16), n * sizeof(int16_t)) != hipSuccess)
     return fail(FVAD_ENOMEM, "hipMalloc failed (16-bit input staging)");
   return FVAD_OK;
@@ -1137,31 +1140,35 @@ extern "C" int fvad_engine_load_synthetic_ex(fvad_engine *e, int n_ticks, int n_
   if (!e) return fail(FVAD_EINVAL, "null engine");
   const fvad_engine_config &c = e->cfg;
   if (n_ticks < 1 || n_ticks > c.max_ticks) return fail(FVAD_EINVAL, "n_ticks out of range");
-  if (n_pushes < 1) return fail(FVAD_EINVAL, "n_pushes must be >= 1");
+  if (n_pushes < 1 || (long long)n_ticks * n_pushes > (1LL << 30))
+    return fail(FVAD_EINVAL, "1 <= n_pushes and n_ticks * n_pushes <= 2^30 required");
   HIP_TRY(hipSetDevice(c.device));
   const size_t per_push = (size_t)n_ticks * c.n_streams * c.n_channels * fvad::kFrame;
+  const int total = n_ticks * n_pushes;
+  // one push at a time through a staging buffer (the generator keeps its own
+  // cache of the whole block for the next engine of the same workload)
   std::vector<float> host;
   try {
-    host.resize(per_push * n_pushes);
+    host.resize(per_push);
   } catch (...) {
     return fail(FVAD_ENOMEM, "host buffer for the synthetic input");
   }
-  int rc = fvad_synth_ticks(base, c.n_streams, c.n_channels, n_ticks * n_pushes, 0, n_ticks * n_pushes, host.data());
-  if (rc) return fail(rc, "fvad_synth_ticks failed");
   // buffer 0 (or the resident set) may still be read by an in-flight push
-  if ((rc = fvad_engine_sync(e))) return rc;
+  int rc = fvad_engine_sync(e);
+  if (rc) return rc;
   if (e->d_res) {
     HIP_TRY(hipFree(e->d_res));
     e->d_res = nullptr;
   }
   e->res_pushes = 0;
-  if (n_pushes == 1) {
-    HIP_TRY(hipMemcpy(e->d_pcm_b[0], host.data(), per_push * sizeof(float), hipMemcpyHostToDevice));
-  } else {
-    if ((rc = dalloc(&e->d_res, per_push * n_pushes))) return rc;
-    HIP_TRY(hipMemcpy(e->d_res, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
-    e->res_pushes = n_pushes;
+  if (n_pushes > 1 && (rc = dalloc(&e->d_res, per_push * n_pushes))) return rc;
+  for (int k = 0; k < n_pushes; k++) {
+    if ((rc = fvad_synth_ticks(base, c.n_streams, c.n_channels, total, k * n_ticks, n_ticks, host.data())))
+      return fail(rc, "fvad_synth_ticks failed");
+    float *dst = n_pushes == 1 ? e->d_pcm_b[0] : e->d_res + per_push * (size_t)k;
+    HIP_TRY(hipMemcpy(dst, host.data(), per_push * sizeof(float), hipMemcpyHostToDevice));
   }
+  if (n_pushes > 1) e->res_pushes = n_pushes;
   e->res_next = 0;
   e->resident_ticks = n_ticks;
   return FVAD_OK;

@@ -104,6 +104,9 @@ def check_exact(ref, got, segs):
     return n_seg
 
 
+MAX_MOVED = 3
+
+
 def check_tolerance(ref, got, segs):
     worst_v, worst_b, n_seg, diffs = 0.0, 0.0, 0, []
     for s, (fr, wi, rsegs) in enumerate(ref):
@@ -128,8 +131,9 @@ def check_tolerance(ref, got, segs):
             diffs.append((s, shift))
         worst_v, worst_b = max(worst_v, dv), max(worst_b, db)
         n_seg += len(rsegs)
-    # at most 1 % of the streams may differ, each by a few windows
-    assert len(diffs) <= max(1, len(ref) // 100), diffs
+    # the observed count plus a margin: 1 of the bench workload's 2048 streams
+    # (one segment end one FFT-B window early), none of the 512-stream shard's
+    assert len(diffs) <= MAX_MOVED, diffs
     return worst_v, worst_b, n_seg, diffs
 
 
