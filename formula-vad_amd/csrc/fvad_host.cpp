@@ -251,7 +251,7 @@ extern "C" size_t fvad_vadm_segments(const fvad_vadm *v, fvad_segment *out, size
 
 namespace {
 struct StreamMachines {
-  std::vector<VADMachine> machines;  // [0] = main; they run on the device (k_vadm_hbm)
+  std::vector<VADMachine> machines;  // [0] = main; they run on the device (k_vadmw)
 };
 }  // namespace
 
@@ -325,7 +325,7 @@ extern "C" int fvad_pipeline_create_ex(int sample_rate, int n_channels, const fv
   int rc = assign_bands(p->sm.machines, p->ec);
   if (!rc) rc = fvad_engine_create(&p->ec, model, &p->engine);
   if (!rc) {
-    // the machines run on the device after every push (k_vadm_hbm)
+    // the machines run on the device after every push (k_vadmw)
     std::vector<fvad_vadm_config> cfgs;
     for (auto &m : p->sm.machines) cfgs.push_back(m.cfg);
     rc = fvad_engine_attach_vadm(p->engine, cfgs.data(), (int)cfgs.size(), kPipelineSegCap);
@@ -455,7 +455,7 @@ extern "C" size_t fvad_pipeline_segments(const fvad_pipeline *p, int alt, fvad_s
 // device) part, lock-step pushes, no collectives.  Input is pulled from a
 // reader per push (the simulator's 48 000-frame read loop,
 // SimulationInstance.zig:171-203) straight into the engine's pinned slot,
-// with two pushes in flight.
+// with FVAD_MAX_IN_FLIGHT pushes in flight.
 // ---------------------------------------------------------------------------
 struct fvad_multi {
   int n_streams, ticks_per_push, n_machines;
@@ -598,7 +598,7 @@ extern "C" int fvad_multi_run_stream(fvad_multi *m, fvad_read_fn read, void *ctx
             }
         }
         if (nt == 0) break;
-        if (in_flight == 2 && !(rc = fvad_engine_collect(p.engine, nullptr, nullptr))) in_flight--;
+        if (in_flight == FVAD_MAX_IN_FLIGHT && !(rc = fvad_engine_collect(p.engine, nullptr, nullptr))) in_flight--;
         if (!rc && !(rc = fvad_engine_submit_ex(p.engine, buf, nt, valid.data(), partial ? last.data() : nullptr)))
           in_flight++;
       }

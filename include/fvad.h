@@ -173,14 +173,18 @@ int fvad_engine_push_ex(fvad_engine *e, const float *pcm, int n_ticks, const int
                         const int32_t *last_tick_samples, fvad_outputs *out);
 
 /* Streaming ingest (the simulator's read loop, SimulationInstance.zig:194-203,
- * reads the next chunk while the pipeline works on the last one).  Two pushes
- * may be in flight: submit copies the input into a pinned slot (or takes it in
- * place when pcm is the pointer fvad_engine_input_slot returned), queues the
- * H2D copy on its own stream -- overlapping the previous push's kernels -- then
- * the kernels and the output copies into pinned memory, and returns without
- * waiting.  collect returns the outputs of the oldest submitted push (blocking
- * until they are on the host; out may be NULL, *n_ticks its tick count).
- * submit fails with FVAD_EINVAL while two pushes are uncollected. */
+ * reads the next chunk while the pipeline works on the last one).  Up to
+ * FVAD_MAX_IN_FLIGHT pushes may be in flight: submit copies the input into a
+ * pinned slot (or takes it in place when pcm is the pointer
+ * fvad_engine_input_slot returned), queues the H2D copy on its own stream --
+ * overlapping the earlier pushes' kernels; it waits only until the device
+ * input buffer it fills has been read by the k_prep3 of the push two before --
+ * then the kernels and the output copies into pinned memory, and returns
+ * without waiting.  collect returns the outputs of the oldest submitted push
+ * (blocking until they are on the host; out may be NULL, *n_ticks its tick
+ * count).  submit fails with FVAD_EINVAL while FVAD_MAX_IN_FLIGHT pushes are
+ * uncollected. */
+#define FVAD_MAX_IN_FLIGHT 3
 /* the pinned [max_ticks][streams][channels][480] slot the next submit reads;
  * blocks until that slot's previous copy to the device finished; NULL on error */
 float *fvad_engine_input_slot(fvad_engine *e);

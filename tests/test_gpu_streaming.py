@@ -2,8 +2,8 @@
 configuration at full size, against the CPU oracle.
 
 The simulator reads the next chunk while the pipeline processes the last one
-(SimulationInstance.zig:194-203); here two pushes are in flight, the H2D copy
-of push k+1 overlapping push k's kernels.  Outputs must be bit-identical to
+(SimulationInstance.zig:194-203); here up to three pushes are in flight, the
+H2D copy of push k+2 overlapping push k+1's kernels.  Outputs must be bit-identical to
 the synchronous push and to the oracle.
 """
 import concurrent.futures as cf
@@ -41,10 +41,11 @@ def _chunks(streams, nt_push):
     return out
 
 
-@pytest.mark.parametrize("mode", ["staged", "fused"])
-def test_submit_collect_equals_push(fvad_mod, models, mode):
-    """Two pushes in flight, alternating caller buffers and the zero-copy input
-    slot, ragged ticks: every output equals the synchronous push's."""
+@pytest.mark.parametrize("mode,depth", [("staged", 2), ("fused", 2), ("staged", 3), ("fp16", 3)])
+def test_submit_collect_equals_push(fvad_mod, models, mode, depth):
+    """depth (2 or FVAD_MAX_IN_FLIGHT = 3) pushes in flight, alternating caller
+    buffers and the zero-copy input slot, ragged ticks: every output equals
+    the synchronous push's."""
     m, _ = models
     secs = [6.0, 4.31, 5.5, 1.2, 6.0]
     streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip((3, 19, 39, 8, 77), secs)]
@@ -54,7 +55,7 @@ def test_submit_collect_equals_push(fvad_mod, models, mode):
     eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=40, want_denoised=True, mode=mode)
     got, in_flight = [], 0
     for k, (p, v) in enumerate(pushes):
-        if in_flight == 2:
+        if in_flight == depth:
             got.append(eng.collect(denoised=True))
             in_flight -= 1
         if k % 2:
@@ -75,11 +76,11 @@ def test_submit_collect_equals_push(fvad_mod, models, mode):
         assert np.array_equal(a["band"][wf], b["band"][wf])
 
 
-@pytest.mark.parametrize("mode", ["staged", "fused", "fp16"])
-def test_submit_i16_equals_float_push(fvad_mod, models, mode):
+@pytest.mark.parametrize("mode,depth", [("staged", 3), ("fused", 2), ("fp16", 3)])
+def test_submit_i16_equals_float_push(fvad_mod, models, mode, depth):
     """16-bit ingest (fvad_engine_submit_i16, k_pcm16): samples k give the
     outputs of a float push of k / 32768.0f (libsndfile's short -> float),
-    bit for bit -- through the zero-copy 16-bit slot and caller buffers, two
+    bit for bit -- through the zero-copy 16-bit slot and caller buffers, depth
     pushes in flight, ragged ticks, full-scale and clipped samples."""
     m, _ = models
     secs = [5.0, 3.37, 4.2, 0.9]
@@ -95,7 +96,7 @@ def test_submit_i16_equals_float_push(fvad_mod, models, mode):
     got, in_flight = [], 0
     for k, (p, v) in enumerate(q_pushes):
         p16 = p.astype(np.int16)
-        if in_flight == 2:
+        if in_flight == depth:
             got.append(eng.collect(denoised=True))
             in_flight -= 1
         if k % 2:
@@ -154,14 +155,14 @@ def test_submit_limits(fvad_mod, models):
     with pytest.raises(fvad_mod.FvadError):
         eng.collect()  # nothing submitted
     z = np.zeros((8, 2, 2, FRAME), np.float32)
-    eng.submit(z)
-    eng.submit(z)
+    for _ in range(3):
+        eng.submit(z)
     with pytest.raises(fvad_mod.FvadError):
-        eng.submit(z)  # two uncollected pushes in flight
+        eng.submit(z)  # FVAD_MAX_IN_FLIGHT = 3 uncollected pushes in flight
     eng.collect(want=False)
     eng.submit(z)
-    eng.collect(want=False)
-    eng.collect(want=False)
+    for _ in range(3):
+        eng.collect(want=False)
 
 
 def _oracle_trace(args):
