@@ -73,7 +73,7 @@ struct fvad_engine {
   float *d_gru16_bias = nullptr;
   // device VADMachines (fvad_engine_attach_vadm)
   fvad::VadmArgs vadm{};
-  // k_vadmw runs on a side stream over copies of one push's window outputs,
+  // k_vadm_hbm runs on a side stream over copies of one push's window outputs,
   // overlapped with the next push (it only depends on its own state)
   hipStream_t side = nullptr;
   // staged mode: k_prep3 runs on pstream, so push k's prep overlaps push k-1's
@@ -90,7 +90,7 @@ struct fvad_engine {
   int last_event = 0;         // the one recorded last (the launch's end)
   hipEvent_t ev_copy = nullptr, ev_vadm = nullptr, ev_vt[2][2] = {};  // [slot][begin/end] timing pairs
   // window outputs of push k in set k & 1 (the second set exists with VADMachines):
-  // k_vadmw of push k reads them in place, push k + 2 rewrites them after it
+  // k_vadm_hbm of push k reads them in place, push k + 2 rewrites them after it
   int *wflag_b[2] = {};
   float *wratio_b[2] = {}, *wvad_b[2] = {}, *band_b[2] = {};
   hipEvent_t ev_vadm_b[2] = {};
@@ -685,7 +685,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     HIP_TRY(fvad::launch_prep(a, e->pstream, timed ? e->ev : nullptr));
     HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
     HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
-    // window output set b is free once push k-2's k_vadmw has read it
+    // window output set b is free once push k-2's k_vadm_hbm has read it
     if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
     HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr));
   } else {
@@ -700,7 +700,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     const fvad_engine_config &c = e->cfg;
     const size_t TB = (size_t)n_ticks * c.n_streams;
     (void)TB;
-    // the ticks copy may be overwritten only once the previous k_vadmw has read it
+    // the ticks copy may be overwritten only once the previous k_vadm_hbm has read it
     if (use_ticks) {
       HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm, 0));
       HIP_TRY(hipMemcpyAsync(e->d_vticks, e->d_ticks, (size_t)c.n_streams * 4, hipMemcpyDeviceToDevice, e->stream));
@@ -709,7 +709,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     HIP_TRY(hipStreamWaitEvent(e->side, e->ev_copy, 0));
     fvad::StagedArgs v = a;
     v.ticks_valid = use_ticks ? e->d_vticks : nullptr;
-    // k_vadmw timing never blocks the host (it would serialise the overlap):
+    // k_vadm_hbm timing never blocks the host (it would serialise the overlap):
     // two event pairs alternate and are read once complete
     const int slot = e->vadm_slot ^= 1;
     if (timed) {
@@ -724,7 +724,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
     HIP_TRY(hipEventRecord(e->ev_vadm_b[b], e->side));
   }
-  // every reader of buffer b (incl. the copy of ticks for k_vadmw) is queued
+  // every reader of buffer b (incl. the copy of ticks for k_vadm_hbm) is queued
   HIP_TRY(hipEventRecord(e->ev_buf_free[b], e->stream));
   e->buf_busy[b] = true;
   e->next_buf = b ^ 1;
@@ -764,7 +764,7 @@ int collect_timing(fvad_engine *e) {
   return rc;
 }
 
-// k_vadmw samples whose end event has completed (non-blocking)
+// k_vadm_hbm samples whose end event has completed (non-blocking)
 int collect_vadm_timing(fvad_engine *e) {
   for (int k = 0; k < 2; k++) {
     if (!e->vadm_pending[k] || hipEventQuery(e->ev_vt[k][1]) != hipSuccess) continue;
@@ -885,7 +885,7 @@ int ensure_slots(fvad_engine *e) {
   const size_t TB = T * B, TBW = TB * e->wpt, frames = TB * C * fvad::kFrame;
   // the copy stream at the highest priority: its own hardware queue, so the
   // 16-bit ingest's k_pcm16 does not queue behind a long kernel of a stream
-  // sharing its queue (it waited for k_vadmw at the default priority)
+  // sharing its queue (it waited for k_vadm_hbm at the default priority)
   int lo_prio = 0, hi_prio = 0;
   if (!e->cstream && (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
                       hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, hi_prio) != hipSuccess))
@@ -1241,7 +1241,7 @@ extern "C" int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_r
   if (rc) return rc;
   for (int i = 0; i < FVAD_MAX_TIMES; i++)
     ms_avg[i] = (e->n_timed && i <= e->n_kernels) ? e->ms_sum[i] / e->n_timed : 0.0;
-  // k_vadmw (side stream, overlapped with the next push): reported after the
+  // k_vadm_hbm (side stream, overlapped with the next push): reported after the
   // pipeline kernels, not part of [0]
   if (e->vadm.n > 0 && e->n_kernels + 1 < FVAD_MAX_TIMES)
     ms_avg[e->n_kernels + 1] = e->vadm_timed ? e->vadm_ms_sum / e->vadm_timed : 0.0;
@@ -1271,7 +1271,7 @@ extern "C" int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out)
 extern "C" int fvad_engine_windows_per_tick(const fvad_engine *e) { return e ? e->wpt : FVAD_EINVAL; }
 
 extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
-  if (e && i == e->n_kernels && e->vadm.n > 0) return "k_vadmw";
+  if (e && i == e->n_kernels && e->vadm.n > 0) return "k_vadm_hbm";
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
   if (e->cfg.mode == FVAD_MODE_FUSED) return i == 0 ? "k_prep" : "k_frame";
   if (e->cfg.mode == FVAD_MODE_FP16 && i == 6) return "k_gru16";

@@ -251,7 +251,7 @@ extern "C" size_t fvad_vadm_segments(const fvad_vadm *v, fvad_segment *out, size
 
 namespace {
 struct StreamMachines {
-  std::vector<VADMachine> machines;  // [0] = main; they run on the device (k_vadmw)
+  std::vector<VADMachine> machines;  // [0] = main; they run on the device (k_vadm_hbm)
 };
 }  // namespace
 
@@ -325,7 +325,7 @@ extern "C" int fvad_pipeline_create_ex(int sample_rate, int n_channels, const fv
   int rc = assign_bands(p->sm.machines, p->ec);
   if (!rc) rc = fvad_engine_create(&p->ec, model, &p->engine);
   if (!rc) {
-    // the machines run on the device after every push (k_vadmw)
+    // the machines run on the device after every push (k_vadm_hbm)
     std::vector<fvad_vadm_config> cfgs;
     for (auto &m : p->sm.machines) cfgs.push_back(m.cfg);
     rc = fvad_engine_attach_vadm(p->engine, cfgs.data(), (int)cfgs.size(), kPipelineSegCap);

@@ -25,7 +25,7 @@
 //   k_winmeta lane/stream   window completion, share-weighted ratio, state
 //   k_fftbw   wave/window   FFT B (kissfft radix-4), magnitudes, band sums
 //                           (k_fftb, workgroup per window, for fft_size 512)
-//   k_vadmw    wave/stream  VADMachine.run per completed window (side stream)
+//   k_vadm_hbm lane/stream  VADMachine.run per completed window (side stream)
 //
 // The wave kernels are persistent (batches of frames from per-XCD queues) so
 // per-lane table values stay in registers across frames.  All arithmetic
@@ -1587,102 +1587,77 @@ __global__ void __launch_bounds__(NT) k_fftb(StagedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_vadmw: VADMachine.run (VADMachine.zig:126-230) for every completed FFT-B
-// window of the push: one wave per (machine, stream), windows in order.
+// k_vadm: VADMachine.run (VADMachine.zig:126-230) for every completed FFT-B
+// window of the push, one lane per stream, every attached machine.
 // RollingAverage.avg (RollingAverage.zig:34-56) recomputes the mean over the
-// whole buffer in array order on every push, in f64 -- reproduced as is (an
-// incremental mean would round differently), so each average is one serial
-// f64 add chain.  The wave runs the machine uniformly (every lane holds the
-// same state); the 64 lanes load a block of 64 consecutive entries (the
-// buffers are stream-major, [stream][i]: one coalesced 256-byte read), form
-// their products entry * (1 / count), and the chain then adds the block's
-// products in index order from v_readlane -- the same operations on the same
-// values as the scalar loop.  Blocks are loaded two ahead of the chain.
+// whole buffer in array order on every push, in f64 - reproduced as is (an
+// incremental mean would round differently).  Buffers are stored [i][stream]
+// so the lanes of a wave read one contiguous line per term.
 // ---------------------------------------------------------------------------
-namespace vw {
-// lane j's product of the block, broadcast (uniform) to the chain
-__device__ __forceinline__ double lane_d(double v, int j) {
-  const unsigned long long u = __double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, j);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), j);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-// acc + sum_{i in [i0, i1)} (double)buf[i] * scalar, in index order
-__device__ __noinline__ double chain(double acc, const float *buf, unsigned i0, unsigned i1, double scalar) {
-  const int lane = threadIdx.x & 63;
-  if (i0 >= i1) return acc;
-  constexpr int kAhead = 3;
-  float v[kAhead];
-#pragma unroll
-  for (int k = 0; k < kAhead; k++) {
-    const unsigned i = i0 + 64u * k + lane;
-    v[k] = i < i1 ? buf[i] : 0.0f;
-  }
-  for (unsigned b = i0; b < i1; b += 64u * kAhead) {
-#pragma unroll
-    for (int k = 0; k < kAhead; k++) {
-      const unsigned bk = b + 64u * k;
-      if (bk >= i1) break;
-      const double p = (double)v[k] * scalar;
-      const unsigned inext = bk + 64u * kAhead + lane;  // the block kAhead ahead
-      v[k] = inext < i1 ? buf[inext] : 0.0f;
-      const int n = (int)min(64u, i1 - bk);
-      if (n == 64) {
-#pragma unroll
-        for (int j = 0; j < 64; j++) acc += lane_d(p, j);
-      } else {
-        for (int j = 0; j < n; j++) acc += lane_d(p, j);
-      }
-    }
-  }
-  return acc;
-}
-
-__device__ __forceinline__ double repeat(double acc, double term, unsigned n) {
-  for (unsigned i = 0; i < n; i++) acc += term;
-  return acc;
-}
-
-// [p, q): entries below nw are pushed f32 values, the rest the initial average
-__device__ __forceinline__ double range(double acc, const float *buf, unsigned p, unsigned q, unsigned nw, double init,
-                                        double scalar) {
-  const unsigned mid = min(max(nw, p), q);
-  acc = chain(acc, buf, p, mid, scalar);
-  return repeat(acc, init * scalar, q - mid);
-}
-
-// the entry written this window must be visible to the lanes that load it
-// (written by lane 0; every lane of the wave is in one workgroup, one CU)
-__device__ __forceinline__ void put(float *buf, unsigned i, float sample) {
-  if ((threadIdx.x & 63) == 0) buf[i] = sample;  // stored as f32: (double)f32 is exact
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-}
-
-// Short rolling averages: the plain recompute (RollingAverage.push / avg)
-__device__ __forceinline__ double push_short(float *buf, int n, unsigned &widx, unsigned &count, double &last,
-                                             int &has, float sample) {
-  put(buf, widx, sample);
+// Short rolling averages: the plain recompute.
+__device__ __forceinline__ double ra_push(float *buf, int B, int n, unsigned &widx, unsigned &count, double &last,
+                                          int &has, float sample) {
+  buf[(size_t)widx * B] = sample;  // stored as f32: (double)f32 is exact
   widx = (widx + 1) % (unsigned)n;
   if (count < (unsigned)n) count++;
-  const double acc = chain(0.0, buf, 0, count, 1.0 / (double)count);
+  double acc = 0.0;
+  const double scalar = 1.0 / (double)count;
+  for (unsigned i = 0; i < count; i++) acc += (double)buf[(size_t)i * B] * scalar;
   last = acc;
   has = 1;
   return acc;
 }
 
 // The long-term average (4218 entries by default).  Same operation sequence as
+// the full recompute, two savings that keep it bit-identical:
+//  * once the buffer is full the scalar 1/n no longer changes, so the running
+//    sum over the entries before the write position is exactly what the
+//    previous pass had accumulated there (those entries have not changed) -
+//    the pass starts from that cached prefix;
+//  * entries are read 32 ahead of the f64 add chain (register double buffer),
+//    so the chain does not wait on memory per term.
+// acc += entry[i] * scalar for i in [i0, i1), C order; entries are pushed f32
+// values (read 8 ahead of the add chain) or, for never-written entries, the
+// initial average (a double).
+__device__ __forceinline__ double lt_sum(double acc, const float *buf, size_t bs, unsigned i0, unsigned i1,
+                                         double scalar) {
+  unsigned i = i0;
+  for (; i + 8 <= i1; i += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = buf[(size_t)(i + u) * bs];
+    double p[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) p[u] = (double)v[u] * scalar;
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += p[u];
+  }
+  for (; i < i1; i++) acc += (double)buf[(size_t)i * bs] * scalar;
+  return acc;
+}
+__device__ __forceinline__ double lt_sum_init(double acc, double term, unsigned n) {
+  for (unsigned i = 0; i < n; i++) acc += term;
+  return acc;
+}
+__device__ __forceinline__ double lt_range(double acc, const float *buf, size_t bs, unsigned p, unsigned q,
+                                           unsigned nw, double init, double scalar) {
+  const unsigned mid = min(max(nw, p), q);  // [p, mid) written, [mid, q) initial
+  acc = lt_sum(acc, buf, bs, p, mid, scalar);
+  return lt_sum_init(acc, init * scalar, q - mid);
+}
+
+// The long-term average (4218 entries by default).  Same operation sequence as
 // the full recompute, with one exact saving: once the buffer is full the
 // scalar 1/n no longer changes, so the running sum over the entries before the
 // write position is exactly what the previous pass had accumulated there
-// (those entries have not changed) -- the pass starts from that cached prefix.
+// (those entries have not changed) - the pass starts from that cached prefix.
 // Entries never written since the machine started hold the initial average
 // (a double, RollingAverage.zig init): entry i is a pushed f32 iff i < nw.
-__device__ __forceinline__ double push_long(float *buf, int n, unsigned &widx, unsigned &count, unsigned &nw,
-                                            double init, double &last, int &has, double &pre, int &pre_ok,
-                                            float sample) {
+__device__ __forceinline__ double ra_push_long(float *buf, size_t bs, int n, unsigned &widx, unsigned &count,
+                                               unsigned &nw, double init, double &last, int &has, double &pre,
+                                               int &pre_ok, float sample) {
   const unsigned w = widx;
-  put(buf, w, sample);
+  buf[(size_t)w * bs] = sample;
   widx = (w + 1) % (unsigned)n;
   if (count < (unsigned)n) count++;
   if (nw < (unsigned)n) nw++;
@@ -1692,12 +1667,12 @@ __device__ __forceinline__ double push_long(float *buf, int n, unsigned &widx, u
   const unsigned save_at = widx;  // the next pass starts at the next write position
   double save = 0.0;              // (save_at == 0: it starts from 0.0)
   if (save_at > start && save_at < count) {
-    acc = range(acc, buf, start, save_at, nw, init, scalar);
+    acc = lt_range(acc, buf, bs, start, save_at, nw, init, scalar);
     save = acc;
-    acc = range(acc, buf, save_at, count, nw, init, scalar);
+    acc = lt_range(acc, buf, bs, save_at, count, nw, init, scalar);
   } else {
     if (save_at == start) save = acc;
-    acc = range(acc, buf, start, count, nw, init, scalar);
+    acc = lt_range(acc, buf, bs, start, count, nw, init, scalar);
   }
   pre = save;
   pre_ok = count == (unsigned)n;
@@ -1705,22 +1680,18 @@ __device__ __forceinline__ double push_long(float *buf, int n, unsigned &widx, u
   has = 1;
   return acc;
 }
-}  // namespace vw
 
-// One machine over all completed windows of the push for one stream (one
-// wave, uniform); buffers of stream s: [s][n] at the machine's offsets.
-__device__ void vadm_wave(const StagedArgs &a, int m, int s) {
+// One machine over all completed windows of the push for one stream; `lt`
+// points at entry 0 of the stream's long-term buffer, `lts` is its stride.
+__device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t lts) {
   const int B = a.n_streams, C = a.n_channels, nb = a.n_bands;
   const int nt = ticks_of(a, s);
   const unsigned long long fft = (unsigned long long)a.plan->nfft_b;
   enum { kClosed = 0, kOpening = 1, kOpen = 2, kClosing = 3 };
   const VadmConst &K = a.vadm.c[m];
   VadmState S = a.vadm.st[(size_t)m * B + s];
-  float *lt = a.vadm.buf + K.lt_off + (size_t)s * K.n_lt;
-  float *st = a.vadm.buf + K.st_off + (size_t)s * K.n_st;
-  float *rb = a.vadm.buf + K.r_off + (size_t)s * K.n_r;
+  float *st = a.vadm.buf + K.st_off + s, *rb = a.vadm.buf + K.r_off + s;
   VadmSeg *seg = a.vadm.seg + ((size_t)m * B + s) * a.vadm.seg_cap;
-  const bool lead = (threadIdx.x & 63) == 0;
   // every window of the push in order: ticks, then a tick's slots (several
   // when fft_size < 480)
   for (int t = 0; t < nt; t++)
@@ -1736,8 +1707,8 @@ __device__ void vadm_wave(const StagedArgs &a, int m, int s) {
     }
     // fft_input.vad orelse 0 (VADMachine.zig:240-246): no vad without the denoiser
     const float vad = a.use_denoiser ? a.out_win_vad[o] : 0.0f, vr = a.out_win_ratio[o];
-    const double st_avg = vw::push_short(st, K.n_st, S.st_widx, S.st_count, S.st_last, S.st_has, min_v);
-    const double r_avg = vw::push_short(rb, K.n_r, S.r_widx, S.r_count, S.r_last, S.r_has, vr);
+    const double st_avg = ra_push(st, B, K.n_st, S.st_widx, S.st_count, S.st_last, S.st_has, min_v);
+    const double r_avg = ra_push(rb, B, K.n_r, S.r_widx, S.r_count, S.r_last, S.r_has, vr);
     double base;
     if (S.lt_has)
       base = S.lt_last;
@@ -1748,8 +1719,8 @@ __device__ void vadm_wave(const StagedArgs &a, int m, int s) {
     const double threshold = base * (double)K.thr_factor;
     const bool met = st_avg > threshold && r_avg > (double)K.ratio_thr;
     if (!met)
-      vw::push_long(lt, K.n_lt, S.lt_widx, S.lt_count, S.lt_nw, K.init, S.lt_last, S.lt_has, S.lt_pre, S.lt_pre_ok,
-                    min_v);
+      ra_push_long(lt, lts, K.n_lt, S.lt_widx, S.lt_count, S.lt_nw, K.init, S.lt_last, S.lt_has, S.lt_pre,
+                   S.lt_pre_ok, min_v);
     const int from = S.state;
     bool ended = false;
     switch (from) {
@@ -1784,7 +1755,7 @@ __device__ void vadm_wave(const StagedArgs &a, int m, int s) {
       const unsigned long long len = S.speech_end - S.speech_start;
       const float len_rt = (float)len / K.sr;
       if (len_rt >= K.min_dur) {
-        if (S.n_segs < (unsigned)a.vadm.seg_cap && lead) {
+        if (S.n_segs < (unsigned)a.vadm.seg_cap) {
           VadmSeg g;
           g.sample_from = K.rec_pad > S.speech_start ? 0ull : S.speech_start - K.rec_pad;
           g.sample_to = S.speech_end + K.rec_pad;
@@ -1808,7 +1779,7 @@ __device__ void vadm_wave(const StagedArgs &a, int m, int s) {
       S.vol_ratio_count += 1;
     }
   }
-  if (lead) a.vadm.st[(size_t)m * B + s] = S;
+  a.vadm.st[(size_t)m * B + s] = S;
 }
 
 // ---------------------------------------------------------------------------
@@ -2082,15 +2053,18 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   return hipSuccess;
 }
 
-// k_vadmw: a wave per (machine, stream), 4 per workgroup (vadm_wave); it
-// co-runs with the next push's pipeline on the engine's side stream.
-constexpr int kVadmWaves = 4;
-__global__ void __launch_bounds__(64 * kVadmWaves) k_vadmw(StagedArgs a) {
-  const long long item = (long long)blockIdx.x * kVadmWaves + (threadIdx.x >> 6);
-  if (item >= (long long)a.vadm.n * a.n_streams) return;
-  const int m = (int)(item / a.n_streams), s = (int)(item - (long long)m * a.n_streams);
-  if (ticks_of(a, s) <= 0) return;
-  vadm_wave(a, m, s);
+// k_vadm_hbm: the same machine, long-term buffers walked in HBM, no LDS, 16
+// lanes per workgroup: a light kernel that co-runs with the next push's
+// pipeline on the engine's side stream.
+#ifndef FVAD_VADM_LANES
+#define FVAD_VADM_LANES 64
+#endif
+constexpr int kVadmHbmLanes = FVAD_VADM_LANES;  // streams per workgroup (one wave); 16 / 32 / 64 measured within noise, 64 takes fewest wave slots
+__global__ void __launch_bounds__(64) k_vadm_hbm(StagedArgs a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.n_streams || ticks_of(a, s) <= 0) return;
+  for (int m = 0; m < a.vadm.n; m++)
+    vadm_stream(a, m, s, a.vadm.buf + a.vadm.c[m].lt_off + s, (size_t)a.n_streams);
 }
 
 hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream) {
@@ -2104,8 +2078,7 @@ hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream) {
 
 hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream) {
   (void)hipGetLastError();
-  const long long items = (long long)a.vadm.n * a.n_streams;
-  FVAD_KERNEL_TRY(k_vadmw, dim3((unsigned)((items + kVadmWaves - 1) / kVadmWaves)), dim3(64 * kVadmWaves), 0, stream,
+  FVAD_KERNEL_TRY(k_vadm_hbm, dim3((a.n_streams + kVadmHbmLanes - 1) / kVadmHbmLanes), dim3(kVadmHbmLanes), 0, stream,
                   a);
   return hipSuccess;
 }

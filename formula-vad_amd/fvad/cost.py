@@ -169,7 +169,7 @@ def staged_kernels(n_channels=2, fft_size=2048):
         "k_fftbw": (p["re-block + FFT B share"], 480 * 4 + 4),
         # fft_size 512: the workgroup-per-window kernel, same work
         "k_fftb": (p["re-block + FFT B share"], 480 * 4 + 4),
-        "k_vadmw": (p["VADMachine share"], (4218 + 4 + 11 + 2) * 4 * FRAME / fft_size / C + 16),
+        "k_vadm_hbm": (p["VADMachine share"], (4218 + 4 + 11 + 2) * 4 * FRAME / fft_size / C + 16),
     }
     # k_olafb (fft_size 2048, <= 4 channels): k_ola + k_winmeta + k_fftbw in one
     # kernel; the ys rows in, per-tick outputs out, the re-block window stays

@@ -2,7 +2,7 @@
 """Per-push timeline of the main stream from a rocprofv3 --kernel-trace
 database (tools/profile.sh writes gpurun_out/prof_<tag>/trace/*.db):
 each kernel's start offset, duration and the gap before it, averaged over
-the timed pushes; k_prep3 and k_vadmw (side streams) are shown as
+the timed pushes; k_prep3 and k_vadm_hbm (side streams) are shown as
 overlap windows.
 Usage: python3 tools/timeline.py gpurun_out/prof_<tag>/trace"""
 import glob
@@ -11,7 +11,7 @@ import sqlite3
 import sys
 from collections import defaultdict
 
-SIDE = {"k_prep3", "k_vadmw"}
+SIDE = {"k_prep3", "k_vadm_hbm"}
 
 
 def short(name):
