@@ -1619,18 +1619,32 @@ __device__ __forceinline__ double ra_push(float *buf, int B, int n, unsigned &wi
 // acc += entry[i] * scalar for i in [i0, i1), C order; entries are pushed f32
 // values (read 8 ahead of the add chain) or, for never-written entries, the
 // initial average (a double).
+#ifndef FVAD_LT_BLOCK
+#define FVAD_LT_BLOCK 16
+#endif
 __device__ __forceinline__ double lt_sum(double acc, const float *buf, size_t bs, unsigned i0, unsigned i1,
                                          double scalar) {
+  // blocks of kL entries, the next block's loads issued before this block's
+  // adds (two blocks in flight: the chain waits a memory latency per kL
+  // entries at most, not per block of its own)
+  constexpr int kL = FVAD_LT_BLOCK;
   unsigned i = i0;
-  for (; i + 8 <= i1; i += 8) {
-    float v[8];
+  if (i + kL <= i1) {
+    float cur[kL];
 #pragma unroll
-    for (int u = 0; u < 8; u++) v[u] = buf[(size_t)(i + u) * bs];
-    double p[8];
+    for (int u = 0; u < kL; u++) cur[u] = buf[(size_t)(i + u) * bs];
+    for (; i + 2 * kL <= i1; i += kL) {
+      float nxt[kL];
 #pragma unroll
-    for (int u = 0; u < 8; u++) p[u] = (double)v[u] * scalar;
+      for (int u = 0; u < kL; u++) nxt[u] = buf[(size_t)(i + kL + u) * bs];
 #pragma unroll
-    for (int u = 0; u < 8; u++) acc += p[u];
+      for (int u = 0; u < kL; u++) acc += (double)cur[u] * scalar;
+#pragma unroll
+      for (int u = 0; u < kL; u++) cur[u] = nxt[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kL; u++) acc += (double)cur[u] * scalar;
+    i += kL;
   }
   for (; i < i1; i++) acc += (double)buf[(size_t)i * bs] * scalar;
   return acc;
