@@ -363,6 +363,12 @@ extern "C" int fvad_engine_reset(fvad_engine *e) {
 }
 
 namespace {
+// CUs named by the config's mask (0: no mask)
+int mask_cus(const fvad_engine_config &c) {
+  int n = 0;
+  for (uint32_t w : c.cu_mask) n += __builtin_popcount(w);
+  return n;
+}
 void fill_bands(const fvad_engine_config &c, int *band_lo, int *band_hi, int *lo_all, int *hi_all) {
   int lo = 1 << 30, hi = -1;
   for (int b = 0; b < fvad::kMaxBandCfg; b++) {
@@ -377,6 +383,14 @@ void fill_bands(const fvad_engine_config &c, int *band_lo, int *band_hi, int *lo
   *hi_all = hi;
 }
 
+}  // namespace
+
+namespace {
+// an engine stream: on the config's CUs when it names any
+hipError_t make_stream(const fvad_engine *e, hipStream_t *s) {
+  if (mask_cus(e->cfg)) return hipExtStreamCreateWithCUMask(s, 8, e->cfg.cu_mask);
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
 }  // namespace
 
 extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_model *model, fvad_engine **out) {
@@ -440,10 +454,9 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     return rc;
   };
   if (hipSetDevice(c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipSetDevice failed"));
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
-    return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
+  if (make_stream(e, &e->stream) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
   if (c.mode != FVAD_MODE_FUSED &&
-      (hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess ||
+      (make_stream(e, &e->pstream) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[0], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[1], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_buf_free[0], hipEventDisableTiming) != hipSuccess ||
@@ -516,7 +529,8 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     e->d_xs = e->d_xs_b[0];
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "device query failed"));
-    e->grid_frames = prop.multiProcessorCount;  // CUs; persistent grids are sized per kernel
+    // CUs; persistent grids are sized per kernel
+    e->grid_frames = mask_cus(c) ? std::min(mask_cus(c), prop.multiProcessorCount) : prop.multiProcessorCount;
     // k_fftb's device scratch when a transform does not fit in LDS: a slice per
     // workgroup, at most two per CU and 1 GiB
     int lo = 0, hi = 0, band_lo[fvad::kMaxBandCfg], band_hi[fvad::kMaxBandCfg];
@@ -1367,7 +1381,7 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
   if ((rc = dalloc(&e->d_vflag, TB)) || (rc = dalloc(&e->d_vwratio, TBW)) || (rc = dalloc(&e->d_vwvad, TBW)) ||
       (rc = dalloc(&e->d_vband, TBW * e->cfg.n_channels * e->cfg.n_bands)) || (rc = dalloc(&e->d_vticks, (size_t)B)))
     return rc;
-  if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
+  if (make_stream(e, &e->side) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_vadm, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&e->ev_vt[0][0]) != hipSuccess || hipEventCreate(&e->ev_vt[0][1]) != hipSuccess ||

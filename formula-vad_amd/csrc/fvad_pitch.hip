@@ -664,12 +664,12 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
 }
 
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream) {
-  static const int resident = [n_cu] {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcorr, kPcNT, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    return per_cu * n_cu;
+  static const int per_cu = [] {
+    int p = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, k_pcorr, kPcNT, 0) != hipSuccess || p < 1) p = 1;
+    return p;
   }();
+  const int resident = per_cu * n_cu;
   const long long groups = tiles * 4 * (ptile::kQuarter / kPcF);
   hipLaunchKernelGGL(k_pcorr, dim3((unsigned)std::min<long long>(groups, resident)), dim3(kPcNT), 0, stream, a);
   return hipGetLastError();

@@ -1809,10 +1809,10 @@ namespace {
 // persistent grids: exactly the resident capacity (blocks per CU from the
 // occupancy calculator x CUs), so no workgroup starts late and leaves a tail
 template <typename K>
-int resident_blocks(K kernel, int threads, int n_cu) {
+int blocks_per_cu(K kernel, int threads) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-  return per_cu * n_cu;
+  return per_cu;
 }
 }  // namespace
 
@@ -2008,7 +2008,8 @@ hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) 
 }
 
 hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev) {
-  static const int g_plpc = resident_blocks(k_plpc, 256, n_cu);
+  static const int p_plpc = blocks_per_cu(k_plpc, 256);
+  const int g_plpc = p_plpc * n_cu;
   const long long frames = (long long)a.n_streams * a.V;
   auto grid = [&](long long units, int resident) { return dim3((unsigned)std::min<long long>(units, resident)); };
   (void)hipGetLastError();

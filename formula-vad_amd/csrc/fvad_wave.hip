@@ -831,21 +831,22 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_olafb(StagedArgs a) {
 }
 
 namespace {
+// workgroups of a kernel one CU holds (occupancy calculator, once per kernel)
 template <typename K>
-int wave_resident_blocks(K kernel, int n_cu) {
+int wave_per_cu(K kernel) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64 * kWNW, 0) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  return per_cu * n_cu;
+  return per_cu;
 }
 }  // namespace
 
+// n_cu: the CUs the engine's stream may use (all, or its CU mask's)
 hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream) {
-  static const int g_fftA = wave_resident_blocks(k_fftAw, n_cu);
-  static const int g_pspec = wave_resident_blocks(k_pspecw, n_cu);
-  static const int g_synth = wave_resident_blocks(k_synthw, n_cu);
-  static const int g_fftb = wave_resident_blocks(k_fftbw, n_cu);
-  static const int g_olafb = wave_resident_blocks(k_olafb, n_cu);
+  static const int p_fftA = wave_per_cu(k_fftAw), p_pspec = wave_per_cu(k_pspecw), p_synth = wave_per_cu(k_synthw),
+                   p_fftb = wave_per_cu(k_fftbw), p_olafb = wave_per_cu(k_olafb);
+  const int g_fftA = p_fftA * n_cu, g_pspec = p_pspec * n_cu, g_synth = p_synth * n_cu, g_fftb = p_fftb * n_cu,
+            g_olafb = p_olafb * n_cu;
   if (which == kWaveOlaFb) {
     const int G = kWNW / a.n_channels;
     hipLaunchKernelGGL(k_olafb, dim3((unsigned)std::min<long long>((a.n_streams + G - 1) / G, g_olafb)), dim3(64 * kWNW),

@@ -116,6 +116,10 @@ typedef struct {
   int use_denoiser;     /* VAD.Config.use_denoiser (default 1).  0: fft_size frames of raw input go
                          * straight to FFT B (VAD.zig:206-212,239-249); per-tick vad / ratio are -1,
                          * the window ratio is preAnalyzeSegment's over the frame, window vad -1 */
+  uint32_t cu_mask[8];  /* CUs the engine's kernels may use (bit i of word i / 32 = CU i, as
+                         * hipExtStreamCreateWithCUMask); all zero = every CU.  Engines with disjoint
+                         * masks on one GPU run side by side without sharing a CU; persistent grids are
+                         * sized to the mask's CU count */
 } fvad_engine_config;
 
 /* staged: time-parallel frame kernels + a thin per-stream recurrence kernel;
