@@ -106,6 +106,15 @@ struct fvad_engine {
   long long *d_wstart = nullptr;
   int V = 0, L = 0, LX = 0, wmax = 0, grid_frames = 0;
   int wpt = 1;  // window slots per (tick, stream): windows_per_tick(fft_size)
+  // fp16 overlap (fvad::Overlap): k_gru16 on gstream (CU set A), the gated
+  // synthesis beside it on sstream (set B, where k_prep3 and the VADMachines
+  // run too, so no wave of theirs holds a GRU CU)
+  bool overlap = false;
+  hipStream_t gstream = nullptr, sstream = nullptr;
+  hipEvent_t ev_ov[3] = {};
+  unsigned *d_gate = nullptr;
+  uint32_t mask_a[8] = {}, mask_b[8] = {};
+  int n_cu_b = 0;
   // FFT B above kMaxFftB: tables [tw | sup | hann | perm] and k_fftb's scratch
   float *d_fbtab = nullptr;
   float2 *d_fbwork = nullptr;
@@ -308,7 +317,7 @@ void free_all(fvad_engine *e) {
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->d_gru16, e->d_gru16_bias, e->vadm.st, e->vadm.buf,
                   e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband,
-                  e->d_fbtab, e->d_fbwork};
+                  e->d_fbtab, e->d_fbwork, e->d_gate};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &set : e->evs)
@@ -321,6 +330,10 @@ void free_all(fvad_engine *e) {
   if (e->d_pcm16) (void)hipFree(e->d_pcm16);
 
   if (e->side) (void)hipStreamDestroy(e->side);
+  if (e->gstream) (void)hipStreamDestroy(e->gstream);
+  if (e->sstream) (void)hipStreamDestroy(e->sstream);
+  for (hipEvent_t ev : e->ev_ov)
+    if (ev) (void)hipEventDestroy(ev);
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
   if (e->cstream) (void)hipStreamDestroy(e->cstream);
   for (auto &sl : e->slots) {
@@ -387,9 +400,16 @@ void fill_bands(const fvad_engine_config &c, int *band_lo, int *band_hi, int *lo
 
 namespace {
 // an engine stream: on the config's CUs when it names any
-hipError_t make_stream(const fvad_engine *e, hipStream_t *s) {
+hipError_t make_stream(const fvad_engine *e, hipStream_t *s, const uint32_t *mask = nullptr) {
+  if (mask) return hipExtStreamCreateWithCUMask(s, 8, mask);
   if (mask_cus(e->cfg)) return hipExtStreamCreateWithCUMask(s, 8, e->cfg.cu_mask);
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+// fp16 overlap CU sets: CU i in set A iff (i / 8) % 2 == 0 -- every XCD keeps
+// half its CUs in each set whether the mask numbering runs XCD-major or
+// interleaves the XCDs
+void overlap_masks(int n_cu, uint32_t *a, uint32_t *b) {
+  for (int i = 0; i < n_cu && i < 256; i++) ((i / 8) % 2 == 0 ? a : b)[i / 32] |= 1u << (i % 32);
 }
 }  // namespace
 
@@ -454,9 +474,32 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     return rc;
   };
   if (hipSetDevice(c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipSetDevice failed"));
+  {
+    // fp16 overlap: default on (FVAD_FP16_OVERLAP=0 off) when the engine has
+    // the whole GPU and k_gru16's workgroups fit set A
+    hipDeviceProp_t prop;
+    static const bool ov_off = [] {
+      const char *v = getenv("FVAD_FP16_OVERLAP");
+      return v && atoi(v) == 0;
+    }();
+    if (c.mode == FVAD_MODE_FP16 && c.use_denoiser && !ov_off && !mask_cus(c) &&
+        hipGetDeviceProperties(&prop, c.device) == hipSuccess) {
+      overlap_masks(prop.multiProcessorCount, e->mask_a, e->mask_b);
+      int na = 0;
+      for (uint32_t w : e->mask_a) na += __builtin_popcount(w);
+      for (uint32_t w : e->mask_b) e->n_cu_b += __builtin_popcount(w);
+      e->overlap = (c.n_streams + 15) / 16 <= na && e->n_cu_b > 0;
+    }
+  }
   if (make_stream(e, &e->stream) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
+  if (e->overlap &&
+      (make_stream(e, &e->gstream, e->mask_a) != hipSuccess || make_stream(e, &e->sstream, e->mask_b) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_ov[0], hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_ov[1], hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_ov[2], hipEventDisableTiming) != hipSuccess))
+    return bail(fail(FVAD_EDEVICE, "overlap stream creation failed"));
   if (c.mode != FVAD_MODE_FUSED &&
-      (make_stream(e, &e->pstream) != hipSuccess ||
+      (make_stream(e, &e->pstream, e->overlap ? e->mask_b : nullptr) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[0], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[1], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_buf_free[0], hipEventDisableTiming) != hipSuccess ||
@@ -527,6 +570,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
         (rc = dalloc(&e->d_gr, F * fvad::kBands)) || (rc = dalloc(&e->d_gs, F * fvad::kBands)))
       return bail(rc);
     e->d_xs = e->d_xs_b[0];
+    if (e->overlap && (rc = dalloc(&e->d_gate, 1 + (B + 15) / 16))) return bail(rc);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "device query failed"));
     // CUs; persistent grids are sized per kernel
@@ -606,7 +650,7 @@ int launch_fused(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
 
 int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bool timed) {
   const fvad_engine_config &c = e->cfg;
-  fvad::StagedArgs a;
+  fvad::StagedArgs a{};
   a.n_streams = c.n_streams;
   a.n_channels = c.n_channels;
   a.n_ticks = n_ticks;
@@ -657,6 +701,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   a.win_start = e->d_wstart;
   a.wmax = e->wmax;
   a.wpt = e->wpt;
+  a.gate = e->overlap ? e->d_gate : nullptr;
   if (e->d_fbtab) {  // fft_size > kMaxFftB: [tw | sup | hann | perm] (fvad_engine_create)
     const size_t n = c.fft_size;
     a.fb_tw = reinterpret_cast<const float2 *>(e->d_fbtab);
@@ -701,7 +746,9 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
     // window output set b is free once push k-2's k_vadm_hbm has read it
     if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
-    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr));
+    fvad::Overlap ov{e->gstream, e->sstream, e->ev_ov[0], e->ev_ov[1], e->ev_ov[2], e->n_cu_b,
+                     sizeof(unsigned) * (1 + (size_t)(c.n_streams + 15) / 16)};
+    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr, e->overlap ? &ov : nullptr));
   } else {
     // no denoiser: raw input frames to the ring, windows, FFT B, all on the
     // engine stream after the input copy (queued on the prep stream)
@@ -1284,6 +1331,8 @@ extern "C" int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out)
 
 extern "C" int fvad_engine_windows_per_tick(const fvad_engine *e) { return e ? e->wpt : FVAD_EINVAL; }
 
+extern "C" int fvad_engine_fp16_overlap(const fvad_engine *e) { return e ? (int)e->overlap : FVAD_EINVAL; }
+
 extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
   if (e && i == e->n_kernels && e->vadm.n > 0) return "k_vadm_hbm";
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
@@ -1381,7 +1430,7 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
   if ((rc = dalloc(&e->d_vflag, TB)) || (rc = dalloc(&e->d_vwratio, TBW)) || (rc = dalloc(&e->d_vwvad, TBW)) ||
       (rc = dalloc(&e->d_vband, TBW * e->cfg.n_channels * e->cfg.n_bands)) || (rc = dalloc(&e->d_vticks, (size_t)B)))
     return rc;
-  if (make_stream(e, &e->side) != hipSuccess ||
+  if (make_stream(e, &e->side, e->overlap ? e->mask_b : nullptr) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_vadm, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&e->ev_vt[0][0]) != hipSuccess || hipEventCreate(&e->ev_vt[0][1]) != hipSuccess ||

@@ -585,8 +585,24 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     }
     if (pf_lane) L.pf[pfs][pfi] = pf_next;  // read by the next phase A only
     WSTAMP_END(1);
-    lds_sync();
+    if (a.gate) {
+      // fp16 overlap: the gains of frames <= u - 4 are final; publish them to
+      // the synthesis waves running on the other CUs (every wave's stores
+      // drained by the barrier, then one agent-scope release)
+      __syncthreads();
+      if (tid == 0) {
+        __threadfence();
+        __hip_atomic_store(&a.gate[1 + blockIdx.x], (unsigned)max(0, u - 3), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      lds_sync();
+    }
     RSTAMP(1);
+  }
+  if (a.gate && tid == 0) {
+    __threadfence();
+    __hip_atomic_store(&a.gate[1 + blockIdx.x], 0x7fffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef FVAD_STAMPS
   if (lane == 0 && a.stamps) {

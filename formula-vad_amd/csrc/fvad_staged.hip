@@ -2007,7 +2007,7 @@ hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) 
   return hipSuccess;
 }
 
-hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev) {
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev, const Overlap *ov) {
   static const int p_plpc = blocks_per_cu(k_plpc, 256);
   const int g_plpc = p_plpc * n_cu;
   const long long frames = (long long)a.n_streams * a.V;
@@ -2042,12 +2042,31 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   REC(7);
   FVAD_LAUNCH_TRY(launch_wave(kWavePspec, a, n_cu, stream));
   REC(8);
-  if (a.gru16_frags)  // FVAD_MODE_FP16: the GRU stack on the matrix cores (configs[4])
-    FVAD_LAUNCH_TRY(launch_gru16(a, stream));
-  else
-    FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
-  REC(9);
-  FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
+  if (ov) {
+    // fp16 overlap: the GRU on its own CUs, the synthesis of the frames whose
+    // gains it has published on the others meanwhile, the rest on every CU
+    // after it (the k_gru16 events bracket the GRU, the k_synthw ones the
+    // synthesis left once the GRU is done)
+    FVAD_LAUNCH_TRY(hipMemsetAsync(a.gate, 0, ov->gate_bytes, stream));
+    FVAD_LAUNCH_TRY(hipEventRecord(ov->ev_p, stream));
+    FVAD_LAUNCH_TRY(hipStreamWaitEvent(ov->g, ov->ev_p, 0));
+    FVAD_LAUNCH_TRY(hipStreamWaitEvent(ov->s, ov->ev_p, 0));
+    FVAD_LAUNCH_TRY(launch_gru16(a, ov->g));
+    if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[9], ov->g));
+    FVAD_LAUNCH_TRY(hipEventRecord(ov->ev_g, ov->g));
+    FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, ov->n_cu_s, ov->s));
+    FVAD_LAUNCH_TRY(hipEventRecord(ov->ev_s, ov->s));
+    FVAD_LAUNCH_TRY(hipStreamWaitEvent(stream, ov->ev_g, 0));
+    FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
+    FVAD_LAUNCH_TRY(hipStreamWaitEvent(stream, ov->ev_s, 0));
+  } else {
+    if (a.gru16_frags)  // FVAD_MODE_FP16: the GRU stack on the matrix cores (configs[4])
+      FVAD_LAUNCH_TRY(launch_gru16(a, stream));
+    else
+      FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
+    REC(9);
+    FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
+  }
   REC(10);
   if (olafb_fused(a)) {
     // overlap-add, window bookkeeping and FFT B in one kernel (k_olafb);

@@ -30,6 +30,7 @@ namespace fvad {
 constexpr int kWB = 8;   // frames per wave batch
 constexpr int kWNW = 4;  // waves per workgroup
 constexpr int kWOcc = 3;  // workgroups per CU (<= 168 VGPRs, <= 53 KB LDS)
+constexpr int kGruS = 16;  // streams per k_gru16 workgroup (fvad_gru16.hip kGS)
 
 
 // Batches of a wave: dynamic (per-XCD queues, wave_take) or static striding
@@ -313,9 +314,33 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
   float *tr = reinterpret_cast<float *>(R);
   float *rr = bp[wv][0], *nrm = bp[wv][1], *gsm = bp[wv][2];
   const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
-  for (long long g = wave_first(a, kWaveSynth, kWorkSynth, lane); g < nb; g = wave_next(a, kWaveSynth, kWorkSynth, lane, g)) {
+  // fp16 overlap (a.gate): batches tick-major from one queue -- batch b is
+  // frames 8 (b / B) .. + 7 of stream b % B -- each once its GRU workgroup has
+  // published their gains; this kernel runs on the CUs k_gru16 does not use,
+  // and a second instance on every CU after it
+  const int C = a.n_channels, B = a.n_streams, nvb = (a.n_ticks * C + kWB - 1) / kWB;
+  const long long nbg = (long long)B * nvb;
+  auto gate_take = [&]() -> long long {
+    unsigned v = 0;
+    if (lane == 0) v = atomicAdd(&a.gate[0], 1u);
+    return __shfl(v, 0);
+  };
+  auto gate_frames = [&](long long b) -> int {
+    const int s = (int)(b % B), vb = (int)(b / B);
+    const int nf = ticks_of(a, s) * C, v = vb * kWB + lane;
+    if (lane == 0) {
+      const unsigned need = (unsigned)min(vb * kWB + kWB, nf);
+      const unsigned *pg = a.gate + 1 + s / kGruS;
+      while (__hip_atomic_load(pg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return (lane < kWB && v < nf) ? (int)((long long)s * a.V + v) : -1;
+  };
+  const bool gated = a.gate != nullptr;
+  for (long long g = gated ? gate_take() : wave_first(a, kWaveSynth, kWorkSynth, lane); g < (gated ? nbg : nb);
+       g = gated ? gate_take() : wave_next(a, kWaveSynth, kWorkSynth, lane, g)) {
     // the batch's frames and silence flags, lane per frame
-    const int fl = batch_frames(a, g, lane);
+    const int fl = gated ? gate_frames(g) : batch_frames(a, g, lane);
     const int sl = fl >= 0 ? a.silence[fl] : 0;
     settle(sl);
     for (int fr = 0; fr < kWB; fr++) {

@@ -155,6 +155,7 @@ SYMBOLS = [
     ("fvad_engine_kernel_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("fvad_engine_kernel_name", C.c_char_p, [C.c_void_p, C.c_int]),
     ("fvad_engine_windows_per_tick", C.c_int, [C.c_void_p]),
+    ("fvad_engine_fp16_overlap", C.c_int, [C.c_void_p]),
     ("fvad_engine_attach_vadm", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     ("fvad_engine_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
     ("fvad_engine_segments_range", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_size_t]),
@@ -300,6 +301,7 @@ class Engine:
         # window slots per (tick, stream): 1 for fft_size >= 480, else several
         # (VAD.zig:307-347); with W > 1 the window outputs get a slot axis
         self.wpt = lib().fvad_engine_windows_per_tick(h)
+        self.overlap = bool(lib().fvad_engine_fp16_overlap(h))
 
     def _alloc_out(self, n_ticks, denoised):
         T, B, Ch, nb, W = n_ticks, self.B, self.C, self.nb, self.wpt
