@@ -567,8 +567,15 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
           const float al = .6f * L.lastg[s][i];
           const float gsm = (gi > al) ? gi : al;
           L.lastg[s][i] = gsm;
-          a.gr[f * kBands + i] = gi;
-          a.gs[f * kBands + i] = gsm;
+          if (a.gate) {
+            // fp16 overlap: read by the synthesis on other CUs (other XCDs'
+            // L2s) before this kernel ends -- write-through (sc1) stores
+            __hip_atomic_store(&a.gr[f * kBands + i], gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.gs[f * kBands + i], gsm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            a.gr[f * kBands + i] = gi;
+            a.gs[f * kBands + i] = gsm;
+          }
         }
       }
     } else {
@@ -587,23 +594,22 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     WSTAMP_END(1);
     if (a.gate) {
       // fp16 overlap: the gains of frames <= u - 4 are final; publish them to
-      // the synthesis waves running on the other CUs (every wave's stores
-      // drained by the barrier, then one agent-scope release)
+      // the synthesis waves on the other CUs: the gains went out write-through
+      // (sc1) and the barrier drained every wave's stores (vmcnt(0)), so the
+      // flag -- also a write-through store -- follows them to memory.  (An
+      // agent-scope release fence here wrote back the whole L2 of the XCD
+      // every superstep: k_gru16 0.56 -> 1.17 ms.)
       __syncthreads();
-      if (tid == 0) {
-        __threadfence();
+      if (tid == 0)
         __hip_atomic_store(&a.gate[1 + blockIdx.x], (unsigned)max(0, u - 3), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      }
     } else {
       lds_sync();
     }
     RSTAMP(1);
   }
-  if (a.gate && tid == 0) {
-    __threadfence();
+  if (a.gate && tid == 0)  // (the last superstep's barrier drained the stores)
     __hip_atomic_store(&a.gate[1 + blockIdx.x], 0x7fffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 #ifdef FVAD_STAMPS
   if (lane == 0 && a.stamps) {
     atomicAdd(&a.stamps[W], wacc[0]);

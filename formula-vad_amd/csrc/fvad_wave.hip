@@ -333,7 +333,10 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
       const unsigned *pg = a.gate + 1 + s / kGruS;
       while (__hip_atomic_load(pg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) __builtin_amdgcn_s_sleep(8);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // the gains are read with coherent (sc1) loads below; this only keeps
+    // the compiler from moving them above the wait (an agent-scope acquire
+    // would invalidate the XCD's L2 for every batch)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     return (lane < kWB && v < nf) ? (int)((long long)s * a.V + v) : -1;
   };
   const bool gated = a.gate != nullptr;
@@ -360,7 +363,10 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
 #pragma unroll
       for (int r = 0; r < 8; r++) pv[r] = P[min(64 * r + lane, kFreq - 1)];
       const size_t o = (size_t)f * kBands + min(lane, kBands - 1);
-      const float Exp = a.Exp[o], gg = a.gr[o], Ex = a.Ex[o], Ep = a.Ep[o], gs = a.gs[o];
+      const float Exp = a.Exp[o], Ex = a.Ex[o], Ep = a.Ep[o];
+      // gains: written by k_gru16 during this kernel under the fp16 overlap
+      const float gg = gated ? __hip_atomic_load(&a.gr[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.gr[o];
+      const float gs = gated ? __hip_atomic_load(&a.gs[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.gs[o];
       if (fil) {
         if (lane < kBands) {
           float r;

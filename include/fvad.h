@@ -165,7 +165,8 @@ int fvad_engine_windows_per_tick(const fvad_engine *e);
 /* 1 when an FVAD_MODE_FP16 engine overlaps its GRU with the synthesis: k_gru16
  * on one half of the CUs, the synthesis of the frames whose gains it has
  * published on the other half, the rest on every CU after it (same results;
- * default on for an engine with the whole GPU, FVAD_FP16_OVERLAP=0 off) */
+ * opt-in with FVAD_FP16_OVERLAP=1 for an engine with the whole GPU: measured
+ * slower than the sequential schedule) */
 int fvad_engine_fp16_overlap(const fvad_engine *e);
 
 /* pcm: host [ticks][streams][channels][480] normalised f32.  ticks_valid

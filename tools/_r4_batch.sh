@@ -1,6 +1,5 @@
 #!/bin/bash
-# one GPU call: fp16 overlap identity test first (its own time limit), then
-# the A/B measurements; every step bounded, the chain stops at the first failure
+# one GPU call: k_plpcs parity (full-size, bit-exact) then A/B of its segment length
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -8,12 +7,26 @@ set -o pipefail
 timeout -k 10 300 python -u -m pytest tests/test_gpu_fp16.py -x -v --timeout 280 --timeout-method thread \
   -k "overlap" > gpurun_out/b_ovtest.log 2>&1 || { echo "overlap test failed"; tail -30 gpurun_out/b_ovtest.log; exit 1; }
 tail -2 gpurun_out/b_ovtest.log
-timeout -k 10 400 python -u -m pytest tests/test_gpu_fp16.py tests/test_gpu_vadm.py -x -q --timeout 300 \
-  --timeout-method thread > gpurun_out/b_fp16.log 2>&1 || { echo "fp16 tests failed"; tail -30 gpurun_out/b_fp16.log; exit 1; }
-tail -1 gpurun_out/b_fp16.log
-timeout -k 10 600 bash tools/ab_quick.sh FVAD_FP16_OVERLAP=0 > gpurun_out/b_abov.log 2>&1 || { tail -20 gpurun_out/b_abov.log; exit 1; }
-cat gpurun_out/b_abov.log
-timeout -k 10 250 python -u tools/split_probe.py staged 12 > gpurun_out/b_split.log 2>&1 || { tail -20 gpurun_out/b_split.log; exit 1; }
-cat gpurun_out/b_split.log
-timeout -k 10 300 bash tools/ab_libs.sh staged 2 base lt8 lt32 > gpurun_out/b_ablt.log 2>&1 || { tail -20 gpurun_out/b_ablt.log; exit 1; }
-cat gpurun_out/b_ablt.log
+for rep in 1 2; do
+  for OV in 1 0; do
+    FVAD_FP16_OVERLAP=$OV timeout -k 10 200 python3 bench.py --cpu-baseline 0 --host-rate 0 --variants 0 --resident-pushes 4 \
+      --mode fp16 > gpurun_out/b_ov.log 2>&1 || { tail -20 gpurun_out/b_ov.log; exit 1; }
+    python3 -c "
+import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print('fp16 overlap', sys.argv[2], d['value'], d['ms_per_step'], {k:round(v['ms'],3) for k,v in d['roofline']['kernels'].items()})" gpurun_out/b_ov.log $OV
+  done
+done
+FVAD_PLPC_K=4 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -q --timeout 300 \
+  --timeout-method thread -k "not fp16" > gpurun_out/b_ps.log 2>&1 || { echo "plpcs tests failed"; tail -30 gpurun_out/b_ps.log; exit 1; }
+tail -1 gpurun_out/b_ps.log
+summ() { python3 -c "
+import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+k=d['roofline']['kernels'];print(sys.argv[2], d['value'], d['ms_per_step'], k['k_plpc']['ms'], k['k_pcorr']['ms'], k['k_fftAw']['ms'])" "$1" "$2"; }
+for rep in 1 2; do
+  for K in 0 4 8; do
+    FVAD_PLPC_K=$K timeout -k 10 200 python3 bench.py --cpu-baseline 0 --host-rate 0 --variants 0 --resident-pushes 4 \
+      > gpurun_out/b_psk.log 2>&1 && summ gpurun_out/b_psk.log "K=$K" || { tail -20 gpurun_out/b_psk.log; exit 1; }
+  done
+done
+timeout -k 10 400 bash tools/ab_libs.sh staged 1 pr12 pr20 pr24u2 base > gpurun_out/b_pr.log 2>&1 || { tail -20 gpurun_out/b_pr.log; exit 1; }
+cat gpurun_out/b_pr.log
