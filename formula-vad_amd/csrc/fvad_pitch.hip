@@ -65,9 +65,6 @@ static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
 #ifndef FVAD_Q1_B64
 #define FVAD_Q1_B64 0
 #endif
-#ifndef FVAD_Q1_MFMA
-#define FVAD_Q1_MFMA 1 // Q1: approximate xcorr on MFMA, exact sums for the scan's survivors only
-#endif
 #ifndef FVAD_Q5_COMPACT
 #define FVAD_Q5_COMPACT 1
 #endif
@@ -93,7 +90,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
   __shared__ float sfl[kPcF][10], fine[kPcF][10];
   __shared__ unsigned char lst[kPcF][kPcSP - 1];  // lags of the coarse scan's survivors (Q1 -> Q2)
   __shared__ int ncand[kPcF];
-  __shared__ float qE[kPcF];  // Q1: the frames' xcorr error bounds
   __shared__ int best[kPcF][2], T0s[kPcF], nvs[kPcF], fval[kPcF];
   __shared__ long long fidx[kPcF];
   // yy_lookup checkpoints yy_{8k}, k = 0..48: k < 6 (walked during Q2, while
@@ -227,120 +223,11 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     }
     __syncthreads();
     RSTAMP(0);
-#if FVAD_Q1_MFMA
-    // Q1 on MFMA, exact sums for the survivors only.  (a) approximate coarse
-    // xcorr of all 147 lags: with bf16 operands and f32 accumulation,
-    //   D[r][c] = sum_k y_lp4[k + 15 r] x_lp4[k - c] = xcorr[c + 15 r]
-    // (r < 10, c < 15; x_lp4[i] = 0 outside 0..239), K = 256 in 8 steps of
-    // v_mfma_f32_16x16x32_bf16, one wave per frame at a time.  Lane l holds
-    // A[r = l & 15][k = kb + 8 (l >> 4) + j] and B[k][c = l & 15], j < 8: every
-    // operand is 8 stride-2 floats of the frame's xf row (ds_read2_b32 pairs;
-    // the A rows 15 r and B columns -c spread over the banks).  Plus each
-    // frame's bound E = 0.02 sqrt(xx4 * sum y_lp4^2): every summation order's
-    // xcorr (the C order's included) lies within 0.0040 sum|x y| <=
-    // 0.0040 sqrt(xx4 * sum y^2) of the exact value (bf16 rounding 2^-9 per
-    // operand, 256-term f32 accumulation), and 0.02 covers that even for a
-    // truncating conversion; 1e-25 covers flushed denormals.
-    {
-      typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-      typedef float f4 __attribute__((ext_vector_type(4)));
-      const int w = tq >> 6, l = tq & 63, rc = l & 15, q = l >> 4;
-      const int ra = min(rc, 9);  // A rows 10..15 repeat row 9 (their lags are not used)
-#pragma unroll 1
-      for (int ff = 0; ff < 2; ff++) {
-        const int fr = 2 * w + ff;
-        const float *xr = xf[fr];
-        const float *Ab = xr + 2 * (8 * q + 15 * ra);   // y_lp4[8q + 15r + k]
-        const float *Bb = xr + 384 + 2 * (8 * q - rc);  // x_lp4[8q - c + k]
-        f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-        auto step = [&](int kb, int mode) {
-          bf16x8 av, bv;
-#pragma unroll
-          for (int j = 0; j < 8; j++) {
-            av[j] = (__bf16)Ab[2 * (kb + j)];
-            const int i = kb + 8 * q + j - rc;  // x_lp4 index of this B element
-            float b;
-            if (mode == 0)
-              b = (i >= 0) ? Bb[2 * (kb + j)] : 0.0f;
-            else if (mode == 2)
-              b = (i < 240) ? xr[384 + 2 * min(i, 239)] : 0.0f;
-            else
-              b = Bb[2 * (kb + j)];
-            bv[j] = (__bf16)b;
-          }
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
-        };
-        step(0, 0);
-#pragma unroll 1
-        for (int kb = 32; kb < 224; kb += 32) step(kb, 1);
-        step(224, 2);
-        // D[row = 4q + reg][col = rc]: lag rc + 15 (4q + reg)
-#pragma unroll
-        for (int reg = 0; reg < 4; reg++) {
-          const int r = 4 * q + reg, lag = rc + 15 * r;
-          if (rc < 15 && r < 10 && lag < 147) xc[fr][lag] = acc[reg];
-        }
-        // the frame's bound: partial sums of x_lp4^2 (240) and y_lp4^2 (432)
-        float sx = 0.0f, sy = 0.0f;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int i = l + 64 * u;
-          if (i < 240) sx += xr[384 + 2 * i] * xr[384 + 2 * i];
-        }
-#pragma unroll
-        for (int u = 0; u < 7; u++) {
-          const int m = l + 64 * u;
-          if (m < 432) sy += xr[2 * m] * xr[2 * m];
-        }
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          sx += __shfl_xor(sx, d);
-          sy += __shfl_xor(sy, d);
-        }
-        if (l == 0) qE[fr] = 0.02f * sqrtf(1.001f * sx * sy) + 1e-25f;
-      }
-    }
-    __syncthreads();
-#endif
     // Q1: xcorr[k] = sum_j x_lp4[j] y_lp4[j+k], x_lp4[j] = xf[384+2j], y_lp4[m] = xf[2m]
     {
       constexpr int R = 5;
       static_assert(R * (kPcL - 1) >= 147 && 240 % R == 0 && kPcL == 32, "Q1 lag blocks");
       const int fr = tq / kPcL, l = tq % kPcL, k0 = R * l;
-#if FVAD_Q1_MFMA
-      // (b) the filter below on bounds from the approximations: hi >= the C
-      // order's ratio (or -inf where its xcorr cannot be > 0), lo <= it (or
-      // -inf where it is not surely > 0); the prefix top-2 runs on lo, the
-      // test on hi
-      constexpr float kNoRatio = -__builtin_inff();
-      float rho[R], rlo[R];
-      {
-        const float E = qE[fr];
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-          rho[r] = rlo[r] = kNoRatio;
-          if (k0 + r < 147) {
-            const float xa = xc[fr][k0 + r], ir = __builtin_amdgcn_rcpf(scl[fr][k0 + r]);
-            if (xa + E > 0) {
-              const float t = (xa + E) * 1e-12f;
-              rho[r] = (t * t) * ir;
-            }
-            if (xa - E > 0) {
-              const float t = (xa - E) * 1e-12f;
-              rlo[r] = (t * t) * ir;
-            }
-          }
-        }
-      }
-      if (k0 >= 147 && k0 < kPcSP)
-        for (int k = 147; k < kPcSP; k++) xc[fr][k] = -1.0f;
-      float m1 = kNoRatio, m2 = kNoRatio;
-#pragma unroll
-      for (int r = 0; r < R; r++) {
-        m2 = fmaxf(m2, fminf(m1, rlo[r]));
-        m1 = fmaxf(m1, rlo[r]);
-      }
-#else
       float acc[R];
 #pragma unroll
       for (int r = 0; r < R; r++) acc[r] = 0.0f;
@@ -401,8 +288,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         m2 = fmaxf(m2, fminf(m1, v));
         m1 = fmaxf(m1, v);
       }
-      const float(&rlo)[R] = rho;
-#endif
       int self = tq & 63;
       asm volatile("" : "+v"(self));
       // inclusive prefix top-2 over the frame's 32 lanes, then exclusive
@@ -421,8 +306,8 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
 #pragma unroll
       for (int r = 0; r < R; r++) {
         if (rho[r] != kNoRatio && !(e2 > rho[r] * 1.001f)) mask |= 1u << r;
-        e2 = fmaxf(e2, fminf(e1, rlo[r]));
-        e1 = fmaxf(e1, rlo[r]);
+        e2 = fmaxf(e2, fminf(e1, rho[r]));
+        e1 = fmaxf(e1, rho[r]);
       }
       // the survivors' lags in order
       const int c = __builtin_popcount(mask);
@@ -444,30 +329,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
       }
     }
     __syncthreads();
-#if FVAD_Q1_MFMA
-    // (c) the exact C-order xcorr of the survivors, the only lags Q2 reads:
-    // items (valid frame, survivor) packed from lane 0 in frame order
-    {
-      int total = 0;
-#pragma unroll
-      for (int f = 0; f < kPcF; f++) total += fval[f] ? ncand[f] : 0;
-      for (int it = tq; it < total; it += NT) {
-        int fr = 0, b = it;
-        while (b >= (fval[fr] ? ncand[fr] : 0)) {
-          b -= fval[fr] ? ncand[fr] : 0;
-          fr++;
-        }
-        const int k = lst[fr][b];
-        const float *X = xf[fr] + (kPitchMax >> 1);
-        const float *Y = xf[fr] + 2 * k;
-        float s = 0.0f;
-#pragma unroll 8
-        for (int j = 0; j < 240; j++) s = s + X[2 * j] * Y[2 * j];
-        xc[fr][k] = s;
-      }
-    }
-    __syncthreads();
-#endif
     RSTAMP(1);
     // remove_doubling's yy_lookup recurrence, lane per frame on wave 2 (idle
     // from Q2 to Q4), in three pieces beside Q2, Q3 and Q4:
