@@ -18,4 +18,13 @@ timeout -k 10 900 bash tools/profile.sh ${TAG}_staged > gpurun_out/base_prof_s.l
 timeout -k 10 900 bash tools/profile.sh ${TAG}_fp16 --mode fp16 > gpurun_out/base_prof_f.log 2>&1 || { tail -20 gpurun_out/base_prof_f.log; exit 1; }
 cp profiles/pmc_traffic*.json gpurun_out/ 2>/dev/null
 ls profiles | grep "$TAG" | sed 's/^/profiles\//' | xargs -I{} cp {} gpurun_out/
+
+# stream-count scaling of the per-kernel times (rounds vs throughput)
+for B in 1536 1024; do
+  timeout -k 10 200 python3 bench.py --cpu-baseline 0 --host-rate 0 --variants 0 --resident-pushes 4 --streams-per-gpu $B \
+    > gpurun_out/base_scale_$B.log 2>&1 || break
+  python3 -c "
+import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], round(d['value']/1e6,2), d['ms_per_step'], {k:round(v['ms'],3) for k,v in d['roofline']['kernels'].items()})" gpurun_out/base_scale_$B.log $B
+done
 echo done
