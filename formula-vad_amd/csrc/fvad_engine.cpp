@@ -94,7 +94,15 @@ struct fvad_engine {
   int *wflag_b[2] = {};
   float *wratio_b[2] = {}, *wvad_b[2] = {}, *band_b[2] = {};
   hipEvent_t ev_vadm_b[2] = {};
-  int32_t *d_vflag = nullptr, *d_vticks = nullptr;
+  int32_t *d_vflag = nullptr, *d_vticks = nullptr, *d_vticks_b[2] = {};
+  // The VADMachine of push k is enqueued when the next push is launched, as
+  // k_vadm_hbm (32 waves, overlapping that push quietly: the 512-wave burst of
+  // k_vadm_par beside the next push's k_fftAw cost more than it saved,
+  // measured), or at a sync point with nothing else queued as k_vadm_par
+  // (0.25 ms instead of 1.45: the drain of a job's last push).
+  bool vpend = false, vpend_timed = false;
+  int vpend_b = 0;
+  fvad::StagedArgs vpend_args{};
   float *d_vwratio = nullptr, *d_vwvad = nullptr, *d_vband = nullptr;
   double vadm_ms_sum = 0;
   int vadm_timed = 0;
@@ -316,7 +324,7 @@ void free_all(fvad_engine *e) {
                   e->d_model, e->d_stamps, e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->d_gru16, e->d_gru16_bias, e->vadm.st, e->vadm.buf,
-                  e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vwratio, e->d_vwvad, e->d_vband,
+                  e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vticks_b[1], e->d_vwratio, e->d_vwvad, e->d_vband,
                   e->d_fbtab, e->d_fbwork, e->d_gate};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -355,6 +363,7 @@ void free_all(fvad_engine *e) {
 }  // namespace
 
 int vadm_reset(fvad_engine *e);
+int vadm_flush(fvad_engine *e, bool fast);
 
 extern "C" int fvad_engine_reset(fvad_engine *e) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
@@ -362,6 +371,7 @@ extern "C" int fvad_engine_reset(fvad_engine *e) {
   if (e->cstream) HIP_TRY(hipStreamSynchronize(e->cstream));
   if (e->pstream) HIP_TRY(hipStreamSynchronize(e->pstream));
   if (e->vadm.n > 0) {
+    if (const int rf = vadm_flush(e, true)) return rf;
     HIP_TRY(hipStreamSynchronize(e->side));
     const int rc = vadm_reset(e);
     if (rc) return rc;
@@ -600,6 +610,7 @@ extern "C" void fvad_engine_destroy(fvad_engine *e) {
   (void)hipSetDevice(e->cfg.device);
   if (e->cstream) (void)hipStreamSynchronize(e->cstream);
   if (e->pstream) (void)hipStreamSynchronize(e->pstream);
+  if (e->side) (void)vadm_flush(e, true);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->side) (void)hipStreamSynchronize(e->side);
   free_all(e);
@@ -650,6 +661,39 @@ int launch_fused(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
   return FVAD_OK;
 }
 
+}  // namespace
+
+// k_vadm of one push on the side stream (its waits already queued), with
+// its timing pair and the events later pushes wait for
+int enqueue_vadm(fvad_engine *e, const fvad::StagedArgs &v, int b, bool timed, bool fast) {
+  // k_vadm timing never blocks the host (it would serialise the overlap):
+  // two event pairs alternate and are read once complete
+  const int slot = e->vadm_slot ^= 1;
+  if (timed) {
+    e->vadm_pending[slot] = false;  // an unread older sample in this slot is dropped
+    HIP_TRY(hipEventRecord(e->ev_vt[slot][0], e->side));
+  }
+  HIP_TRY(fvad::launch_vadm(v, e->side, fast));
+  if (timed) {
+    HIP_TRY(hipEventRecord(e->ev_vt[slot][1], e->side));
+    e->vadm_pending[slot] = true;
+  }
+  HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
+  HIP_TRY(hipEventRecord(e->ev_vadm_b[b], e->side));
+  return FVAD_OK;
+}
+
+// the last push's VADMachine, enqueued now (after its push's kernels);
+// fast: nothing else is queued behind it (a sync point)
+int vadm_flush(fvad_engine *e, bool fast = true) {
+  if (!e->vpend) return FVAD_OK;
+  e->vpend = false;
+  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_copy, 0));
+  return enqueue_vadm(e, e->vpend_args, e->vpend_b, e->vpend_timed, fast);
+}
+
+namespace {
+
 int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bool timed) {
   const fvad_engine_config &c = e->cfg;
   fvad::StagedArgs a{};
@@ -658,6 +702,9 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   a.n_ticks = n_ticks;
   a.V = e->V;
   a.L = e->L;
+  // the previous push's VADMachine (ev_copy still marks that push's end)
+  if (e->vpend)
+    if (const int rf = vadm_flush(e, false)) return rf;
   // push k uses buffer b = k & 1 of xs / ratio / ticks; its k_prep3 waits
   // (on pstream) until push k-2 released b, then runs beside push k-1
   const int b = e->next_buf;
@@ -760,32 +807,17 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     HIP_TRY(fvad::launch_nodenoise(a, e->grid_frames, e->stream));
   }
   if (e->vadm.n > 0) {
-    const fvad_engine_config &c = e->cfg;
-    const size_t TB = (size_t)n_ticks * c.n_streams;
-    (void)TB;
-    // the ticks copy may be overwritten only once the previous k_vadm_hbm has read it
-    if (use_ticks) {
-      HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm, 0));
-      HIP_TRY(hipMemcpyAsync(e->d_vticks, e->d_ticks, (size_t)c.n_streams * 4, hipMemcpyDeviceToDevice, e->stream));
-    }
+    // the ticks copy of parity b may be overwritten once push k - 2's
+    // VADMachine has read it (ev_vadm_b[b], waited for above)
+    if (use_ticks)
+      HIP_TRY(hipMemcpyAsync(e->d_vticks_b[b], e->d_ticks, (size_t)c.n_streams * 4, hipMemcpyDeviceToDevice, e->stream));
     HIP_TRY(hipEventRecord(e->ev_copy, e->stream));
-    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_copy, 0));
     fvad::StagedArgs v = a;
-    v.ticks_valid = use_ticks ? e->d_vticks : nullptr;
-    // k_vadm_hbm timing never blocks the host (it would serialise the overlap):
-    // two event pairs alternate and are read once complete
-    const int slot = e->vadm_slot ^= 1;
-    if (timed) {
-      e->vadm_pending[slot] = false;  // an unread older sample in this slot is dropped
-      HIP_TRY(hipEventRecord(e->ev_vt[slot][0], e->side));
-    }
-    HIP_TRY(fvad::launch_vadm(v, e->side));
-    if (timed) {
-      HIP_TRY(hipEventRecord(e->ev_vt[slot][1], e->side));
-      e->vadm_pending[slot] = true;
-    }
-    HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
-    HIP_TRY(hipEventRecord(e->ev_vadm_b[b], e->side));
+    v.ticks_valid = use_ticks ? e->d_vticks_b[b] : nullptr;
+    e->vpend = true;
+    e->vpend_args = v;
+    e->vpend_b = b;
+    e->vpend_timed = timed;
   }
   // every reader of buffer b (incl. the copy of ticks for k_vadm_hbm) is queued
   HIP_TRY(hipEventRecord(e->ev_buf_free[b], e->stream));
@@ -1289,6 +1321,8 @@ extern "C" int fvad_engine_sync(fvad_engine *e) {
   HIP_TRY(hipSetDevice(e->cfg.device));
   if (e->cstream) HIP_TRY(hipStreamSynchronize(e->cstream));
   if (e->pstream) HIP_TRY(hipStreamSynchronize(e->pstream));
+  if (e->side)
+    if (const int rf = vadm_flush(e, true)) return rf;
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (e->side) {
     HIP_TRY(hipStreamSynchronize(e->side));
@@ -1430,7 +1464,8 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
   e->vadm_buf_len = (size_t)off;
   const size_t TB = (size_t)e->cfg.max_ticks * B, TBW = TB * e->wpt;
   if ((rc = dalloc(&e->d_vflag, TB)) || (rc = dalloc(&e->d_vwratio, TBW)) || (rc = dalloc(&e->d_vwvad, TBW)) ||
-      (rc = dalloc(&e->d_vband, TBW * e->cfg.n_channels * e->cfg.n_bands)) || (rc = dalloc(&e->d_vticks, (size_t)B)))
+      (rc = dalloc(&e->d_vband, TBW * e->cfg.n_channels * e->cfg.n_bands)) || (rc = dalloc(&e->d_vticks, (size_t)B)) ||
+      (rc = dalloc(&e->d_vticks_b[1], (size_t)B)))
     return rc;
   if (make_stream(e, &e->side, e->overlap ? e->mask_b : nullptr) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_copy, hipEventDisableTiming) != hipSuccess ||
@@ -1440,6 +1475,7 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
       hipEventCreateWithFlags(&e->ev_vadm_b[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_vadm_b[1], hipEventDisableTiming) != hipSuccess)
     return fail(FVAD_EDEVICE, "side stream / event creation failed");
+  e->d_vticks_b[0] = e->d_vticks;
   HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
   HIP_TRY(hipEventRecord(e->ev_vadm_b[0], e->side));
   HIP_TRY(hipEventRecord(e->ev_vadm_b[1], e->side));
@@ -1461,6 +1497,7 @@ extern "C" int fvad_engine_vadm_state(fvad_engine *e, int stream, int machine, i
     return fail(FVAD_EINVAL, "no such attached machine");
   HIP_TRY(hipSetDevice(e->cfg.device));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  if (const int rf = vadm_flush(e, true)) return rf;
   HIP_TRY(hipStreamSynchronize(e->side));
   fvad::VadmState st;
   HIP_TRY(hipMemcpy(&st, e->vadm.st + (size_t)machine * e->cfg.n_streams + stream, sizeof(st),
@@ -1475,8 +1512,8 @@ extern "C" size_t fvad_engine_segments_range(fvad_engine *e, int stream, int mac
                                              fvad_segment *out, size_t cap) {
   if (!e || e->vadm.n == 0 || stream < 0 || stream >= e->cfg.n_streams || machine < 0 || machine >= e->vadm.n)
     return 0;
-  if (hipSetDevice(e->cfg.device) != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess ||
-      hipStreamSynchronize(e->side) != hipSuccess)
+  if (hipSetDevice(e->cfg.device) != hipSuccess || vadm_flush(e, true) != FVAD_OK ||
+      hipStreamSynchronize(e->stream) != hipSuccess || hipStreamSynchronize(e->side) != hipSuccess)
     return 0;
   const size_t idx = (size_t)machine * e->cfg.n_streams + stream;
   fvad::VadmState st;

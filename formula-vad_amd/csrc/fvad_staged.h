@@ -158,7 +158,9 @@ enum WaveKernel { kWaveFftA, kWavePspec, kWaveSynth, kWaveFftB, kWaveOlaFb };
 hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream);
 // Device VADMachines over the window outputs a.out_* of one push: overlap =
 // the light HBM variant meant to co-run with the next push on a side stream.
-hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream);
+// fast: k_vadm_par (a burst of 16 lanes per stream, for a GPU with nothing
+// else queued) where it applies, else k_vadm_hbm (32 waves, overlaps quietly)
+hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream, bool fast = false);
 // use_denoiser = 0 (VAD.zig:206-212,239-249): k_ndring, k_ndmeta, FFT B
 hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream);
 // k_fftb's scratch need: 0 when a transform fits in LDS, else float2 per workgroup

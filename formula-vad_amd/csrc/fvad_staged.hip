@@ -36,6 +36,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "fvad_device.h"
@@ -1622,12 +1623,12 @@ __device__ __forceinline__ double ra_push(float *buf, int B, int n, unsigned &wi
 #ifndef FVAD_LT_BLOCK
 #define FVAD_LT_BLOCK 16
 #endif
+template <int kL = FVAD_LT_BLOCK>
 __device__ __forceinline__ double lt_sum(double acc, const float *buf, size_t bs, unsigned i0, unsigned i1,
                                          double scalar) {
   // blocks of kL entries, the next block's loads issued before this block's
   // adds (two blocks in flight: the chain waits a memory latency per kL
   // entries at most, not per block of its own)
-  constexpr int kL = FVAD_LT_BLOCK;
   unsigned i = i0;
   if (i + kL <= i1) {
     float cur[kL];
@@ -1653,10 +1654,11 @@ __device__ __forceinline__ double lt_sum_init(double acc, double term, unsigned 
   for (unsigned i = 0; i < n; i++) acc += term;
   return acc;
 }
+template <int kL = FVAD_LT_BLOCK>
 __device__ __forceinline__ double lt_range(double acc, const float *buf, size_t bs, unsigned p, unsigned q,
                                            unsigned nw, double init, double scalar) {
   const unsigned mid = min(max(nw, p), q);  // [p, mid) written, [mid, q) initial
-  acc = lt_sum(acc, buf, bs, p, mid, scalar);
+  acc = lt_sum<kL>(acc, buf, bs, p, mid, scalar);
   return lt_sum_init(acc, init * scalar, q - mid);
 }
 
@@ -1695,13 +1697,93 @@ __device__ __forceinline__ double ra_push_long(float *buf, size_t bs, int n, uns
   return acc;
 }
 
+// VADMachine.run's per-window steps (VADMachine.zig:126-230), shared by the
+// serial walk (vadm_stream) and the window-parallel kernel (k_vadm_par).
+enum { kVmClosed = 0, kVmOpening = 1, kVmOpen = 2, kVmClosing = 3 };
+// short-term and channel-ratio averages (pushed every window); `met`: the
+// speech condition against the long-term average of the last long push
+__device__ __forceinline__ bool vadm_short(VadmState &S, const VadmConst &K, float *st, float *rb, int B, float min_v,
+                                           float vr) {
+  const double st_avg = ra_push(st, B, K.n_st, S.st_widx, S.st_count, S.st_last, S.st_has, min_v);
+  const double r_avg = ra_push(rb, B, K.n_r, S.r_widx, S.r_count, S.r_last, S.r_has, vr);
+  double base;
+  if (S.lt_has)
+    base = S.lt_last;
+  else if (K.has_init)
+    base = K.init;
+  else
+    base = st_avg;
+  const double threshold = base * (double)K.thr_factor;
+  return st_avg > threshold && r_avg > (double)K.ratio_thr;
+}
+// the speech-state transition, segment output and tracking of one window
+__device__ __forceinline__ void vadm_fsm(VadmState &S, const VadmConst &K, unsigned long long index, bool met,
+                                         float vad, float vr, VadmSeg *seg, int seg_cap) {
+  const int from = S.state;
+  bool ended = false;
+  switch (from) {
+    case kVmClosed:
+      if (met) {
+        S.state = kVmOpening;
+        S.speech_start = index;
+      }
+      break;
+    case kVmOpening:
+      if (met && index - S.speech_start >= K.min_open)
+        S.state = kVmOpen;
+      else if (!met)
+        S.state = kVmClosed;
+      break;
+    case kVmOpen:
+      if (!met) {
+        S.state = kVmClosing;
+        S.speech_end = index;
+      }
+      break;
+    default:  // kVmClosing
+      if (met) {
+        S.state = kVmOpen;
+      } else if (index - S.speech_end >= K.max_gap) {
+        S.state = kVmClosed;
+        ended = true;
+      }
+      break;
+  }
+  if (ended) {  // onSpeechEnd (before the tracking update of this window, as in VADMachine.zig)
+    const unsigned long long len = S.speech_end - S.speech_start;
+    const float len_rt = (float)len / K.sr;
+    if (len_rt >= K.min_dur) {
+      if (S.n_segs < (unsigned)seg_cap) {
+        VadmSeg g;
+        g.sample_from = K.rec_pad > S.speech_start ? 0ull : S.speech_start - K.rec_pad;
+        g.sample_to = S.speech_end + K.rec_pad;
+        g.debug_rnn_vad = S.rnn_vad / (float)S.rnn_vad_count;
+        g.debug_avg_speech_vol_ratio = S.vol_ratio / (float)S.vol_ratio_count;
+        seg[S.n_segs] = g;
+      }
+      S.n_segs++;
+    }
+  }
+  // track(vad, vr, from, to)
+  if (from == kVmClosed && S.state == kVmOpening) {
+    S.rnn_vad = vad;
+    S.rnn_vad_count = 1;
+    S.vol_ratio = vr;
+    S.vol_ratio_count = 1;
+  } else if (from == kVmOpening || from == kVmOpen) {
+    S.rnn_vad += vad;
+    S.rnn_vad_count += 1;
+    S.vol_ratio += vr;
+    S.vol_ratio_count += 1;
+  }
+}
+
 // One machine over all completed windows of the push for one stream; `lt`
 // points at entry 0 of the stream's long-term buffer, `lts` is its stride.
 __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t lts) {
   const int B = a.n_streams, C = a.n_channels, nb = a.n_bands;
   const int nt = ticks_of(a, s);
   const unsigned long long fft = (unsigned long long)a.plan->nfft_b;
-  enum { kClosed = 0, kOpening = 1, kOpen = 2, kClosing = 3 };
   const VadmConst &K = a.vadm.c[m];
   VadmState S = a.vadm.st[(size_t)m * B + s];
   float *st = a.vadm.buf + K.st_off + s, *rb = a.vadm.buf + K.r_off + s;
@@ -1710,90 +1792,223 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
   // when fft_size < 480)
   for (int t = 0; t < nt; t++)
     for (int w = 0, nw = a.out_win_flag[(size_t)t * B + s]; w < nw; w++) {
-    const size_t o = ((size_t)t * B + s) * a.wpt + w;
-    const unsigned long long index = S.windows_done * fft;
-    S.windows_done++;
-    float min_v = 999, max_v = 0;
-    for (int c = 0; c < C; c++) {
-      const float v = a.out_band[(o * C + c) * nb + K.slot];
-      if (v < min_v) min_v = v;
-      if (v > max_v) max_v = v;
+      const size_t o = ((size_t)t * B + s) * a.wpt + w;
+      const unsigned long long index = S.windows_done * fft;
+      S.windows_done++;
+      float min_v = 999, max_v = 0;
+      for (int c = 0; c < C; c++) {
+        const float v = a.out_band[(o * C + c) * nb + K.slot];
+        if (v < min_v) min_v = v;
+        if (v > max_v) max_v = v;
+      }
+      // fft_input.vad orelse 0 (VADMachine.zig:240-246): no vad without the denoiser
+      const float vad = a.use_denoiser ? a.out_win_vad[o] : 0.0f, vr = a.out_win_ratio[o];
+      const bool met = vadm_short(S, K, st, rb, B, min_v, vr);
+      if (!met)
+        ra_push_long(lt, lts, K.n_lt, S.lt_widx, S.lt_count, S.lt_nw, K.init, S.lt_last, S.lt_has, S.lt_pre,
+                     S.lt_pre_ok, min_v);
+      vadm_fsm(S, K, index, met, vad, vr, seg, a.vadm.seg_cap);
     }
-    // fft_input.vad orelse 0 (VADMachine.zig:240-246): no vad without the denoiser
-    const float vad = a.use_denoiser ? a.out_win_vad[o] : 0.0f, vr = a.out_win_ratio[o];
-    const double st_avg = ra_push(st, B, K.n_st, S.st_widx, S.st_count, S.st_last, S.st_has, min_v);
-    const double r_avg = ra_push(rb, B, K.n_r, S.r_widx, S.r_count, S.r_last, S.r_has, vr);
-    double base;
-    if (S.lt_has)
-      base = S.lt_last;
-    else if (K.has_init)
-      base = K.init;
-    else
-      base = st_avg;
-    const double threshold = base * (double)K.thr_factor;
-    const bool met = st_avg > threshold && r_avg > (double)K.ratio_thr;
-    if (!met)
-      ra_push_long(lt, lts, K.n_lt, S.lt_widx, S.lt_count, S.lt_nw, K.init, S.lt_last, S.lt_has, S.lt_pre,
-                   S.lt_pre_ok, min_v);
-    const int from = S.state;
-    bool ended = false;
-    switch (from) {
-      case kClosed:
-        if (met) {
-          S.state = kOpening;
-          S.speech_start = index;
+  a.vadm.st[(size_t)m * B + s] = S;
+}
+
+// ---------------------------------------------------------------------------
+// k_vadm_par: the same machine with the long-term averages of a push's
+// windows computed side by side.  Once the long-term buffer is full (from
+// the start with an initial average) a push at write index w averages
+//   acc = P_w + v * s, then acc += e_i * s for i = w + 1 .. n - 1 (C order),
+// P_w the cached prefix, a chain of one add per push; the suffix entries are
+// the old buffer's, or values pushed earlier in this push (a wrap).  So given
+// which windows push, the ~12 averages of a push are independent serial
+// chains.  Whether a window pushes (`met` false) depends on the average of the
+// last push, so 16 lanes per stream fold the hypothesis "the next 16 windows
+// all push" in one round; the stream's leader lane then replays the windows
+// in order with the exact averages -- each `met` decided exactly as the
+// serial walk does -- and commits every push up to the first window that
+// does not push (speech); the next round starts after it.  A round costs one
+// suffix chain instead of one per window; windows with no push cost none.
+// Bit-identical to vadm_stream (same adds, same order); streams whose buffer
+// is not full yet (no initial average) or with more than kVpMaxW windows in
+// the push take the serial walk.
+// ---------------------------------------------------------------------------
+// (48 windows: 4.2 KB of LDS, which fits beside three k_fftAw or four
+// k_pcorr workgroups on a CU; the machine state lives in LDS, not in VGPRs)
+#ifndef FVAD_VP_BLOCK
+#define FVAD_VP_BLOCK 8  // long-term entries per prefetched block
+#endif
+constexpr int kVpG = 16, kVpS = 4, kVpMaxW = 48;  // lanes per stream, streams per workgroup, windows per push
+// acc += e_i * s over old entries [i0, i1): pushed f32 below nw, the initial
+// average above (entry i of the stream at lt[i * lts])
+__device__ __forceinline__ double lt_fold(double acc, const float *lt, size_t lts, unsigned i0, unsigned i1, unsigned nw,
+                                          double init, double scalar) {
+  if (i0 >= i1) return acc;
+  return lt_range<FVAD_VP_BLOCK>(acc, lt, lts, i0, i1, nw, init, scalar);
+}
+__global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
+  __shared__ float wmin[kVpS][kVpMaxW], wvad[kVpS][kVpMaxW], wvr[kVpS][kVpMaxW];
+  __shared__ float pv[kVpS][kVpMaxW];  // values pushed in this push, in push order (committed + the round's hypotheses)
+  __shared__ double favg[kVpS][kVpG];
+  __shared__ double rpre[kVpS];  // the cached prefix before the round's first push
+  __shared__ int rnd[kVpS][4];  // round: first window, pushes committed so far, state (0 run, 1 done, 2 serial)
+  __shared__ VadmState Ss[kVpS];
+  const int B = a.n_streams, C = a.n_channels, nb = a.n_bands;
+  const int g = threadIdx.x / kVpG, r = threadIdx.x % kVpG;
+  const int s = blockIdx.x * kVpS + g;
+  const bool sok = s < B && ticks_of(a, s) > 0;
+  const int nt = sok ? ticks_of(a, s) : 0;
+  const unsigned long long fft = (unsigned long long)a.plan->nfft_b;
+  const int self = threadIdx.x;
+  for (int m = 0; m < a.vadm.n; m++) {
+    const VadmConst &K = a.vadm.c[m];
+    float *lt = a.vadm.buf + K.lt_off + (sok ? s : 0);
+    const size_t lts = (size_t)B;
+    // the push's windows in order -> LDS (16 ticks at a time, positions by a
+    // prefix count over the group's lanes)
+    int Kw = 0;
+    for (int t0 = 0; t0 < nt; t0 += kVpG) {
+      const int t = t0 + r;
+      const int nwt = t < nt ? a.out_win_flag[(size_t)t * B + s] : 0;
+      int pos = nwt;
+#pragma unroll
+      for (int d = 1; d < kVpG; d <<= 1) {
+        const int up = __shfl(pos, self - d);
+        if (r >= d) pos += up;
+      }
+      const int tot = __shfl(pos, g * kVpG + kVpG - 1);
+      for (int w = 0; w < nwt; w++) {
+        const int k = Kw + pos - nwt + w;
+        if (k < kVpMaxW) {
+          const size_t o = ((size_t)t * B + s) * a.wpt + w;
+          float min_v = 999;
+          for (int c = 0; c < C; c++) {
+            const float v = a.out_band[(o * C + c) * nb + K.slot];
+            if (v < min_v) min_v = v;
+          }
+          wmin[g][k] = min_v;
+          wvad[g][k] = a.use_denoiser ? a.out_win_vad[o] : 0.0f;
+          wvr[g][k] = a.out_win_ratio[o];
         }
-        break;
-      case kOpening:
-        if (met && index - S.speech_start >= K.min_open)
-          S.state = kOpen;
-        else if (!met)
-          S.state = kClosed;
-        break;
-      case kOpen:
-        if (!met) {
-          S.state = kClosing;
-          S.speech_end = index;
-        }
-        break;
-      default:  // kClosing
-        if (met) {
-          S.state = kOpen;
-        } else if (index - S.speech_end >= K.max_gap) {
-          S.state = kClosed;
-          ended = true;
-        }
-        break;
+      }
+      Kw += tot;
     }
-    if (ended) {  // onSpeechEnd (before the tracking update of this window, as in VADMachine.zig)
-      const unsigned long long len = S.speech_end - S.speech_start;
-      const float len_rt = (float)len / K.sr;
-      if (len_rt >= K.min_dur) {
-        if (S.n_segs < (unsigned)a.vadm.seg_cap) {
-          VadmSeg g;
-          g.sample_from = K.rec_pad > S.speech_start ? 0ull : S.speech_start - K.rec_pad;
-          g.sample_to = S.speech_end + K.rec_pad;
-          g.debug_rnn_vad = S.rnn_vad / (float)S.rnn_vad_count;
-          g.debug_avg_speech_vol_ratio = S.vol_ratio / (float)S.vol_ratio_count;
-          seg[S.n_segs] = g;
+    if (r == 0) Ss[g] = a.vadm.st[(size_t)m * B + (sok ? s : 0)];
+    wave_sync();
+    VadmState &S = Ss[g];
+    float *st = a.vadm.buf + K.st_off + (sok ? s : 0), *rb = a.vadm.buf + K.r_off + (sok ? s : 0);
+    VadmSeg *seg = a.vadm.seg + ((size_t)m * B + (sok ? s : 0)) * a.vadm.seg_cap;
+    // (n > kVpMaxW: a push wraps around the buffer at most once)
+    const bool fast = sok && Kw <= kVpMaxW && K.n_lt > kVpMaxW && S.lt_count == (unsigned)K.n_lt && S.lt_pre_ok;
+    const unsigned n = (unsigned)K.n_lt, wbase = S.lt_widx, nw0 = S.lt_nw;
+    const double scalar = 1.0 / (double)n;  // the full buffer's
+    if (r == 0) {
+      rnd[g][0] = 0;
+      rnd[g][1] = 0;
+      rnd[g][2] = !sok ? 1 : (fast ? 0 : 2);
+    }
+    wave_sync();
+    // leader state across rounds (lane 0 of the group)
+    int j = 0, npush = 0;
+    double pre = S.lt_pre;
+    bool pending = false;  // window j's short pushes done, it pushes (met false)
+    for (;;) {
+      if (r == 0 && rnd[g][2] == 0) {
+        // windows that do not push need no fold: replay them up to the next
+        // one that does (its short-term pushes done, its long push pending)
+        while (j < Kw) {
+          const unsigned long long index = S.windows_done * fft;
+          const bool met = vadm_short(S, K, st, rb, B, wmin[g][j], wvr[g][j]);
+          if (!met) {
+            pending = true;
+            break;
+          }
+          S.windows_done++;
+          vadm_fsm(S, K, index, met, wvad[g][j], wvr[g][j], seg, a.vadm.seg_cap);
+          j++;
         }
-        S.n_segs++;
+        if (j >= Kw) rnd[g][2] = 1;
+        rnd[g][0] = j;
+        rnd[g][1] = npush;
+        // the round's hypotheses: windows j, j + 1, ... push in order
+        for (int q = 0; q < kVpG && j + q < Kw; q++) pv[g][npush + q] = wmin[g][j + q];
+        rpre[g] = pre;
+      }
+      wave_sync();
+      const int state = rnd[g][2];
+      if (__ballot(state == 0) == 0) break;  // every group of the wave is done with its fast walk
+      if (state == 0) {
+        // lane r: the push of window j0 + r after the r pushes before it
+        const int j0 = rnd[g][0], np = rnd[g][1];
+        if (j0 + r < Kw) {
+          const unsigned k = (unsigned)(np + r);  // pushes of this push before it
+          const unsigned nw = min(n, nw0 + k + 1);
+          // its prefix P_w: the chain of one add per push since the cached
+          // one; w: its write index
+          double P = rpre[g];
+          unsigned w = (wbase + (unsigned)np) % n;
+#pragma unroll 1
+          for (int q = 0; q < r; q++) {
+            P = (w + 1 == n) ? 0.0 : P + (double)pv[g][np + q] * scalar;
+            w = (w + 1 == n) ? 0u : w + 1;
+          }
+          double acc = P + (double)pv[g][np + r] * scalar;
+          if (wbase + k < n) {
+            // no wrap in this push: every entry past w is the old buffer's
+            acc = lt_fold(acc, lt, lts, w + 1, n, nw, K.init, scalar);
+          } else {
+            // wrapped: (w, wbase) old entries (all pushed by now), [wbase, n) pushed in this push
+            acc = lt_fold(acc, lt, lts, w + 1, wbase, nw, K.init, scalar);
+            for (unsigned i = wbase; i < n; i++) acc += (double)pv[g][i - wbase] * scalar;
+          }
+          favg[g][r] = acc;
+        }
+      }
+      wave_sync();
+      if (r == 0 && state == 0) {
+        // replay in order with the exact averages; commit up to the first
+        // window that does not push
+        const int j0 = j;
+        for (int q = 0; q < kVpG && j0 + q < Kw; q++) {
+          const int jj = j0 + q;
+          const unsigned long long index = S.windows_done * fft;
+          bool met = false;
+          if (q > 0) met = vadm_short(S, K, st, rb, B, wmin[g][jj], wvr[g][jj]);
+          if (!met) {
+            // the long push (ra_push_long's state updates, the average folded above)
+            const unsigned w = S.lt_widx;
+            S.lt_widx = (w + 1) % n;
+            if (S.lt_nw < n) S.lt_nw++;
+            pre = (w + 1 == n) ? 0.0 : pre + (double)wmin[g][jj] * scalar;
+            S.lt_pre = pre;
+            S.lt_last = favg[g][q];
+            S.lt_has = 1;
+            npush++;
+          }
+          S.windows_done++;
+          vadm_fsm(S, K, index, met, wvad[g][jj], wvr[g][jj], seg, a.vadm.seg_cap);
+          j = jj + 1;
+          if (met) break;
+        }
+        pending = false;
+      }
+      wave_sync();
+    }
+    (void)pending;
+    if (r == 0 && sok) {
+      if (rnd[g][2] == 2) {
+        a.vadm.st[(size_t)m * B + s].pad = 1;  // not this kernel's case (launch_vadm checks): flagged, untouched
+      } else {
+        // the push's long-term values into the buffer (read above as the old entries)
+        unsigned w = wbase;
+#pragma unroll 1
+        for (int q = 0; q < npush; q++) {
+          lt[(size_t)w * lts] = pv[g][q];
+          w = (w + 1 == n) ? 0u : w + 1;
+        }
+        a.vadm.st[(size_t)m * B + s] = S;
       }
     }
-    // track(vad, vr, from, to)
-    if (from == kClosed && S.state == kOpening) {
-      S.rnn_vad = vad;
-      S.rnn_vad_count = 1;
-      S.vol_ratio = vr;
-      S.vol_ratio_count = 1;
-    } else if (from == kOpening || from == kOpen) {
-      S.rnn_vad += vad;
-      S.rnn_vad_count += 1;
-      S.vol_ratio += vr;
-      S.vol_ratio_count += 1;
-    }
+    wave_sync();
   }
-  a.vadm.st[(size_t)m * B + s] = S;
 }
 
 // ---------------------------------------------------------------------------
@@ -2110,10 +2325,18 @@ hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream) {
   return launch_fftb(a, n_cu, stream);
 }
 
-hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream) {
+hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream, bool fast) {
   (void)hipGetLastError();
-  FVAD_KERNEL_TRY(k_vadm_hbm, dim3((a.n_streams + kVadmHbmLanes - 1) / kVadmHbmLanes), dim3(kVadmHbmLanes), 0, stream,
-                  a);
+  // k_vadm_par's case: every machine's long-term buffer full from the start
+  // (an initial average) and longer than a push's windows, at most kVpMaxW
+  // windows per push (wmax bounds them)
+  bool par = fast && a.wmax <= kVpMaxW;
+  for (int m = 0; m < a.vadm.n; m++) par = par && a.vadm.c[m].has_init && a.vadm.c[m].n_lt > kVpMaxW;
+  if (!par)
+    FVAD_KERNEL_TRY(k_vadm_hbm, dim3((a.n_streams + kVadmHbmLanes - 1) / kVadmHbmLanes), dim3(kVadmHbmLanes), 0,
+                    stream, a);
+  else
+    FVAD_KERNEL_TRY(k_vadm_par, dim3((a.n_streams + kVpS - 1) / kVpS), dim3(kVpS * kVpG), 0, stream, a);
   return hipSuccess;
 }
 

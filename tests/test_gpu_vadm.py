@@ -2,7 +2,10 @@
 host restatement (fvad_vadm_*, itself checked against the oracle in
 test_host_cpu.py) fed the same engine outputs: segments and their debug
 averages must be identical, for the default and an alternative config, over
-ragged pushes of several streams."""
+ragged pushes of several streams.  Machines that all start from an initial
+long-term average run on k_vadm_par (the push's long-term averages folded
+side by side); an alternative machine without one sends the push through the
+serial k_vadm_hbm walk."""
 import numpy as np
 import pytest
 
@@ -24,11 +27,14 @@ def host_segments(fvad_mod, outs, cfg, C, slot, stream):
     return vm.segments()
 
 
-def test_device_vadm_matches_host(fvad_mod):
+@pytest.mark.parametrize("alt_init", [True, False])
+def test_device_vadm_matches_host(fvad_mod, alt_init):
     m = fvad_mod.Model(seed=1)
     alt = fvad_mod.VadmConfig.default()
     alt.speech_min_freq, alt.speech_max_freq = 300.0, 3000.0
     alt.min_vad_duration_sec = 0.3
+    if not alt_init:
+        alt.has_initial_long_term_avg = 0
     ids, secs = [0, 4, 19, 42, 7], [70.0, 55.5, 40.0, 66.0, 12.0]
     streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip(ids, secs)]
     eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=64, bands=((4, 64), (13, 128)))
