@@ -663,6 +663,20 @@ int launch_fused(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
 
 }  // namespace
 
+// a cross-stream wait; FVAD_WAIT_SKIP=1 skips it when the event has already
+// completed (the host usually runs a push or more ahead, so the main
+// stream's waits on the push k - 2 VADMachine and the buffer releases are
+// often long satisfied; each queued wait is a barrier packet at the push
+// boundary)
+hipError_t wait_event(hipStream_t stream, hipEvent_t ev) {
+  static const bool skip = [] {
+    const char *v = getenv("FVAD_WAIT_SKIP");
+    return v && atoi(v) == 1;
+  }();
+  if (skip && hipEventQuery(ev) == hipSuccess) return hipSuccess;
+  return hipStreamWaitEvent(stream, ev, 0);
+}
+
 // k_vadm of one push on the side stream (its waits already queued), with
 // its timing pair and the events later pushes wait for
 int enqueue_vadm(fvad_engine *e, const fvad::StagedArgs &v, int b, bool timed, bool fast) {
@@ -688,7 +702,9 @@ int enqueue_vadm(fvad_engine *e, const fvad::StagedArgs &v, int b, bool timed, b
 int vadm_flush(fvad_engine *e, bool fast = true) {
   if (!e->vpend) return FVAD_OK;
   e->vpend = false;
-  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_copy, 0));
+  // the push's end: ev_buf_free of its parity (recorded after its kernels and
+  // ticks copy; re-recorded only by the push after next)
+  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_buf_free[e->vpend_b], 0));
   return enqueue_vadm(e, e->vpend_args, e->vpend_b, e->vpend_timed, fast);
 }
 
@@ -702,13 +718,13 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   a.n_ticks = n_ticks;
   a.V = e->V;
   a.L = e->L;
-  // the previous push's VADMachine (ev_copy still marks that push's end)
+  // the previous push's VADMachine (after that push's ev_buf_free)
   if (e->vpend)
     if (const int rf = vadm_flush(e, false)) return rf;
   // push k uses buffer b = k & 1 of xs / ratio / ticks; its k_prep3 waits
   // (on pstream) until push k-2 released b, then runs beside push k-1
   const int b = e->next_buf;
-  if (e->buf_busy[b]) HIP_TRY(hipStreamWaitEvent(e->pstream, e->ev_buf_free[b], 0));
+  if (e->buf_busy[b]) HIP_TRY(wait_event(e->pstream, e->ev_buf_free[b]));
   e->d_xs = e->d_xs_b[b];
   e->d_ratio = e->d_ratio_b[b];
   e->d_ticks = e->d_ticks_b[b];
@@ -792,9 +808,9 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   if (c.use_denoiser) {
     HIP_TRY(fvad::launch_prep(a, e->pstream, timed ? e->ev : nullptr));
     HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
-    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
+    HIP_TRY(wait_event(e->stream, e->ev_prep_done[b]));
     // window output set b is free once push k-2's k_vadm_hbm has read it
-    if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
+    if (e->vadm.n > 0) HIP_TRY(wait_event(e->stream, e->ev_vadm_b[b]));
     fvad::Overlap ov{e->gstream, e->sstream, e->ev_ov[0], e->ev_ov[1], e->ev_ov[2], e->n_cu_b,
                      sizeof(unsigned) * (1 + (size_t)(c.n_streams + 15) / 16)};
     HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr, e->overlap ? &ov : nullptr));
@@ -802,8 +818,8 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     // no denoiser: raw input frames to the ring, windows, FFT B, all on the
     // engine stream after the input copy (queued on the prep stream)
     HIP_TRY(hipEventRecord(e->ev_prep_done[b], e->pstream));
-    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_prep_done[b], 0));
-    if (e->vadm.n > 0) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_vadm_b[b], 0));
+    HIP_TRY(wait_event(e->stream, e->ev_prep_done[b]));
+    if (e->vadm.n > 0) HIP_TRY(wait_event(e->stream, e->ev_vadm_b[b]));
     HIP_TRY(fvad::launch_nodenoise(a, e->grid_frames, e->stream));
   }
   if (e->vadm.n > 0) {
@@ -811,7 +827,6 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     // VADMachine has read it (ev_vadm_b[b], waited for above)
     if (use_ticks)
       HIP_TRY(hipMemcpyAsync(e->d_vticks_b[b], e->d_ticks, (size_t)c.n_streams * 4, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipEventRecord(e->ev_copy, e->stream));
     fvad::StagedArgs v = a;
     v.ticks_valid = use_ticks ? e->d_vticks_b[b] : nullptr;
     e->vpend = true;

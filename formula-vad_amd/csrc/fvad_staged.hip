@@ -1004,6 +1004,16 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 #ifndef FVAD_GVPRE
 #define FVAD_GVPRE 1
 #endif
+// FVAD_FD4: the denoise GRU one step further behind (frame t-4 at step t), so
+// the denoise candidates' whole input prefix (b + the 114 input terms) runs in
+// the P2 before its step, beside the lighter candidate roles, and the denoise
+// z|r gates' first segment moves to P1's freed waves (zpre double-buffered)
+#ifndef FVAD_FD4
+#define FVAD_FD4 0
+#endif
+#if FVAD_FD4 && !FVAD_GVPRE
+#error "FVAD_FD4 needs FVAD_GVPRE"
+#endif
 constexpr int kR3S = 8, kR3G = 2, kR3NT = 1024;
 __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   constexpr int S = kR3S, G = kR3G, NT = kR3NT;
@@ -1015,7 +1025,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     alignas(16) float gdT[2][96 * S];
     alignas(16) float zrv[48 * S], zrn[96 * S], zrd[192 * S];
     alignas(16) float dhp[2][96 * S];  // denoise candidate input prefixes of frame f in slot f & 1
-    alignas(16) float zpre[192 * S];   // denoise z|r: b + the vad-state segment (P2 -> next P1)
+    alignas(16) float zpre[2][192 * S];  // denoise z|r: b + the vad-state segment of frame f in slot f & 1
     alignas(16) float gout[2][22 * S];  // denoise_output of frame f in slot f & 1
     alignas(16) float vo[S];  // vad_output of the frame P2 computed last
     float tt[204];
@@ -1216,13 +1226,13 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       a.gs[f * kBands + i] = gsm;
     }
   };
-  for (int t = 0; t <= maxnf + 4; t++) {
+  for (int t = 0; t <= maxnf + 4 + FVAD_FD4; t++) {
     // per-step opaque thread id: the roles' per-thread offsets are recomputed
     // each step instead of hoisted out of the frame loop, where they spilled
     // (128 VGPRs + 34 spilled -> 112, no scratch: 1.27 -> 1.23-1.24 ms)
     int tq = tid;
     asm volatile("" : "+v"(tq));
-    const int fv = t - 1, fn = t - 2, fd = t - 3;
+    const int fv = t - 1, fn = t - 2, fd = t - 3 - FVAD_FD4;
     ROLE_BEGIN();
     // frame t+1's raw features, staged at the end of P1 for P2's feat_c:
     // issued here, so no load is outstanding across a step boundary (a
@@ -1233,7 +1243,8 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     if (wv < 6) {
       if (fd >= 0 && fd < maxnf)
         rnn_gates<5, S, G, 0, FVAD_GVPRE ? 5 : 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]},
-                                                  L.gdT[(fd + 1) & 1], L.zrd, kActSigmoid, L.tt, tq, L.zpre);
+                                                  L.gdT[(fd + 1) & 1], L.zrd, kActSigmoid, L.tt, tq,
+                                                  L.zpre[FVAD_FD4 ? (fd & 1) : 0]);
     } else if (wv == 6 || wv == 7 || wv == 10) {
       if (fn >= 0 && fn < maxnf)
         rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
@@ -1242,13 +1253,23 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       if (fv >= 0 && fv < maxnf)
         rnn_gates<1, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, kActSigmoid,
                               L.tt, (wv == 14 ? 64 : 0) + ln);
-    } else if (wv == 12 || wv == 13 || wv == 15) {  // denoise candidate input prefixes of frame t-3
+    } else if (wv == 12 || wv == 13 || wv == 15) {
+#if FVAD_FD4
+      // denoise z|r first segment (b + the vad-state terms) of frame t-3,
+      // two tasks per lane, for the next step's P1
+      const int fz = t - 3;
+      if (fz >= 0 && fz < maxnf)
+        rnn_gates<5, S, G, 192, 3>(L.W, RnnIn{L.gvT[fz & 3], nullptr, nullptr}, nullptr, nullptr, kActSigmoid, L.tt,
+                                   (wv == 15 ? 128 : 64 * (wv - 12)) + ln, L.zpre[fz & 1]);
+#else
+      // denoise candidate input prefixes of frame t-3
       if (fd >= 0 && fd < maxnf)
         rnn_cand<6, S, G, 0, FVAD_GVPRE ? 4 : 1>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, nullptr,
                                                  nullptr, nullptr, nullptr, 0, nullptr,
                                                  (wv == 15 ? 128 : 64 * (wv - 12)) + ln, L.dhp[fd & 1]);
-    } else if (wv == 8 && ln < 48) {  // gain smoothing of frame t-5
-      gains(t - 5, ln, 48);
+#endif
+    } else if (wv == 8 && ln < 48) {  // gain smoothing of frame t-5 (t-6 with FVAD_FD4)
+      gains(t - 5 - FVAD_FD4, ln, 48);
     } else if (wv == 9 && ln < S) {  // spectral variability of frame t (features: P2 of step t-1)
       if (t < maxnf) feat_d(t, ln);
     } else if (wv == 8 && ln >= 48 && ln < 48 + S) {  // vad_output of frame t-3 (P2 of step t-1)
@@ -1261,7 +1282,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     RSTAMP(0);
     ROLE_BEGIN();
     // ---- P2
-    const int fo = t - 4;
+    const int fo = t - 4 - FVAD_FD4;
     if (wv < 3) {
       if (fd >= 0 && fd < maxnf)
         rnn_cand<6, S, G, 0, 2>(L.W, RnnIn{nullptr, nullptr, nullptr}, L.gdT[(fd + 1) & 1], L.zrd, L.gdT[fd & 1],
@@ -1292,14 +1313,25 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       // vad_output(t-2) -> L.vo, stored by the next step's P1
       if (fn >= 0 && fn < maxnf)
         rnn_gates<8, S, G, 0>(L.W, RnnIn{L.gvT[fn & 3], nullptr, nullptr}, nullptr, L.vo, ra[8], L.tt, ln);
-#if FVAD_GVPRE
+#if FVAD_FD4
+    } else if (tq >= kP2Feat && tq < kP2Feat + 192) {  // features of t+1 on waves 9..11
+      for (int idx = tq - kP2Feat; t + 1 < maxnf && idx < kFeatItems; idx += 192) feat_c(t + 1, idx);
+    } else if (wv >= 12 && wv <= 14) {
+      // denoise candidates of frame t-3: b + the 114 input terms (they do not
+      // need the reset gate), one task per lane, for the next step's P2
+      const int fz = t - 3;
+      if (fz >= 0 && fz < maxnf)
+        rnn_cand<6, S, G, 192, 1>(L.W, RnnIn{L.gvT[fz & 3], L.gnT[fz & 1], L.featT[fz & 7]}, nullptr, nullptr, nullptr,
+                                  nullptr, 0, nullptr, tq - 768, L.dhp[fz & 1]);
+    }
+#elif FVAD_GVPRE
     } else if (tq >= kP2Feat && tq < kP2Feat + 192) {  // features of t+1 on waves 9..11
       for (int idx = tq - kP2Feat; t + 1 < maxnf && idx < kFeatItems; idx += 192) feat_c(t + 1, idx);
     } else if (wv >= 12 && wv <= 14) {  // denoise z|r of frame t-2: b + the vad-state segment
       const int fz = t - 2;
       if (fz >= 0 && fz < maxnf)
         rnn_gates<5, S, G, 192, 3>(L.W, RnnIn{L.gvT[fz & 3], nullptr, nullptr}, nullptr, nullptr, kActSigmoid, L.tt,
-                                   tq - 768, L.zpre);
+                                   tq - 768, L.zpre[0]);
     } else if (wv == 15) {  // denoise candidates of frame t-2: b + the vad-state segment
       const int fz = t - 2;
       if (FVAD_PRIO & 128) __builtin_amdgcn_s_setprio(2);

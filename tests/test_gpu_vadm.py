@@ -5,7 +5,11 @@ averages must be identical, for the default and an alternative config, over
 ragged pushes of several streams.  Machines that all start from an initial
 long-term average run on k_vadm_par (the push's long-term averages folded
 side by side); an alternative machine without one sends the push through the
-serial k_vadm_hbm walk."""
+serial k_vadm_hbm walk; a 10 s long-term buffer (234 windows) wraps around
+several times within the streams (the wrap branch of k_vadm_par), with a
+sync point after every push so each push's machines take k_vadm_par (between
+pushes the engine runs k_vadm_hbm; a sync point flushes the last push as
+k_vadm_par)."""
 import numpy as np
 import pytest
 
@@ -27,12 +31,13 @@ def host_segments(fvad_mod, outs, cfg, C, slot, stream):
     return vm.segments()
 
 
-@pytest.mark.parametrize("alt_init", [True, False])
-def test_device_vadm_matches_host(fvad_mod, alt_init):
+@pytest.mark.parametrize("alt_init,alt_lt_sec", [(True, 180.0), (False, 180.0), (True, 10.0)])
+def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec):
     m = fvad_mod.Model(seed=1)
     alt = fvad_mod.VadmConfig.default()
     alt.speech_min_freq, alt.speech_max_freq = 300.0, 3000.0
     alt.min_vad_duration_sec = 0.3
+    alt.long_term_speech_avg_sec = alt_lt_sec
     if not alt_init:
         alt.has_initial_long_term_avg = 0
     ids, secs = [0, 4, 19, 42, 7], [70.0, 55.5, 40.0, 66.0, 12.0]
@@ -52,6 +57,8 @@ def test_device_vadm_matches_host(fvad_mod, alt_init):
             if v:
                 pcm[:v, s] = x[:, t0 * 480:(t0 + v) * 480].reshape(C, v, 480).transpose(1, 0, 2)
         outs.append((eng.push(pcm, ticks_valid=valid), valid))
+        if alt_lt_sec < 60:
+            eng.sync()  # a sync point per push: every push's machines run as k_vadm_par
     total = 0
     for s in range(B):
         for mi, (cfg, slot) in enumerate(((fvad_mod.VadmConfig.default(), 0), (alt, 1))):
