@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 set -o pipefail
-FVAD_LIB=formula-vad_amd/lib/var/libfvad_fd4.so FVAD_WAIT_SKIP=1 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
+FVAD_LIB=$PWD/formula-vad_amd/lib/var/libfvad_fd4.so FVAD_WAIT_SKIP=1 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
   --timeout 300 --timeout-method thread > gpurun_out/fd4_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/fd4_tests.log; exit 1; }
 tail -1 gpurun_out/fd4_tests.log
 timeout -k 10 700 bash tools/_r4_abenv.sh 3 base=FVAD_X=1 fd4=FVAD_LIB=formula-vad_amd/lib/var/libfvad_fd4.so skip=FVAD_WAIT_SKIP=1 \
