@@ -1943,7 +1943,6 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
     // leader state across rounds (lane 0 of the group)
     int j = 0, npush = 0;
     double pre = S.lt_pre;
-    bool pending = false;  // window j's short pushes done, it pushes (met false)
     for (;;) {
       if (r == 0 && rnd[g][2] == 0) {
         // windows that do not push need no fold: replay them up to the next
@@ -1951,10 +1950,7 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
         while (j < Kw) {
           const unsigned long long index = S.windows_done * fft;
           const bool met = vadm_short(S, K, st, rb, B, wmin[g][j], wvr[g][j]);
-          if (!met) {
-            pending = true;
-            break;
-          }
+          if (!met) break;  // window j pushes: its short-term pushes are done, its long push waits for the folds
           S.windows_done++;
           vadm_fsm(S, K, index, met, wvad[g][j], wvr[g][j], seg, a.vadm.seg_cap);
           j++;
@@ -2022,14 +2018,15 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
           j = jj + 1;
           if (met) break;
         }
-        pending = false;
       }
       wave_sync();
     }
-    (void)pending;
     if (r == 0 && sok) {
       if (rnd[g][2] == 2) {
-        a.vadm.st[(size_t)m * B + s].pad = 1;  // not this kernel's case (launch_vadm checks): flagged, untouched
+        // not this kernel's case: launch_vadm sends such machines to
+        // k_vadm_hbm (no initial average, or more windows than kVpMaxW);
+        // flagged in the state's spare word, the push's windows left unprocessed
+        a.vadm.st[(size_t)m * B + s].pad = 1;
       } else {
         // the push's long-term values into the buffer (read above as the old entries)
         unsigned w = wbase;
