@@ -65,6 +65,9 @@ static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
 #ifndef FVAD_Q1_B64
 #define FVAD_Q1_B64 0
 #endif
+#ifndef FVAD_DIAG_SKIP
+#define FVAD_DIAG_SKIP 0
+#endif
 #ifndef FVAD_Q5_COMPACT
 #define FVAD_Q5_COMPACT 1
 #endif
@@ -249,7 +252,9 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
 #endif
 #pragma unroll
         for (int r = 0; r < R; r++) win[r] = yld(r);
-        for (int jb = 0; jb < 240; jb += R) {
+        // (FVAD_DIAG_SKIP & 1: diagnostic builds without this phase's sums, for
+        // the per-phase LDS attribution of tools/_r4_ldsattr.sh; never the product)
+        for (int jb = 0; jb < ((FVAD_DIAG_SKIP & 1) ? 0 : 240); jb += R) {
 #pragma unroll
           for (int u = 0; u < R; u++) {
             const float xv = X[2 * (jb + u)];
@@ -433,10 +438,11 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         typedef float v2f __attribute__((ext_vector_type(2)));
         const v2f *xp = reinterpret_cast<const v2f *>(xf[fr] + (kPitchMax >> 1));
         float sum = 0.0f;
+        constexpr int kQ3N = (FVAD_DIAG_SKIP & 2) ? 0 : 240;
         if (!odd) {
           const v2f *yp = reinterpret_cast<const v2f *>(xf[fr] + i);
 #pragma unroll 8
-          for (int j = 0; j < 240; j++) {
+          for (int j = 0; j < kQ3N; j++) {
             const v2f xv = xp[j], yv = yp[j];
             sum = sum + xv.x * yv.x;
             sum = sum + xv.y * yv.y;
@@ -446,7 +452,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
           const v2f *yp = reinterpret_cast<const v2f *>(xf[fr] + i - 1);
           v2f prev = yp[0];
 #pragma unroll 8
-          for (int j = 0; j < 240; j++) {
+          for (int j = 0; j < kQ3N; j++) {
             const v2f xv = xp[j], nx = yp[j + 1];
             sum = sum + xv.x * prev.y;
             sum = sum + xv.y * nx.x;
@@ -572,7 +578,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         int oB = (int)(reinterpret_cast<const char *>(Bq) - xb0);
         float aB = 0;
         FVAD_UNROLL(FVAD_Q5_UNROLL)
-        for (int i = 0; i < 240; i++) {
+        for (int i = 0; i < ((FVAD_DIAG_SKIP & 4) ? 0 : 240); i++) {
           const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
           const v2f rn = *reinterpret_cast<const v2f *>(xb0 + oB + 16);
           oX += 8;
@@ -594,7 +600,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         float w2 = ow ? q1.y : q1.x, w3 = ow ? qp.x : q1.y;
         int oW = (int)(reinterpret_cast<const char *>(W) - xb0);
         FVAD_UNROLL(FVAD_Q5_UNROLL)
-        for (int i = 0; i < 240; i++) {  // j = 2i, 2i + 1
+        for (int i = 0; i < ((FVAD_DIAG_SKIP & 4) ? 0 : 240); i++) {  // j = 2i, 2i + 1
           const v2f xp = *reinterpret_cast<const v2f *>(xb0 + oX);
           const v2f qn = *reinterpret_cast<const v2f *>(xb0 + oW + 24);
           oX += 8;
