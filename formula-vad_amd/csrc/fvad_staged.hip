@@ -83,9 +83,6 @@ constexpr int kPrepRing = FVAD_PREP_RING;  // float4 loads in flight per lane
 #ifndef FVAD_PREP_UNROLL
 #define FVAD_PREP_UNROLL 4
 #endif
-#ifndef FVAD_PREP_OMOD
-#define FVAD_PREP_OMOD 0  // the biquad's b0 x folded into its fma by the output modifier (A/B)
-#endif
 static_assert((kFrame / 4) % kPrepRing == 0, "prep ring must divide a frame");
 
 // One lane walks its stream's input in blocks of kPrepRing float4 chunks: per
@@ -116,19 +113,8 @@ __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, f
     const float xi = Scaled ? v * scalar : v;
     const float yi = xi + mem0;
     const double yd = (double)yi;
-#if FVAD_PREP_OMOD
-    // b0 = -2: fl(b0 x - a0 y) = 2 fl(-(a0 / 2) y - x) (scaling by 2 is exact
-    // and commutes with the rounding), one v_fma_f64 with the output
-    // modifier instead of a v_mul_f64 and the fma
-    const double xd = (double)xi;
-    double t;
-    asm("v_fma_f64 %0, %1, %2, -%3 mul:2" : "=v"(t) : "v"(yd), "s"(-(double)a0 * 0.5), "v"(xd));
-    mem0 = (float)((double)mem1 + t);
-    mem1 = (float)__builtin_fma(-(double)a1, yd, b1 * xd);
-#else
     mem0 = (float)((double)mem1 + __builtin_fma(-(double)a0, yd, b0 * (double)xi));
     mem1 = (float)__builtin_fma(-(double)a1, yd, b1 * (double)xi);
-#endif
     return yi;
   };
   // RMS volume (VAD.zig:253-272): sum of squares of the raw samples of each
