@@ -503,10 +503,11 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks):
         kernels[name] = {"ms": round(ms, 4), "tflops": round(c["flops"] * frames_launch / sec / 1e12, 3),
                          "gbs": round(c["bytes"] * frames_launch / sec / 1e9, 1),
                          "intensity": round(c["flops"] / c["bytes"], 2) if c["bytes"] else None}
-    # k_vadm_hbm (side stream, after the push) and k_prep3 (prep stream, beside
-    # the previous push) are overlapped with the main stream's kernels: timed
-    # and listed, but not candidates for the pipeline's bottleneck
-    side = ("k_vadm_hbm", "k_prep3")
+    # k_vadm_hbm (side stream, beside the next push), k_vadm_par (the last
+    # push's machine, at the final sync) and k_prep3 (prep stream, beside the
+    # previous push) run off the main stream: timed and listed, but not
+    # candidates for the pipeline's bottleneck
+    side = ("k_vadm_hbm", "k_vadm_par", "k_prep3")
     dom = max((n for n in kt["kernels"] if n not in side), key=lambda n: kt["kernels"][n])
     c = per_k[dom]
     dom_s = kt["kernels"][dom] / 1000.0

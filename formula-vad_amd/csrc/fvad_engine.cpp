@@ -104,10 +104,21 @@ struct fvad_engine {
   int vpend_b = 0;
   fvad::StagedArgs vpend_args{};
   float *d_vwratio = nullptr, *d_vwvad = nullptr, *d_vband = nullptr;
-  double vadm_ms_sum = 0;
-  int vadm_timed = 0;
+  // VADMachine timing, by kernel: [0] k_vadm_hbm (steady state), [1] k_vadm_par
+  // (a push flushed at a sync point); vadm_kind[slot]: the kernel a pending
+  // event pair brackets
+  double vadm_ms_sum[2] = {};
+  int vadm_timed[2] = {};
   bool vadm_pending[2] = {false, false};
+  int vadm_kind[2] = {};
   int vadm_slot = 0;
+  bool dbg_always_par = false;  // test hook FVAD_DEBUG_VADM_ALWAYS_PAR
+  // test hook (fvad_engine_output_log): the per-tick outputs of the next
+  // log_cap pushes, copied on the engine stream as each push ends
+  float *d_log = nullptr;
+  int log_cap = 0, log_n = 0;
+  size_t log_stride = 0;
+  std::vector<int> log_ticks;
   std::vector<fvad::VadmState> vadm_init;  // [m][stream] initial states
   size_t vadm_buf_len = 0;
   int rnn_act[fvad::rnnimg::kMats] = {};
@@ -325,7 +336,7 @@ void free_all(fvad_engine *e) {
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->d_gru16, e->d_gru16_bias, e->vadm.st, e->vadm.buf,
                   e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vticks_b[1], e->d_vwratio, e->d_vwvad, e->d_vband,
-                  e->d_fbtab, e->d_fbwork, e->d_gate};
+                  e->d_fbtab, e->d_fbwork, e->d_gate, e->d_log};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &set : e->evs)
@@ -371,7 +382,8 @@ extern "C" int fvad_engine_reset(fvad_engine *e) {
   if (e->cstream) HIP_TRY(hipStreamSynchronize(e->cstream));
   if (e->pstream) HIP_TRY(hipStreamSynchronize(e->pstream));
   if (e->vadm.n > 0) {
-    if (const int rf = vadm_flush(e, true)) return rf;
+    e->vpend = false;  // the pending push's machine state is wiped below: not run
+    HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->side));
     const int rc = vadm_reset(e);
     if (rc) return rc;
@@ -610,7 +622,7 @@ extern "C" void fvad_engine_destroy(fvad_engine *e) {
   (void)hipSetDevice(e->cfg.device);
   if (e->cstream) (void)hipStreamSynchronize(e->cstream);
   if (e->pstream) (void)hipStreamSynchronize(e->pstream);
-  if (e->side) (void)vadm_flush(e, true);
+  e->vpend = false;  // the last push's machine would only update state that is freed
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->side) (void)hipStreamSynchronize(e->side);
   free_all(e);
@@ -687,10 +699,12 @@ int enqueue_vadm(fvad_engine *e, const fvad::StagedArgs &v, int b, bool timed, b
     e->vadm_pending[slot] = false;  // an unread older sample in this slot is dropped
     HIP_TRY(hipEventRecord(e->ev_vt[slot][0], e->side));
   }
-  HIP_TRY(fvad::launch_vadm(v, e->side, fast));
+  bool par = false;
+  HIP_TRY(fvad::launch_vadm(v, e->side, fast || e->dbg_always_par, &par));
   if (timed) {
     HIP_TRY(hipEventRecord(e->ev_vt[slot][1], e->side));
     e->vadm_pending[slot] = true;
+    e->vadm_kind[slot] = par ? 1 : 0;
   }
   HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
   HIP_TRY(hipEventRecord(e->ev_vadm_b[b], e->side));
@@ -834,6 +848,17 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     e->vpend_b = b;
     e->vpend_timed = timed;
   }
+  if (e->log_n < e->log_cap) {  // test hook: this push's outputs into the log (read after a sync)
+    const size_t B = c.n_streams, TB = (size_t)n_ticks * B, TBW = TB * e->wpt, MT = (size_t)c.max_ticks * B,
+                 MW = MT * e->wpt;
+    float *L = e->d_log + e->log_stride * (size_t)e->log_n;
+    const void *src[6] = {e->d_vad, e->d_ratio, e->d_wflag, e->d_wratio, e->d_wvad, e->d_band};
+    const size_t off[6] = {0, MT, 2 * MT, 3 * MT, 3 * MT + MW, 3 * MT + 2 * MW};
+    const size_t n[6] = {TB, TB, TB, TBW, TBW, TBW * c.n_channels * c.n_bands};
+    for (int i = 0; i < 6; i++)
+      HIP_TRY(hipMemcpyAsync(L + off[i], src[i], n[i] * 4, hipMemcpyDeviceToDevice, e->stream));
+    e->log_ticks[e->log_n++] = n_ticks;
+  }
   // every reader of buffer b (incl. the copy of ticks for k_vadm_hbm) is queued
   HIP_TRY(hipEventRecord(e->ev_buf_free[b], e->stream));
   e->buf_busy[b] = true;
@@ -874,14 +899,14 @@ int collect_timing(fvad_engine *e) {
   return rc;
 }
 
-// k_vadm_hbm samples whose end event has completed (non-blocking)
+// VADMachine samples whose end event has completed (non-blocking), by kernel
 int collect_vadm_timing(fvad_engine *e) {
   for (int k = 0; k < 2; k++) {
     if (!e->vadm_pending[k] || hipEventQuery(e->ev_vt[k][1]) != hipSuccess) continue;
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, e->ev_vt[k][0], e->ev_vt[k][1]));
-    e->vadm_ms_sum += ms;
-    e->vadm_timed++;
+    e->vadm_ms_sum[e->vadm_kind[k]] += ms;
+    e->vadm_timed[e->vadm_kind[k]]++;
     e->vadm_pending[k] = false;
   }
   return FVAD_OK;
@@ -1353,10 +1378,12 @@ extern "C" int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_r
   if (rc) return rc;
   for (int i = 0; i < FVAD_MAX_TIMES; i++)
     ms_avg[i] = (e->n_timed && i <= e->n_kernels) ? e->ms_sum[i] / e->n_timed : 0.0;
-  // k_vadm_hbm (side stream, overlapped with the next push): reported after the
-  // pipeline kernels, not part of [0]
-  if (e->vadm.n > 0 && e->n_kernels + 1 < FVAD_MAX_TIMES)
-    ms_avg[e->n_kernels + 1] = e->vadm_timed ? e->vadm_ms_sum / e->vadm_timed : 0.0;
+  // the VADMachine (side stream, overlapped with the next push): reported after
+  // the pipeline kernels, not part of [0]; k_vadm_hbm (steady state) and
+  // k_vadm_par (the push flushed at a sync point) separately
+  for (int k = 0; k < 2; k++)
+    if (e->vadm.n > 0 && e->n_kernels + 1 + k < FVAD_MAX_TIMES)
+      ms_avg[e->n_kernels + 1 + k] = e->vadm_timed[k] ? e->vadm_ms_sum[k] / e->vadm_timed[k] : 0.0;
   if (n_runs) *n_runs = e->n_timed;
   return FVAD_OK;
 }
@@ -1366,8 +1393,10 @@ extern "C" int fvad_engine_clear_times(fvad_engine *e) {
   int rc = fvad_engine_sync(e);
   if (rc) return rc;
   for (double &v : e->ms_sum) v = 0;
-  e->vadm_ms_sum = 0;
-  e->vadm_timed = 0;
+  for (int k = 0; k < 2; k++) {
+    e->vadm_ms_sum[k] = 0;
+    e->vadm_timed[k] = 0;
+  }
   e->n_timed = 0;
   e->res_count = 0;
   return FVAD_OK;
@@ -1386,6 +1415,7 @@ extern "C" int fvad_engine_fp16_overlap(const fvad_engine *e) { return e ? (int)
 
 extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
   if (e && i == e->n_kernels && e->vadm.n > 0) return "k_vadm_hbm";
+  if (e && i == e->n_kernels + 1 && e->vadm.n > 0) return "k_vadm_par";
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
   if (e->cfg.mode == FVAD_MODE_FUSED) return i == 0 ? "k_prep" : "k_frame";
   if (e->cfg.mode == FVAD_MODE_FP16 && i == 6) return "k_gru16";
@@ -1548,4 +1578,122 @@ extern "C" size_t fvad_engine_segments_range(fvad_engine *e, int stream, int mac
     }
   }
   return st.n_segs;
+}
+
+// ---------------------------------------------------------------------------
+// Checker access: the whole device machine state and the test hooks
+// ---------------------------------------------------------------------------
+namespace {
+int vadm_read_state(fvad_engine *e, int stream, int machine, fvad::VadmState *st) {
+  if (!e || e->vadm.n == 0 || stream < 0 || stream >= e->cfg.n_streams || machine < 0 || machine >= e->vadm.n)
+    return fail(FVAD_EINVAL, "no such attached machine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  if (const int rc = fvad_engine_sync(e)) return rc;
+  HIP_TRY(hipMemcpy(st, e->vadm.st + (size_t)machine * e->cfg.n_streams + stream, sizeof(*st),
+                    hipMemcpyDeviceToHost));
+  return FVAD_OK;
+}
+}  // namespace
+
+extern "C" int fvad_engine_vadm_snapshot(fvad_engine *e, int stream, int machine, fvad_vadm_snapshot *out) {
+  if (!out) return fail(FVAD_EINVAL, "null argument");
+  fvad::VadmState st;
+  if (const int rc = vadm_read_state(e, stream, machine, &st)) return rc;
+  std::memset(out, 0, sizeof(*out));
+  out->speech_state = st.state;
+  out->speech_start = st.speech_start;
+  out->speech_end = st.speech_end;
+  out->windows = st.windows_done;
+  out->avg[0] = st.lt_last;
+  out->avg[1] = st.st_last;
+  out->avg[2] = st.r_last;
+  out->write_idx[0] = st.lt_widx;
+  out->write_idx[1] = st.st_widx;
+  out->write_idx[2] = st.r_widx;
+  out->written[0] = st.lt_count;
+  out->written[1] = st.st_count;
+  out->written[2] = st.r_count;
+  out->speech_rnn_vad = st.rnn_vad;
+  out->speech_vol_ratio = st.vol_ratio;
+  out->speech_rnn_vad_count = st.rnn_vad_count;
+  out->speech_vol_ratio_count = st.vol_ratio_count;
+  out->n_segments = st.n_segs;
+  return FVAD_OK;
+}
+
+extern "C" long fvad_engine_vadm_rolling(fvad_engine *e, int stream, int machine, int which, double *out, size_t cap) {
+  if (which < 0 || which > 2) return fail(FVAD_EINVAL, "which: 0 long-term, 1 short-term, 2 volume ratio");
+  fvad::VadmState st;
+  if (const int rc = vadm_read_state(e, stream, machine, &st)) return rc;
+  const fvad::VadmConst &K = e->vadm.c[machine];
+  const int n = which == 0 ? K.n_lt : which == 1 ? K.n_st : K.n_r;
+  const long long off = which == 0 ? K.lt_off : which == 1 ? K.st_off : K.r_off;
+  const size_t B = e->cfg.n_streams, k = std::min<size_t>((size_t)n, cap);
+  if (out && k) {
+    // entries are [i][stream]: one strided 2D copy of the stream's column
+    std::vector<float> col(k);
+    HIP_TRY(hipMemcpy2D(col.data(), sizeof(float), e->vadm.buf + off + stream, B * sizeof(float), sizeof(float), k,
+                        hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < k; i++)
+      // long-term entries never written since the machine started hold the
+      // initial average, a double (RollingAverage.zig:16-32; lt_nw counts the written)
+      out[i] = (which == 0 && K.has_init && i >= st.lt_nw) ? K.init : (double)col[i];
+  }
+  return n;
+}
+
+extern "C" int fvad_engine_set_debug(fvad_engine *e, int key, int value) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  switch (key) {
+    case FVAD_DEBUG_VADM_PAR_SERIAL_EVERY:
+      if (value < 0) return fail(FVAD_EINVAL, "value >= 0 required");
+      e->vadm.par_serial_every = value;
+      return FVAD_OK;
+    case FVAD_DEBUG_VADM_ALWAYS_PAR:
+      e->dbg_always_par = value != 0;
+      return FVAD_OK;
+    default:
+      return fail(FVAD_EINVAL, "unknown debug key");
+  }
+}
+
+extern "C" int fvad_engine_output_log(fvad_engine *e, int n_pushes) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  if (e->cfg.mode == FVAD_MODE_FUSED || !e->cfg.use_denoiser)
+    return fail(FVAD_EINVAL, "the output log records staged / fp16 engines with the denoiser");
+  if (n_pushes < 0) return fail(FVAD_EINVAL, "n_pushes >= 0 required");
+  if (const int rc = fvad_engine_sync(e)) return rc;
+  if (e->d_log) {
+    HIP_TRY(hipFree(e->d_log));
+    e->d_log = nullptr;
+  }
+  const fvad_engine_config &c = e->cfg;
+  const size_t MT = (size_t)c.max_ticks * c.n_streams, MW = MT * e->wpt;
+  e->log_stride = 3 * MT + 2 * MW + MW * c.n_channels * c.n_bands;
+  e->log_cap = e->log_n = 0;
+  e->log_ticks.assign((size_t)n_pushes, 0);
+  if (n_pushes > 0) {
+    if (const int rc = dalloc(&e->d_log, e->log_stride * (size_t)n_pushes)) return rc;
+    e->log_cap = n_pushes;
+  }
+  return FVAD_OK;
+}
+
+extern "C" int fvad_engine_output_log_read(fvad_engine *e, int push, fvad_outputs *out, int *n_ticks) {
+  if (!e) return fail(FVAD_EINVAL, "null engine");
+  if (push < 0 || push >= e->log_n) return fail(FVAD_EINVAL, "push not in the log");
+  if (const int rc = fvad_engine_sync(e)) return rc;
+  const fvad_engine_config &c = e->cfg;
+  const int T = e->log_ticks[push];
+  const size_t MT = (size_t)c.max_ticks * c.n_streams, MW = MT * e->wpt;
+  const size_t TB = (size_t)T * c.n_streams, TBW = TB * e->wpt;
+  const float *L = e->d_log + e->log_stride * (size_t)push;
+  if (n_ticks) *n_ticks = T;
+  if (!out) return FVAD_OK;
+  void *dst[6] = {out->vad, out->ratio, out->win_flag, out->win_ratio, out->win_vad, out->band};
+  const size_t off[6] = {0, MT, 2 * MT, 3 * MT, 3 * MT + MW, 3 * MT + 2 * MW};
+  const size_t n[6] = {TB, TB, TB, TBW, TBW, TBW * c.n_channels * c.n_bands};
+  for (int i = 0; i < 6; i++)
+    if (dst[i]) HIP_TRY(hipMemcpy(dst[i], L + off[i], n[i] * 4, hipMemcpyDeviceToHost));
+  return FVAD_OK;
 }

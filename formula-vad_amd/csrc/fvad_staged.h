@@ -57,6 +57,8 @@ struct VadmArgs {
   float *buf;     // rolling-average data (f32: each entry is a pushed f32)
   VadmSeg *seg;   // [m][stream][seg_cap]
   int seg_cap;
+  int par_serial_every;  // test hook (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY): k_vadm_par hands stream s to its
+                         //   in-kernel serial walk when s % par_serial_every == 0; 0 = never
 };
 
 struct StagedArgs {
@@ -159,8 +161,9 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
 // Device VADMachines over the window outputs a.out_* of one push: overlap =
 // the light HBM variant meant to co-run with the next push on a side stream.
 // fast: k_vadm_par (a burst of 16 lanes per stream, for a GPU with nothing
-// else queued) where it applies, else k_vadm_hbm (32 waves, overlaps quietly)
-hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream, bool fast = false);
+// else queued) where it applies, else k_vadm_hbm (32 waves, overlaps quietly);
+// *ran_par (nullable): which of the two was launched
+hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream, bool fast = false, bool *ran_par = nullptr);
 // use_denoiser = 0 (VAD.zig:206-212,239-249): k_ndring, k_ndmeta, FFT B
 hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream);
 // k_fftb's scratch need: 0 when a transform fits in LDS, else float2 per workgroup

@@ -1931,7 +1931,9 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
     float *st = a.vadm.buf + K.st_off + (sok ? s : 0), *rb = a.vadm.buf + K.r_off + (sok ? s : 0);
     VadmSeg *seg = a.vadm.seg + ((size_t)m * B + (sok ? s : 0)) * a.vadm.seg_cap;
     // (n > kVpMaxW: a push wraps around the buffer at most once)
-    const bool fast = sok && Kw <= kVpMaxW && K.n_lt > kVpMaxW && S.lt_count == (unsigned)K.n_lt && S.lt_pre_ok;
+    const bool forced = a.vadm.par_serial_every > 0 && s % a.vadm.par_serial_every == 0;
+    const bool fast = sok && !forced && Kw <= kVpMaxW && K.n_lt > kVpMaxW && S.lt_count == (unsigned)K.n_lt &&
+                      S.lt_pre_ok;
     const unsigned n = (unsigned)K.n_lt, wbase = S.lt_widx, nw0 = S.lt_nw;
     const double scalar = 1.0 / (double)n;  // the full buffer's
     if (r == 0) {
@@ -2023,10 +2025,11 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
     }
     if (r == 0 && sok) {
       if (rnd[g][2] == 2) {
-        // not this kernel's case: launch_vadm sends such machines to
-        // k_vadm_hbm (no initial average, or more windows than kVpMaxW);
-        // flagged in the state's spare word, the push's windows left unprocessed
-        a.vadm.st[(size_t)m * B + s].pad = 1;
+        // a machine outside the window-parallel case (launch_vadm sends
+        // engines whose machines can get here to k_vadm_hbm; the test hook
+        // par_serial_every forces it): the serial walk on the leader lane,
+        // from the untouched state in HBM
+        vadm_stream(a, m, s, lt, lts);
       } else {
         // the push's long-term values into the buffer (read above as the old entries)
         unsigned w = wbase;
@@ -2356,13 +2359,14 @@ hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream) {
   return launch_fftb(a, n_cu, stream);
 }
 
-hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream, bool fast) {
+hipError_t launch_vadm(const StagedArgs &a, hipStream_t stream, bool fast, bool *ran_par) {
   (void)hipGetLastError();
   // k_vadm_par's case: every machine's long-term buffer full from the start
   // (an initial average) and longer than a push's windows, at most kVpMaxW
   // windows per push (wmax bounds them)
   bool par = fast && a.wmax <= kVpMaxW;
   for (int m = 0; m < a.vadm.n; m++) par = par && a.vadm.c[m].has_init && a.vadm.c[m].n_lt > kVpMaxW;
+  if (ran_par) *ran_par = par;
   if (!par)
     FVAD_KERNEL_TRY(k_vadm_hbm, dim3((a.n_streams + kVadmHbmLanes - 1) / kVadmHbmLanes), dim3(kVadmHbmLanes), 0,
                     stream, a);

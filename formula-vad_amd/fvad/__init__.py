@@ -82,6 +82,21 @@ class VadConfig(C.Structure):
         return c
 
 
+class VadmSnapshot(C.Structure):
+    """fvad_vadm_snapshot (include/fvad.h): a device machine's whole state."""
+    _fields_ = [("speech_state", C.c_int), ("speech_start", C.c_uint64), ("speech_end", C.c_uint64),
+                ("windows", C.c_uint64), ("avg", C.c_double * 3), ("write_idx", C.c_uint64 * 3),
+                ("written", C.c_uint64 * 3), ("speech_rnn_vad", C.c_float), ("speech_vol_ratio", C.c_float),
+                ("speech_rnn_vad_count", C.c_uint64), ("speech_vol_ratio_count", C.c_uint64),
+                ("n_segments", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: (list(getattr(self, n)) if n in ("avg", "write_idx", "written") else getattr(self, n))
+                for n, _ in self._fields_}
+
+
+DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR = 1, 2
+
 READ_FN = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.c_int, C.POINTER(F32P), C.c_size_t)
 
 
@@ -161,6 +176,11 @@ SYMBOLS = [
     ("fvad_engine_segments_range", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_size_t]),
     ("fvad_engine_vadm_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint64),
                                          C.POINTER(C.c_uint64)]),
+    ("fvad_engine_vadm_snapshot", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    ("fvad_engine_vadm_rolling", C.c_long, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
+    ("fvad_engine_set_debug", C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    ("fvad_engine_output_log", C.c_int, [C.c_void_p, C.c_int]),
+    ("fvad_engine_output_log_read", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int)]),
     ("fvad_engine_clear_times", C.c_int, [C.c_void_p]),
     ("fvad_engine_fetch", C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     ("fvad_vadm_config_default", None, [C.c_void_p]),
@@ -428,6 +448,35 @@ class Engine:
         buf = (Segment * max(1, n))()
         lib().fvad_engine_segments(self.h, stream, machine, buf, n)
         return [(s.sample_from, s.sample_to, s.debug_rnn_vad, s.debug_avg_speech_vol_ratio) for s in buf[:n]]
+
+    def vadm_snapshot(self, stream, machine=0):
+        """The device machine's whole state (fvad_engine_vadm_snapshot) as a dict."""
+        s = VadmSnapshot()
+        _check(lib().fvad_engine_vadm_snapshot(self.h, stream, machine, C.byref(s)), "fvad_engine_vadm_snapshot")
+        return s.as_dict()
+
+    def vadm_rolling(self, stream, which, machine=0):
+        """RollingAverage.data (which 0 long-term, 1 short-term, 2 volume ratio) as float64."""
+        n = lib().fvad_engine_vadm_rolling(self.h, stream, machine, which, None, 0)
+        if n < 0:
+            raise FvadError("fvad_engine_vadm_rolling failed (%d): %s" % (n, last_error()))
+        out = np.zeros(n, np.float64)
+        lib().fvad_engine_vadm_rolling(self.h, stream, machine, which, out.ctypes.data_as(C.c_void_p), n)
+        return out
+
+    def set_debug(self, key, value):
+        """Test hooks (fvad_engine_set_debug): DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR."""
+        _check(lib().fvad_engine_set_debug(self.h, key, value), "fvad_engine_set_debug")
+
+    def output_log(self, n_pushes):
+        """Record the per-tick outputs of the next n_pushes pushes on the device (no host sync)."""
+        _check(lib().fvad_engine_output_log(self.h, n_pushes), "fvad_engine_output_log")
+
+    def output_log_read(self, push):
+        o, s = self._alloc_out(self.max_ticks, False)
+        n = C.c_int()
+        _check(lib().fvad_engine_output_log_read(self.h, push, C.byref(s), C.byref(n)), "fvad_engine_output_log_read")
+        return {k: v[: n.value] for k, v in o.items()}
 
     def fetch(self, n_ticks, denoised=False):
         o, s = self._alloc_out(n_ticks, denoised)

@@ -176,6 +176,7 @@ def staged_kernels(n_channels=2, fft_size=2048):
     # in LDS (only the partial window crosses pushes through the ring:
     # <= 2047 samples each way per channel and push, ~2 x 8 KB / 50 ticks)
     k["k_olafb"] = (960 + p["re-block + FFT B share"], 960 * 4 + 4 * 4.0 / C + 2 * 8192.0 / 50)
+    k["k_vadm_par"] = k["k_vadm_hbm"]  # the same machine, window-parallel (the push flushed at a sync point)
     k["k_gru16"] = k["k_rnn3"]  # FVAD_MODE_FP16: the same recurrence, gate sums on MFMA
     return {n: {"flops": f, "bytes": b} for n, (f, b) in k.items()}
 

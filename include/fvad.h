@@ -231,7 +231,10 @@ int fvad_engine_sync(fvad_engine *e);
 /* average per-launch kernel durations (ms) of the timed resident runs,
  * measured with HIP events on the engine's stream.  ms_avg holds
  * FVAD_MAX_TIMES doubles: [0] whole push (GPU time from its first to its last
- * kernel; staged kernels may overlap), [1 + i] kernel i (names below). */
+ * kernel; staged kernels may overlap), [1 + i] kernel i (names below).  With
+ * device VADMachines the last two names are k_vadm_hbm (a push's machine run
+ * beside the next push) and k_vadm_par (the push whose machine ran at a sync
+ * point, nothing queued behind it), each averaged over its own runs. */
 int fvad_engine_kernel_times(fvad_engine *e, double *ms_avg, int *n_runs);
 /* name of kernel i of this engine's mode, NULL past the last one */
 const char *fvad_engine_kernel_name(const fvad_engine *e, int i);
@@ -279,7 +282,12 @@ size_t fvad_vadm_segments(const fvad_vadm *v, fvad_segment *out, size_t cap);
  * stream, after FFT B of every push).  Staged engines only.
  * Each config's speech band (FFT.freqToBin of speech_min/max_freq) must be one
  * of the engine's bands.  Up to FVAD_MAX_BANDS machines; segments accumulate
- * on the device, seg_capacity per (stream, machine); a reset clears them. */
+ * on the device, seg_capacity per (stream, machine); a reset clears them.
+ * A push's machines are enqueued when the next push is launched (beside it, on
+ * a side stream) or at the next sync point (fvad_engine_sync, _segments,
+ * _vadm_state, _vadm_snapshot, _kernel_times), so after submit / collect the
+ * last collected push's windows are not in the machine state yet; every
+ * reader above flushes them first.  A reset or destroy drops them. */
 int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *cfgs, int n, int seg_capacity);
 /* total segments of (stream, machine) so far; copies min(total, capacity, cap) */
 size_t fvad_engine_segments(fvad_engine *e, int stream, int machine, fvad_segment *out, size_t cap);
@@ -290,6 +298,45 @@ size_t fvad_engine_segments_range(fvad_engine *e, int stream, int machine, size_
  * 2 open, 3 closing) and its current speech start / end sample indices */
 int fvad_engine_vadm_state(fvad_engine *e, int stream, int machine, int *speech_state, uint64_t *speech_start,
                            uint64_t *speech_end);
+/* The whole state of an attached machine in the reference's terms
+ * (VADMachine.zig:65-125 fields; RollingAverage.zig:5-14 for long_term [0],
+ * short_term [1] and the channel volume ratio [2]), after every queued push:
+ * what a checker compares with a CPU VADMachine fed the same windows. */
+typedef struct {
+  int speech_state;                 /* 0 closed, 1 opening, 2 open, 3 closing */
+  uint64_t speech_start, speech_end;  /* speech_start_index, speech_end_index */
+  uint64_t windows;                 /* windows the machine has run */
+  double avg[3];                    /* RollingAverage.last_avg (0 before the first avg) */
+  uint64_t write_idx[3];            /* RollingAverage.write_idx */
+  uint64_t written[3];              /* RollingAverage.written_count */
+  float speech_rnn_vad, speech_vol_ratio;  /* the current speech's tracked sums */
+  uint64_t speech_rnn_vad_count, speech_vol_ratio_count;
+  uint64_t n_segments;              /* segments emitted so far (also past seg_capacity) */
+} fvad_vadm_snapshot;
+int fvad_engine_vadm_snapshot(fvad_engine *e, int stream, int machine, fvad_vadm_snapshot *out);
+/* RollingAverage.data of (stream, machine), which = 0 long-term, 1 short-term,
+ * 2 volume ratio, as doubles: copies min(len, cap) entries, returns len (< 0:
+ * error code) */
+long fvad_engine_vadm_rolling(fvad_engine *e, int stream, int machine, int which, double *out, size_t cap);
+
+/* Test hooks: knobs and a recorder the parity tests use; no product path sets
+ * them.  fvad_engine_set_debug keys:
+ *   FVAD_DEBUG_VADM_PAR_SERIAL_EVERY  value k > 0: k_vadm_par hands every
+ *     stream s with s % k == 0 to its in-kernel serial walk (the fallback for a
+ *     machine outside the window-parallel case); 0: never (default)
+ *   FVAD_DEBUG_VADM_ALWAYS_PAR  value 1: every push's VADMachine runs as
+ *     k_vadm_par, not only the one flushed at a sync point */
+#define FVAD_DEBUG_VADM_PAR_SERIAL_EVERY 1
+#define FVAD_DEBUG_VADM_ALWAYS_PAR 2
+int fvad_engine_set_debug(fvad_engine *e, int key, int value);
+/* Output log: the per-tick outputs (fvad_outputs without denoised) of the next
+ * n_pushes pushes are copied into device memory on the engine stream as each
+ * push's kernels end -- no host synchronisation, so a run of asynchronous
+ * pushes (run_resident, submit) keeps its schedule; read them back after the
+ * pushes with fvad_engine_output_log_read (push = 0 .. n_pushes - 1 in launch
+ * order).  n_pushes = 0 frees the log.  Staged / fp16 engines with the denoiser. */
+int fvad_engine_output_log(fvad_engine *e, int n_pushes);
+int fvad_engine_output_log_read(fvad_engine *e, int push, fvad_outputs *out, int *n_ticks);
 
 /* VAD.Config (VAD.zig:17-23) */
 typedef struct {

@@ -144,6 +144,7 @@ typedef struct {
   ora_segment *segs;
   size_t n_segs, cap_segs;
   size_t min_bin, max_bin;
+  uint64_t n_runs; /* windows run (checker bookkeeping, not a reference field) */
 } vadm;
 
 static size_t freq_to_bin(int sample_rate, int nfft, float freq) {
@@ -228,6 +229,7 @@ static void vadm_run(vadm *m, uint64_t index, const float *const *bins, int has_
   size_t min_open, max_gap;
   double short_term, ratio_avg, threshold_base, threshold;
   int met;
+  m->n_runs++;
   for (ch = 0; ch < m->n_channels; ch++) {
     vols[ch] = 0.0f;
     for (i = m->min_bin; i <= m->max_bin; i++) vols[ch] += bins[ch][i];
@@ -518,3 +520,38 @@ size_t ora_pipeline_segments(const ora_pipeline *p, int alt_idx, ora_segment *ou
 }
 
 const ora_denoise *ora_pipeline_denoiser(const ora_pipeline *p) { return p->use_denoiser ? p->den : NULL; }
+
+/* the whole machine state (VADMachine.zig:65-125, RollingAverage.zig:5-14) for
+ * the checker's comparison with the device machine; alt_idx < 0: the main one */
+static const vadm *machine_of(const ora_pipeline *p, int alt_idx) {
+  return (alt_idx < 0) ? &p->main : &p->alts[alt_idx];
+}
+
+void ora_pipeline_vadm_snapshot(const ora_pipeline *p, int alt_idx, ora_vadm_snapshot *out) {
+  const vadm *m = machine_of(p, alt_idx);
+  const rolling *r[3] = {&m->long_term, &m->short_term, &m->ratio};
+  int k;
+  memset(out, 0, sizeof(*out));
+  out->speech_state = m->state;
+  out->speech_start = m->speech_start_index;
+  out->speech_end = m->speech_end_index;
+  out->windows = m->n_runs;
+  for (k = 0; k < 3; k++) {
+    out->avg[k] = r[k]->last_avg;
+    out->write_idx[k] = r[k]->write_idx;
+    out->written[k] = r[k]->written_count;
+  }
+  out->speech_rnn_vad = m->speech_rnn_vad;
+  out->speech_vol_ratio = m->speech_vol_ratio;
+  out->speech_rnn_vad_count = m->speech_rnn_vad_count;
+  out->speech_vol_ratio_count = m->speech_vol_ratio_count;
+  out->n_segments = m->n_segs;
+}
+
+size_t ora_pipeline_vadm_rolling(const ora_pipeline *p, int alt_idx, int which, double *out, size_t cap) {
+  const vadm *m = machine_of(p, alt_idx);
+  const rolling *r = which == 0 ? &m->long_term : which == 1 ? &m->short_term : &m->ratio;
+  size_t i;
+  for (i = 0; i < r->len && i < cap; i++) out[i] = r->data[i];
+  return r->len;
+}

@@ -146,6 +146,20 @@ void ora_pipeline_destroy(ora_pipeline *p);
 uint64_t ora_pipeline_push(ora_pipeline *p, const float *const *channel_pcm, size_t n);
 /* main VADMachine segments (alt_idx<0) or alternative machine alt_idx */
 size_t ora_pipeline_segments(const ora_pipeline *p, int alt_idx, ora_segment *out, size_t cap);
+/* the machine's whole state (VADMachine.zig:65-125; RollingAverage.zig:5-14 for
+ * long_term [0], short_term [1], ratio [2]); field layout of fvad.h's
+ * fvad_vadm_snapshot, so the checker compares the two field by field */
+typedef struct {
+  int speech_state;
+  uint64_t speech_start, speech_end, windows;
+  double avg[3];
+  uint64_t write_idx[3], written[3];
+  float speech_rnn_vad, speech_vol_ratio;
+  uint64_t speech_rnn_vad_count, speech_vol_ratio_count, n_segments;
+} ora_vadm_snapshot;
+void ora_pipeline_vadm_snapshot(const ora_pipeline *p, int alt_idx, ora_vadm_snapshot *out);
+/* RollingAverage.data (which: 0 long_term, 1 short_term, 2 ratio); returns its length */
+size_t ora_pipeline_vadm_rolling(const ora_pipeline *p, int alt_idx, int which, double *out, size_t cap);
 
 /* per-frame trace of the hot path (filled when tracing is enabled) */
 typedef struct {

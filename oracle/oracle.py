@@ -69,6 +69,9 @@ def lib():
         L.ora_pipeline_push.argtypes = [C.c_void_p, C.POINTER(F32P), C.c_size_t]
         L.ora_pipeline_segments.restype = C.c_size_t
         L.ora_pipeline_segments.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
+        L.ora_pipeline_vadm_snapshot.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.ora_pipeline_vadm_rolling.restype = C.c_size_t
+        L.ora_pipeline_vadm_rolling.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]
         L.ora_pipeline_enable_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                                 F32P, C.c_size_t]
         L.ora_pipeline_trace_counts.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
@@ -107,6 +110,19 @@ class VadmConfig(C.Structure):
 class Segment(C.Structure):
     _fields_ = [("sample_from", C.c_uint64), ("sample_to", C.c_uint64),
                 ("debug_rnn_vad", C.c_float), ("debug_avg_speech_vol_ratio", C.c_float)]
+
+
+class VadmSnapshot(C.Structure):
+    """ora_vadm_snapshot (oracle.h): the machine's whole state."""
+    _fields_ = [("speech_state", C.c_int), ("speech_start", C.c_uint64), ("speech_end", C.c_uint64),
+                ("windows", C.c_uint64), ("avg", C.c_double * 3), ("write_idx", C.c_uint64 * 3),
+                ("written", C.c_uint64 * 3), ("speech_rnn_vad", C.c_float), ("speech_vol_ratio", C.c_float),
+                ("speech_rnn_vad_count", C.c_uint64), ("speech_vol_ratio_count", C.c_uint64),
+                ("n_segments", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: (list(getattr(self, n)) if n in ("avg", "write_idx", "written") else getattr(self, n))
+                for n, _ in self._fields_}
 
 
 class FrameTrace(C.Structure):
@@ -304,6 +320,18 @@ class Pipeline:
         buf = (Segment * max(1, n))()
         lib().ora_pipeline_segments(self.h, alt, buf, n)
         return [(s.sample_from, s.sample_to, s.debug_rnn_vad, s.debug_avg_speech_vol_ratio) for s in buf[:n]]
+
+    def vadm_snapshot(self, alt=-1):
+        s = VadmSnapshot()
+        lib().ora_pipeline_vadm_snapshot(self.h, alt, C.byref(s))
+        return s.as_dict()
+
+    def vadm_rolling(self, which, alt=-1):
+        """RollingAverage.data of the machine: which 0 long_term, 1 short_term, 2 ratio."""
+        n = lib().ora_pipeline_vadm_rolling(self.h, alt, which, None, 0)
+        out = np.zeros(n, np.float64)
+        lib().ora_pipeline_vadm_rolling(self.h, alt, which, out.ctypes.data_as(C.c_void_p), n)
+        return out
 
     def trace(self):
         nf = C.c_size_t()

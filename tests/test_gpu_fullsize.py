@@ -5,10 +5,19 @@ re-block, FFT B; VADMachine.zig:126-230 segments):
 * the bench's exact timed workload (bench.py): 2048 stereo streams, 50-tick
   pushes, the 20 distinct resident pushes (the first 10 s of every stream:
   burst onsets, speech, the every-20th-stream digital silence at t = 5 s),
-  device VADMachine attached; then two pushes streamed from host memory
-  (submit / collect) that replay the cycle's first second, as the bench's
-  second cycle does -- staged mode bit for bit, fp16 mode (configs[4]'s
-  variant) at the stated tolerance;
+  device VADMachine attached; then five pushes streamed from host memory
+  (submit / collect, three in flight) that replay the cycle's first 2.5 s, as
+  the bench's second cycle does -- staged mode bit for bit, fp16 mode
+  (configs[4]'s variant) at the stated tolerance;
+* the bench's exact SCHEDULE (bench.py:387-401): the same 25 pushes through
+  run_resident with no synchronisation between them -- the next push's
+  k_prep3 overlapping this one's kernels, the steady-state k_vadm_hbm beside
+  the next push, k_vadm_par only for the push before a sync -- every push's
+  outputs (recorded on the device by fvad_engine_output_log, no host sync),
+  every stream's segments, the whole VADMachine state (fvad_engine_vadm_snapshot)
+  and its RollingAverage buffers against the oracle fed the same 25 pushes;
+  also with every machine on k_vadm_par and a third of them forced through its
+  in-kernel serial fallback;
 * configs[3]'s per-GPU shard: 4096 streams over 8 GPUs = 512 streams, here
   rank 3's ids 1536..2047, 12 pushes (6 s, the silence included), staged and
   fp16.
@@ -18,6 +27,7 @@ and shared by the staged and fp16 tests.
 """
 import concurrent.futures as cf
 import functools
+import hashlib
 
 import numpy as np
 import pytest
@@ -34,6 +44,10 @@ BAND_REL = 2e-3
 SEG_SHIFT = 4 * 2048  # fp16: a segment bound may move by at most 4 FFT-B windows
 
 
+def _digest(a):
+    return hashlib.sha1(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
+
+
 def _oracle_stream(args):
     import fvad
     import oracle
@@ -48,7 +62,10 @@ def _oracle_stream(args):
     for a in range(0, replay_ticks * FRAME, n):
         p.push([x[0, a:a + n], x[1, a:a + n]])
     fr, wi = p.trace()
-    return fr, wi, p.segments()
+    # the machine's whole state after every push, its long-term buffer (4218
+    # entries) as a digest, the short ones as arrays
+    state = (p.vadm_snapshot(), _digest(p.vadm_rolling(0)), p.vadm_rolling(1), p.vadm_rolling(2))
+    return fr, wi, p.segments(), state
 
 
 @functools.lru_cache(maxsize=None)
@@ -66,7 +83,7 @@ def oracle_workload(base, n_streams, pushes, replay_pushes):
         return list(ex.map(_oracle_stream, [(base + s, pushes * T, replay_pushes * T) for s in range(n_streams)]))
 
 
-def run_engine(fvad_mod, model, mode, base, n_streams, pushes, replay_pushes):
+def run_engine(fvad_mod, model, mode, base, n_streams, pushes, replay_pushes, want_state=False):
     """The bench's engine: resident cycle (run_resident), then the cycle's
     first replay_pushes pushes again through submit / collect."""
     eng = fvad_mod.Engine(model, n_streams, 2, max_ticks=T, mode=mode)
@@ -78,20 +95,42 @@ def run_engine(fvad_mod, model, mode, base, n_streams, pushes, replay_pushes):
         eng.sync()
         outs.append(eng.fetch(T))
     if replay_pushes:
+        # streamed, at most FVAD_MAX_IN_FLIGHT (3) uncollected
         src = fvad_mod.synth_ticks(base, n_streams, 2, pushes * T, 0, replay_pushes * T)
+        inflight = 0
         for k in range(replay_pushes):
+            if inflight == 3:
+                outs.append(eng.collect())
+                inflight -= 1
             eng.submit(src[k * T:(k + 1) * T])
-        for k in range(replay_pushes):
+            inflight += 1
+        for _ in range(inflight):
             outs.append(eng.collect())
     eng.sync()
     got = {k: np.concatenate([o[k] for o in outs]) for k in outs[0]}
     segs = [eng.segments(s) for s in range(n_streams)]
+    if want_state:
+        return got, segs, device_state(eng, n_streams)
     return got, segs
+
+
+def device_state(eng, n_streams):
+    """Every stream's machine state and RollingAverage buffers (the oracle's form)."""
+    return [(eng.vadm_snapshot(s), _digest(eng.vadm_rolling(s, 0)), eng.vadm_rolling(s, 1), eng.vadm_rolling(s, 2))
+            for s in range(n_streams)]
+
+
+def check_state(ref, got_state):
+    for s, (r, g) in enumerate(zip(ref, got_state)):
+        rs, gs = r[3], g
+        assert rs[0] == gs[0], (s, rs[0], gs[0])
+        assert rs[1] == gs[1], (s, "long-term RollingAverage buffer differs")
+        assert np.array_equal(rs[2], gs[2]) and np.array_equal(rs[3], gs[3]), (s, "short RollingAverage buffers")
 
 
 def check_exact(ref, got, segs):
     n_seg = 0
-    for s, (fr, wi, rsegs) in enumerate(ref):
+    for s, (fr, wi, rsegs, _) in enumerate(ref):
         assert np.array_equal(fr["vad"], got["vad"][:, s]), (s, pu.first_mismatch(fr["vad"], got["vad"][:, s]))
         assert np.array_equal(fr["ratio"], got["ratio"][:, s]), s
         wf = got["win_flag"][:, s].astype(bool)
@@ -109,7 +148,7 @@ MAX_MOVED = 3
 
 def check_tolerance(ref, got, segs):
     worst_v, worst_b, n_seg, diffs = 0.0, 0.0, 0, []
-    for s, (fr, wi, rsegs) in enumerate(ref):
+    for s, (fr, wi, rsegs, _) in enumerate(ref):
         dv = float(np.abs(fr["vad"] - got["vad"][:, s]).max())
         assert dv <= VAD_ABS, (s, dv)
         assert np.array_equal(fr["ratio"], got["ratio"][:, s]), s  # computed before the GRU
@@ -142,7 +181,7 @@ def model(fvad_mod):
     return fvad_mod.Model(seed=1)
 
 
-BENCH = (0, 2048, 20, 2)      # base, streams, resident pushes, replayed pushes
+BENCH = (0, 2048, 20, 5)      # base, streams, resident pushes, replayed pushes (25 = bench warmup 5 + steps 20)
 SHARD = (1536, 512, 12, 0)    # configs[3]: rank 3 of 8, 512 streams, 6 s
 
 
@@ -151,11 +190,12 @@ def test_bench_workload_staged_every_stream(fvad_mod, oracle_mod, model):
     """bench.py's timed input (the 20-push resident cycle) + two streamed
     replay pushes: every stream's vad, ratio, window flag / ratio / vad, band
     sums and segments equal the oracle's bit for bit."""
-    got, segs = run_engine(fvad_mod, model, "staged", *BENCH)
+    got, segs, state = run_engine(fvad_mod, model, "staged", *BENCH, want_state=True)
     assert (got["vad"][500:600, 19::20] == 0).sum() > 5000  # the silent streams hit the E < 0.04 gate
     ref = oracle_workload(*BENCH)
     n_seg = check_exact(ref, got, segs)
     assert n_seg > 100
+    check_state(ref, state)
     print("bench workload staged: 2048 streams x %d frames bit-exact, %d segments" % (len(ref[0][0]), n_seg))
 
 
@@ -190,3 +230,73 @@ def test_configs3_shard_512_streams(fvad_mod, oracle_mod, model, mode):
         wv, wb, n_seg, diffs = check_tolerance(ref, got, segs)
         print("configs[3] shard fp16: max |dvad| %.3g, band rel %.3g, %d segments, moved bounds %s" % (
             wv, wb, n_seg, diffs))
+
+
+# bench.py:387-401: warmup pushes, a sync (the drain: k_vadm_par), the timed
+# pushes back to back, a sync
+SCHEDULES = {"bench": (5, 20), "nosync": (25, 0)}
+
+
+def run_schedule(eng, schedule, log, n_streams):
+    """The resident cycle from push 0 with the bench's schedule; the outputs of
+    every push from the device log (log=True) or only the last push's (fetch)."""
+    eng.reset()
+    eng.resident_seek(0)
+    n_pushes = sum(SCHEDULES[schedule])
+    eng.output_log(n_pushes if log else 0)
+    for n in SCHEDULES[schedule]:
+        for _ in range(n):
+            eng.run_resident(T)  # no sync in between: the host queues pushes ahead of the GPU
+        if n:
+            eng.sync()
+    outs = [eng.output_log_read(k) for k in range(n_pushes)] if log else [eng.fetch(T)]
+    got = {k: np.concatenate([o[k] for o in outs]) for k in outs[0]}
+    segs = [eng.segments(s) for s in range(n_streams)]
+    return got, segs, device_state(eng, n_streams)
+
+
+def last_push(ref, n_ticks):
+    """The oracle's outputs of the workload's last push only (fetch after the run)."""
+    out = []
+    for fr, wi, rsegs, st in ref:
+        t0 = len(fr) - n_ticks
+        wsel = wi["index"] + 2048 > fr["index"][t0]  # windows whose last sample is in the push
+        out.append((fr[t0:], wi[wsel], rsegs, st))
+    return out
+
+
+@pytest.mark.timeout(1200)
+def test_bench_schedule_staged_every_stream(fvad_mod, oracle_mod, model):
+    """The bench's timed schedule itself: 2048 streams, the 25
+    pushes of bench.py's default --warmup 5 --steps 20 through run_resident
+    with no synchronisation between the pushes of a leg -- k_prep3 of push k+1
+    beside push k (double-buffered xs / ratio / ticks), k_vadm_hbm of push k
+    beside push k+1 on the side stream reading window-output set k & 1 in
+    place, k_vadm_par only for the push before a sync.  Schedules: the bench's
+    (5, sync, 20, sync) and 25 back to back.  Checked against the oracle fed
+    the same 25 pushes: every stream's segments, VADMachine state and
+    RollingAverage buffers after an unlogged run (the exact bench schedule),
+    and every push's per-tick outputs from a run with the device output log.
+    Then the same with every machine on k_vadm_par (FVAD_DEBUG_VADM_ALWAYS_PAR)
+    and every third stream forced through k_vadm_par's in-kernel serial
+    fallback (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY = 3)."""
+    base, B, P, R = BENCH
+    eng = fvad_mod.Engine(model, B, 2, max_ticks=T, mode="staged")
+    eng.attach_vadm()
+    eng.load_synthetic(T, base=base, pushes=P)
+    ref = oracle_workload(*BENCH)
+    for schedule in ("bench", "nosync"):
+        got, segs, state = run_schedule(eng, schedule, False, B)
+        check_exact(last_push(ref, T), got, segs)
+        check_state(ref, state)
+        got, segs, state = run_schedule(eng, schedule, True, B)
+        assert got["vad"].shape == (len(ref[0][0]), B)
+        n_seg = check_exact(ref, got, segs)
+        check_state(ref, state)
+        print("bench schedule %s: 2048 streams x 25 pushes bit-exact, %d segments" % (schedule, n_seg))
+    eng.set_debug(fvad_mod.DEBUG_VADM_ALWAYS_PAR, 1)
+    eng.set_debug(fvad_mod.DEBUG_VADM_PAR_SERIAL_EVERY, 3)
+    got, segs, state = run_schedule(eng, "nosync", True, B)
+    check_exact(ref, got, segs)
+    check_state(ref, state)
+    print("k_vadm_par on every push, every third stream on its serial fallback: bit-exact")

@@ -67,3 +67,34 @@ def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec):
             assert got == ref, (s, mi, got[:3], ref[:3])
             total += len(ref)
     assert total > 0
+
+
+@pytest.mark.parametrize("flavour", ["default", "always_par", "par_serial_fallback"])
+def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
+    """The whole device machine state (fvad_engine_vadm_snapshot: speech state
+    and indices, RollingAverage last averages / write indices / counts, the
+    tracked speech sums, segment count) and its RollingAverage buffers equal
+    the oracle's VADMachine after the same windows.  default: k_vadm_hbm
+    between pushes, k_vadm_par for the last one; always_par: every push's
+    machine on k_vadm_par (FVAD_DEBUG_VADM_ALWAYS_PAR); par_serial_fallback:
+    the same with every second stream forced through k_vadm_par's in-kernel
+    serial walk (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY = 2)."""
+    m = fvad_mod.Model(seed=1)
+    om = oracle_mod.Model(seed=1)
+    ids = [0, 3, 19, 39, 7, 12, 59, 8]
+    streams, _ = pu.make_streams(fvad_mod, ids, 14.0)
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=50)
+    eng.attach_vadm()
+    if flavour != "default":
+        eng.set_debug(fvad_mod.DEBUG_VADM_ALWAYS_PAR, 1)
+    if flavour == "par_serial_fallback":
+        eng.set_debug(fvad_mod.DEBUG_VADM_PAR_SERIAL_EVERY, 2)
+    pu.engine_run(fvad_mod, eng, streams, 50, denoised=False)
+    for s, x in enumerate(streams):
+        p = oracle_mod.Pipeline(2, om)
+        for k in range(0, x.shape[1], 24000):
+            p.push([x[0, k:k + 24000], x[1, k:k + 24000]])
+        assert eng.vadm_snapshot(s) == p.vadm_snapshot(), s
+        for which in range(3):
+            assert np.array_equal(eng.vadm_rolling(s, which), p.vadm_rolling(which)), (s, which)
+        assert eng.segments(s) == p.segments(), s
