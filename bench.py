@@ -74,8 +74,6 @@ def parse():
                     help="also time pushes from host buffers (PCIe-inclusive; reported as host_buffers, never value)")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="no GPU: gloo ranks with a stub engine (tests the launcher, barrier and max-reduce)")
-    ap.add_argument("--split", type=int, default=1,
-                    help="engines per GPU on disjoint CU masks, B / split streams each, run side by side")
     ap.add_argument("--variants", type=int, default=1,
                     help="staged runs: also time the fp16 engine mode (configs[4]'s variant) on the same "
                          "workload and report it under `variants` (never `value`)")
@@ -273,50 +271,43 @@ def host_rate(eng, args, rank, dist, torch, base):
     submit_i16 (half the PCIe bytes, converted on the device)."""
     import fvad
     import numpy as np
-    engs = eng if isinstance(eng, list) else [eng]  # --split: the engines side by side, B / split streams each
+    e = eng
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
-    Bp = B // len(engs)
     src = fvad.synth_ticks(base, B, Ch, args.resident_pushes * T, 0, 2 * T)
     halves = (src[:T], src[T:])
+    del src
     q16 = [np.clip(np.round(h * 32768.0), -32768, 32767).astype(np.int16) for h in halves]
     res = {}
     for kind in ("pinned", "pageable", "pinned_i16"):
-        for p, e in enumerate(engs):
-            part = slice(p * Bp, (p + 1) * Bp)
-            if kind.startswith("pinned"):
-                for k in range(DEPTH):  # every slot holds one of the two pushes
-                    if kind == "pinned":
-                        sl = e.input_slot()
-                        sl[:T] = halves[k & 1][:, part]
-                        e.submit(sl[:T])
-                    else:
-                        sl = e.input_slot_i16()
-                        sl[:T] = q16[k & 1][:, part]
-                        e.submit_i16(sl[:T])
-                for _ in range(DEPTH):
-                    e.collect(want=False)
-            e.sync()
-        pages = [[np.ascontiguousarray(h[:, p * Bp:(p + 1) * Bp]) for h in halves] for p in range(len(engs))]
+        if kind.startswith("pinned"):
+            for k in range(DEPTH):  # every slot holds one of the two pushes
+                if kind == "pinned":
+                    sl = e.input_slot()
+                    sl[:T] = halves[k & 1]
+                    e.submit(sl[:T])
+                else:
+                    sl = e.input_slot_i16()
+                    sl[:T] = q16[k & 1]
+                    e.submit_i16(sl[:T])
+            for _ in range(DEPTH):
+                e.collect(want=False)
+        e.sync()
         barrier(dist, torch)
         t0 = time.perf_counter()
         inflight = 0
         for k in range(args.steps):
             if inflight == DEPTH:
-                for e in engs:
-                    e.collect(want=True)
+                e.collect(want=True)
                 inflight -= 1
-            for p, e in enumerate(engs):
-                if kind == "pinned_i16":
-                    e.submit_i16(e.input_slot_i16()[:T])
-                else:
-                    e.submit(e.input_slot()[:T] if kind == "pinned" else pages[p][k & 1])
+            if kind == "pinned_i16":
+                e.submit_i16(e.input_slot_i16()[:T])
+            else:
+                e.submit(e.input_slot()[:T] if kind == "pinned" else halves[k & 1])
             inflight += 1
         while inflight:
-            for e in engs:
-                e.collect(want=True)
+            e.collect(want=True)
             inflight -= 1
-        for e in engs:
-            e.sync()
+        e.sync()
         barrier(dist, torch)
         sec = max_over_ranks(time.perf_counter() - t0, dist, torch)
         res[kind] = (aggregate_rate(B * Ch * T, 1 if dist is None else dist.get_world_size(), args.steps, sec),
@@ -368,40 +359,23 @@ def main():
     base, _ = stream_partition(rank, B)
 
     def measure(mode):
-        """warmup, then exactly args.steps pushes between barriers; max over ranks.
-        --split S: S engines of B / S streams each on disjoint CU masks of this
-        GPU, side by side (a step pushes every stream once); the kernel table
-        is engine 0's"""
-        S = args.split
-        if S > 1:
-            n_cu = torch.cuda.get_device_properties(local).multi_processor_count
-            masks = [[i for i in range(n_cu) if (i // 8) % S == p] for p in range(S)]
-            engs = [fvad.Engine(model, B // S, Ch, device=local, max_ticks=T, mode=mode, cu_mask=masks[p])
-                    for p in range(S)]
-            bases = [base + p * (B // S) for p in range(S)]
-        else:
-            engs, bases = [fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=mode)], [base]
-        for e, b in zip(engs, bases):
-            if mode != "fused" and not args.no_vadm:
-                e.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
-            e.load_synthetic(T, base=b, pushes=P)
+        """warmup, then exactly args.steps pushes between barriers; max over ranks"""
+        e = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=mode)
+        if mode != "fused" and not args.no_vadm:
+            e.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
+        e.load_synthetic(T, base=base, pushes=P)
         for _ in range(args.warmup):
-            for e in engs:
-                e.run_resident(T)
-        for e in engs:
-            e.sync()
-            e.clear_times()
+            e.run_resident(T)
+        e.sync()
+        e.clear_times()
         barrier(dist, torch)
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            for e in engs:
-                e.run_resident(T)
-        for e in engs:
-            e.sync()
+            e.run_resident(T)
+        e.sync()
         barrier(dist, torch)
         elapsed = max_over_ranks(time.perf_counter() - t0, dist, torch)
-        kt = engs[0].kernel_times()
-        return (engs[0] if S == 1 else engs), elapsed, kt
+        return e, elapsed, e.kernel_times()
 
     eng, elapsed, kt_local = measure(args.mode)
     kt, ranks = gather_kernel_tables(kt_local, dist, torch, rank)
@@ -413,7 +387,6 @@ def main():
     if args.variants and args.mode == "staged":
         del eng  # one engine's buffers at a time
         e16, el16, kt16 = measure("fp16")
-        ov16 = e16.overlap if not isinstance(e16, list) else False
         del e16
         kt16, _ = gather_kernel_tables(kt16, dist, torch, rank)
         variants = {"fp16": {
@@ -421,13 +394,22 @@ def main():
             "ms_per_step": round(1000.0 * el16 / args.steps, 3),
             "dtype": "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
             "k_gru16_ms": round(kt16["kernels"].get("k_gru16", 0.0), 4),
-            "gru_synth_overlap": ov16,
             "kernels_ms": {k: round(v, 4) for k, v in kt16["kernels"].items()},
             "parity": "tolerance (SURVEY.md 8(c): vad |d| <= 2e-2, segments identical or reported -- 1238 of "
                       "1239 segment lists identical on this workload; tests/test_gpu_fp16.py, test_gpu_fullsize.py)",
             "note": "BASELINE configs[4]'s fp16-GRU variant on the same workload and clock (bench.py --mode fp16 "
                     "gives its full line)"}}
-    fvad.synth_cache_clear()
+    # host memory of this rank after its GPU legs (bounded: the synthetic input
+    # is generated and uploaded 64 streams at a time, nothing cached; the
+    # pinned slots of the streaming leg are FVAD_MAX_IN_FLIGHT pushes each way)
+    import resource
+    host_mem = {"peak_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1),
+                "pinned_slots_mb": round(DEPTH * (B * Ch * T * 480 * 6 + B * T * 4 * 8) / 2 ** 20, 1)
+                if args.host_rate else 0.0}
+    host_mem_all = None
+    if dist is not None:
+        host_mem_all = [None] * world
+        dist.all_gather_object(host_mem_all, host_mem)
 
     if rank != 0:
         if dist is not None:
@@ -449,12 +431,13 @@ def main():
                    "fft_size": 2048,
                    "parallelism": "stream-partition x%d (no collectives)" % world, "mode": args.mode,
                    "vad_machine": "device" if (args.mode != "fused" and not args.no_vadm) else "none",
-                   "gru_synth_overlap": bool(getattr(eng, "overlap", False)) if args.mode == "fp16" else None,
-                   "split": args.split},
+                   },
         "realtime_streams": round(value / (100.0 * Ch), 1),
         "roofline": roofline(args, kt, value, world, ms_per_step, cost, ranks),
         "cpu_baseline": None,
     }
+    line["host_memory"] = dict(host_mem, **({"per_rank_peak_rss_mb": [h["peak_rss_mb"] for h in host_mem_all]}
+                                            if host_mem_all else {}))
     if variants is not None:
         line["variants"] = variants
     if host is not None:
@@ -479,7 +462,7 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks):
     ceilings.  The engine records the events on every 4th timed push
     (FVAD_EVENT_EVERY): on every push their markers cost it ~1 %."""
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
-    frames_launch = B * Ch * T // args.split  # --split: engine 0's launches carry B / split streams
+    frames_launch = B * Ch * T
     if args.mode == "fused":
         prep_share = cost.phases(Ch)["prep: s16 scale + HP biquad + rms"]
         per_k = {"k_prep": {"flops": prep_share, "bytes": cost.prep_kernel_bytes(B, Ch, T) / frames_launch},

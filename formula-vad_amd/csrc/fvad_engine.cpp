@@ -125,15 +125,6 @@ struct fvad_engine {
   long long *d_wstart = nullptr;
   int V = 0, L = 0, LX = 0, wmax = 0, grid_frames = 0;
   int wpt = 1;  // window slots per (tick, stream): windows_per_tick(fft_size)
-  // fp16 overlap (fvad::Overlap): k_gru16 on gstream (CU set A), the gated
-  // synthesis beside it on sstream (set B, where k_prep3 and the VADMachines
-  // run too, so no wave of theirs holds a GRU CU)
-  bool overlap = false;
-  hipStream_t gstream = nullptr, sstream = nullptr;
-  hipEvent_t ev_ov[3] = {};
-  unsigned *d_gate = nullptr;
-  uint32_t mask_a[8] = {}, mask_b[8] = {};
-  int n_cu_b = 0;
   // FFT B above kMaxFftB: tables [tw | sup | hann | perm] and k_fftb's scratch
   float *d_fbtab = nullptr;
   float2 *d_fbwork = nullptr;
@@ -336,7 +327,7 @@ void free_all(fvad_engine *e) {
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->d_gru16, e->d_gru16_bias, e->vadm.st, e->vadm.buf,
                   e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vticks_b[1], e->d_vwratio, e->d_vwvad, e->d_vband,
-                  e->d_fbtab, e->d_fbwork, e->d_gate, e->d_log};
+                  e->d_fbtab, e->d_fbwork, e->d_log};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &set : e->evs)
@@ -349,10 +340,6 @@ void free_all(fvad_engine *e) {
   if (e->d_pcm16) (void)hipFree(e->d_pcm16);
 
   if (e->side) (void)hipStreamDestroy(e->side);
-  if (e->gstream) (void)hipStreamDestroy(e->gstream);
-  if (e->sstream) (void)hipStreamDestroy(e->sstream);
-  for (hipEvent_t ev : e->ev_ov)
-    if (ev) (void)hipEventDestroy(ev);
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
   if (e->cstream) (void)hipStreamDestroy(e->cstream);
   for (auto &sl : e->slots) {
@@ -398,12 +385,6 @@ extern "C" int fvad_engine_reset(fvad_engine *e) {
 }
 
 namespace {
-// CUs named by the config's mask (0: no mask)
-int mask_cus(const fvad_engine_config &c) {
-  int n = 0;
-  for (uint32_t w : c.cu_mask) n += __builtin_popcount(w);
-  return n;
-}
 void fill_bands(const fvad_engine_config &c, int *band_lo, int *band_hi, int *lo_all, int *hi_all) {
   int lo = 1 << 30, hi = -1;
   for (int b = 0; b < fvad::kMaxBandCfg; b++) {
@@ -421,18 +402,9 @@ void fill_bands(const fvad_engine_config &c, int *band_lo, int *band_hi, int *lo
 }  // namespace
 
 namespace {
-// an engine stream: on the config's CUs when it names any
-hipError_t make_stream(const fvad_engine *e, hipStream_t *s, const uint32_t *mask = nullptr) {
-  if (mask) return hipExtStreamCreateWithCUMask(s, 8, mask);
-  if (mask_cus(e->cfg)) return hipExtStreamCreateWithCUMask(s, 8, e->cfg.cu_mask);
-  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-}
-// fp16 overlap CU sets: CU i in set A iff (i / 8) % 2 == 0 -- every XCD keeps
-// half its CUs in each set whether the mask numbering runs XCD-major or
-// interleaves the XCDs
-void overlap_masks(int n_cu, uint32_t *a, uint32_t *b) {
-  for (int i = 0; i < n_cu && i < 256; i++) ((i / 8) % 2 == 0 ? a : b)[i / 32] |= 1u << (i % 32);
-}
+// an engine stream: non-blocking, so the synchronous null-stream copies of the
+// setup calls never wait for queued pushes
+hipError_t make_stream(hipStream_t *s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
 }  // namespace
 
 extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_model *model, fvad_engine **out) {
@@ -496,34 +468,9 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
     return rc;
   };
   if (hipSetDevice(c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipSetDevice failed"));
-  {
-    // fp16 overlap: opt-in (FVAD_FP16_OVERLAP=1) when the engine has the whole
-    // GPU and k_gru16's workgroups fit set A.  Measured slower than the
-    // sequential schedule (5.07-5.14 vs 4.50 ms per push), so
-    // it stays off by default.
-    hipDeviceProp_t prop;
-    static const bool ov_on = [] {
-      const char *v = getenv("FVAD_FP16_OVERLAP");
-      return v && atoi(v) != 0;
-    }();
-    if (c.mode == FVAD_MODE_FP16 && c.use_denoiser && ov_on && !mask_cus(c) &&
-        hipGetDeviceProperties(&prop, c.device) == hipSuccess) {
-      overlap_masks(prop.multiProcessorCount, e->mask_a, e->mask_b);
-      int na = 0;
-      for (uint32_t w : e->mask_a) na += __builtin_popcount(w);
-      for (uint32_t w : e->mask_b) e->n_cu_b += __builtin_popcount(w);
-      e->overlap = (c.n_streams + 15) / 16 <= na && e->n_cu_b > 0;
-    }
-  }
-  if (make_stream(e, &e->stream) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
-  if (e->overlap &&
-      (make_stream(e, &e->gstream, e->mask_a) != hipSuccess || make_stream(e, &e->sstream, e->mask_b) != hipSuccess ||
-       hipEventCreateWithFlags(&e->ev_ov[0], hipEventDisableTiming) != hipSuccess ||
-       hipEventCreateWithFlags(&e->ev_ov[1], hipEventDisableTiming) != hipSuccess ||
-       hipEventCreateWithFlags(&e->ev_ov[2], hipEventDisableTiming) != hipSuccess))
-    return bail(fail(FVAD_EDEVICE, "overlap stream creation failed"));
+  if (make_stream(&e->stream) != hipSuccess) return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
   if (c.mode != FVAD_MODE_FUSED &&
-      (make_stream(e, &e->pstream, e->overlap ? e->mask_b : nullptr) != hipSuccess ||
+      (make_stream(&e->pstream) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[0], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[1], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_buf_free[0], hipEventDisableTiming) != hipSuccess ||
@@ -594,11 +541,10 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
         (rc = dalloc(&e->d_gr, F * fvad::kBands)) || (rc = dalloc(&e->d_gs, F * fvad::kBands)))
       return bail(rc);
     e->d_xs = e->d_xs_b[0];
-    if (e->overlap && (rc = dalloc(&e->d_gate, 1 + (B + 15) / 16))) return bail(rc);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return bail(fail(FVAD_EDEVICE, "device query failed"));
     // CUs; persistent grids are sized per kernel
-    e->grid_frames = mask_cus(c) ? std::min(mask_cus(c), prop.multiProcessorCount) : prop.multiProcessorCount;
+    e->grid_frames = prop.multiProcessorCount;
     // k_fftb's device scratch when a transform does not fit in LDS: a slice per
     // workgroup, at most two per CU and 1 GiB
     int lo = 0, hi = 0, band_lo[fvad::kMaxBandCfg], band_hi[fvad::kMaxBandCfg];
@@ -675,19 +621,9 @@ int launch_fused(fvad_engine *e, int n_ticks, bool use_ticks, bool timed) {
 
 }  // namespace
 
-// a cross-stream wait; FVAD_WAIT_SKIP=1 skips it when the event has already
-// completed (the host usually runs a push or more ahead, so the main
-// stream's waits on the push k - 2 VADMachine and the buffer releases are
-// often long satisfied; each queued wait is a barrier packet at the push
-// boundary)
-hipError_t wait_event(hipStream_t stream, hipEvent_t ev) {
-  static const bool skip = [] {
-    const char *v = getenv("FVAD_WAIT_SKIP");
-    return v && atoi(v) == 1;
-  }();
-  if (skip && hipEventQuery(ev) == hipSuccess) return hipSuccess;
-  return hipStreamWaitEvent(stream, ev, 0);
-}
+// a cross-stream wait (skipping the ones already complete measured no gain:
+// DESIGN §8 r4)
+hipError_t wait_event(hipStream_t stream, hipEvent_t ev) { return hipStreamWaitEvent(stream, ev, 0); }
 
 // k_vadm of one push on the side stream (its waits already queued), with
 // its timing pair and the events later pushes wait for
@@ -780,7 +716,6 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   a.win_start = e->d_wstart;
   a.wmax = e->wmax;
   a.wpt = e->wpt;
-  a.gate = e->overlap ? e->d_gate : nullptr;
   if (e->d_fbtab) {  // fft_size > kMaxFftB: [tw | sup | hann | perm] (fvad_engine_create)
     const size_t n = c.fft_size;
     a.fb_tw = reinterpret_cast<const float2 *>(e->d_fbtab);
@@ -803,13 +738,6 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   fill_bands(c, a.band_lo, a.band_hi, &a.bin_lo_all, &a.bin_hi_all);
   a.nfft_b = c.fft_size;
   a.use_denoiser = c.use_denoiser;
-  // wave kernels with static batch striding (bit 1 << fvad::WaveKernel):
-  // k_pspecw and k_synthw by default; FVAD_WSTATIC=<mask> overrides
-  static const int wstatic = [] {
-    const char *v = getenv("FVAD_WSTATIC");
-    return v ? atoi(v) : (1 << fvad::kWavePspec) | (1 << fvad::kWaveSynth);
-  }();
-  a.wave_static = wstatic;
   a.out_vad = e->d_vad;
   a.out_win_ratio = e->d_wratio;
   a.out_win_vad = e->d_wvad;
@@ -825,9 +753,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     HIP_TRY(wait_event(e->stream, e->ev_prep_done[b]));
     // window output set b is free once push k-2's k_vadm_hbm has read it
     if (e->vadm.n > 0) HIP_TRY(wait_event(e->stream, e->ev_vadm_b[b]));
-    fvad::Overlap ov{e->gstream, e->sstream, e->ev_ov[0], e->ev_ov[1], e->ev_ov[2], e->n_cu_b,
-                     sizeof(unsigned) * (1 + (size_t)(c.n_streams + 15) / 16)};
-    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr, e->overlap ? &ov : nullptr));
+    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr));
   } else {
     // no denoiser: raw input frames to the ring, windows, FFT B, all on the
     // engine stream after the input copy (queued on the prep stream)
@@ -1273,6 +1199,9 @@ extern "C" int fvad_engine_load_synthetic(fvad_engine *e, int n_ticks, uint32_t 
 // n_pushes * n_ticks ticks of fvad_synth_stream(base + s) (generated at that
 // length).  One push lives in the input buffer d_pcm_b[0]; more get their own
 // [push][tick][stream][ch][480] buffer, and run_resident cycles through them.
+// Host memory stays bounded: groups of kGroup streams are generated and copied
+// (one strided copy per group: a group's rows of every tick), never the whole
+// block.
 extern "C" int fvad_engine_load_synthetic_ex(fvad_engine *e, int n_ticks, int n_pushes, uint32_t base) {
   if (!e) return fail(FVAD_EINVAL, "null engine");
   const fvad_engine_config &c = e->cfg;
@@ -1280,13 +1209,14 @@ extern "C" int fvad_engine_load_synthetic_ex(fvad_engine *e, int n_ticks, int n_
   if (n_pushes < 1 || (long long)n_ticks * n_pushes > (1LL << 30))
     return fail(FVAD_EINVAL, "1 <= n_pushes and n_ticks * n_pushes <= 2^30 required");
   HIP_TRY(hipSetDevice(c.device));
-  const size_t per_push = (size_t)n_ticks * c.n_streams * c.n_channels * fvad::kFrame;
+  const size_t row = (size_t)c.n_channels * fvad::kFrame;  // floats of one (tick, stream)
+  const size_t per_push = (size_t)n_ticks * c.n_streams * row;
   const int total = n_ticks * n_pushes;
-  // one push at a time through a staging buffer (the generator keeps its own
-  // cache of the whole block for the next engine of the same workload)
+  constexpr int kGroup = 64;
+  const int gs = std::min(kGroup, c.n_streams);
   std::vector<float> host;
   try {
-    host.resize(per_push);
+    host.resize((size_t)total * gs * row);
   } catch (...) {
     return fail(FVAD_ENOMEM, "host buffer for the synthetic input");
   }
@@ -1299,11 +1229,15 @@ extern "C" int fvad_engine_load_synthetic_ex(fvad_engine *e, int n_ticks, int n_
   }
   e->res_pushes = 0;
   if (n_pushes > 1 && (rc = dalloc(&e->d_res, per_push * n_pushes))) return rc;
-  for (int k = 0; k < n_pushes; k++) {
-    if ((rc = fvad_synth_ticks(base, c.n_streams, c.n_channels, total, k * n_ticks, n_ticks, host.data())))
-      return fail(rc, "fvad_synth_ticks failed");
-    float *dst = n_pushes == 1 ? e->d_pcm_b[0] : e->d_res + per_push * (size_t)k;
-    HIP_TRY(hipMemcpy(dst, host.data(), per_push * sizeof(float), hipMemcpyHostToDevice));
+  // [push][tick][stream] rows are [global tick][stream] rows: tick g = k * n_ticks + t
+  float *dst = n_pushes == 1 ? e->d_pcm_b[0] : e->d_res;
+  for (int s0 = 0; s0 < c.n_streams; s0 += gs) {
+    const int ns = std::min(gs, c.n_streams - s0);
+    if ((rc = fvad_synth_group(base, s0, ns, c.n_channels, total, 0, total, host.data(), (size_t)ns)))
+      return fail(rc, "synthetic input generation failed");
+    HIP_TRY(hipMemcpy2D(dst + (size_t)s0 * row, (size_t)c.n_streams * row * sizeof(float), host.data(),
+                        (size_t)ns * row * sizeof(float), (size_t)ns * row * sizeof(float), (size_t)total,
+                        hipMemcpyHostToDevice));
   }
   if (n_pushes > 1) e->res_pushes = n_pushes;
   e->res_next = 0;
@@ -1411,8 +1345,6 @@ extern "C" int fvad_engine_fetch(fvad_engine *e, int n_ticks, fvad_outputs *out)
 
 extern "C" int fvad_engine_windows_per_tick(const fvad_engine *e) { return e ? e->wpt : FVAD_EINVAL; }
 
-extern "C" int fvad_engine_fp16_overlap(const fvad_engine *e) { return e ? (int)e->overlap : FVAD_EINVAL; }
-
 extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
   if (e && i == e->n_kernels && e->vadm.n > 0) return "k_vadm_hbm";
   if (e && i == e->n_kernels + 1 && e->vadm.n > 0) return "k_vadm_par";
@@ -1512,7 +1444,7 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
       (rc = dalloc(&e->d_vband, TBW * e->cfg.n_channels * e->cfg.n_bands)) || (rc = dalloc(&e->d_vticks, (size_t)B)) ||
       (rc = dalloc(&e->d_vticks_b[1], (size_t)B)))
     return rc;
-  if (make_stream(e, &e->side, e->overlap ? e->mask_b : nullptr) != hipSuccess ||
+  if (make_stream(&e->side) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_vadm, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&e->ev_vt[0][0]) != hipSuccess || hipEventCreate(&e->ev_vt[0][1]) != hipSuccess ||

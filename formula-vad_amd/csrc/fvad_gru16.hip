@@ -299,7 +299,7 @@ __device__ __forceinline__ void epi_h(Lds &L, const f4 &acc, int tile, int lane,
 // kSpw = the streams a workgroup owns (<= kGS; the MFMA columns past it stay
 // inactive).  8 puts 256 workgroups on the 256 CUs at 2048 streams instead of
 // 128: k_gru16 0.554 -> 0.530 ms (latency-bound supersteps, the same per
-// workgroup); the overlap mode's gates count 16-stream groups and keep 16.
+// workgroup).
 template <int kSpw>
 __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
   static_assert(kSpw > 0 && kSpw <= kGS, "streams per k_gru16 workgroup");
@@ -574,15 +574,8 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
           const float al = .6f * L.lastg[s][i];
           const float gsm = (gi > al) ? gi : al;
           L.lastg[s][i] = gsm;
-          if (a.gate) {
-            // fp16 overlap: read by the synthesis on other CUs (other XCDs'
-            // L2s) before this kernel ends -- write-through (sc1) stores
-            __hip_atomic_store(&a.gr[f * kBands + i], gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.gs[f * kBands + i], gsm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          } else {
-            a.gr[f * kBands + i] = gi;
-            a.gs[f * kBands + i] = gsm;
-          }
+          a.gr[f * kBands + i] = gi;
+          a.gs[f * kBands + i] = gsm;
         }
       }
     } else {
@@ -599,24 +592,9 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     }
     if (pf_lane) L.pf[pfs][pfi] = pf_next;  // read by the next phase A only
     WSTAMP_END(1);
-    if (a.gate) {
-      // fp16 overlap: the gains of frames <= u - 4 are final; publish them to
-      // the synthesis waves on the other CUs: the gains went out write-through
-      // (sc1) and the barrier drained every wave's stores (vmcnt(0)), so the
-      // flag -- also a write-through store -- follows them to memory.  (An
-      // agent-scope release fence here wrote back the whole L2 of the XCD
-      // every superstep: k_gru16 0.56 -> 1.17 ms.)
-      __syncthreads();
-      if (tid == 0)
-        __hip_atomic_store(&a.gate[1 + blockIdx.x], (unsigned)max(0, u - 3), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      lds_sync();
-    }
+    lds_sync();
     RSTAMP(1);
   }
-  if (a.gate && tid == 0)  // (the last superstep's barrier drained the stores)
-    __hip_atomic_store(&a.gate[1 + blockIdx.x], 0x7fffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef FVAD_STAMPS
   if (lane == 0 && a.stamps) {
     atomicAdd(&a.stamps[W], wacc[0]);
@@ -652,10 +630,7 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
 }
 
 hipError_t launch_gru16(const StagedArgs &a, hipStream_t stream) {
-  if (a.gate)  // the overlap gates count 16-stream groups
-    hipLaunchKernelGGL(k_gru16<kGS>, dim3((a.n_streams + kGS - 1) / kGS), dim3(kGNT), 0, stream, a);
-  else
-    hipLaunchKernelGGL(k_gru16<8>, dim3((a.n_streams + 7) / 8), dim3(kGNT), 0, stream, a);
+  hipLaunchKernelGGL(k_gru16<8>, dim3((a.n_streams + 7) / 8), dim3(kGNT), 0, stream, a);
   return hipGetLastError();
 }
 

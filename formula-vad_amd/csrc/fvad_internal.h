@@ -167,3 +167,9 @@ void build_plan(Plan *p, int nfft_b);
 float build_fftb_tables(int nfft_b, const int *fac, float *twb, float *superb, int *permb, float *hannb);
 
 }  // namespace fvad
+
+// Synthetic streams base + s0 .. base + s0 + ns - 1 (each generated with length
+// total_ticks * 480) in push layout: ticks [tick0, tick0 + n_ticks) to
+// out[t][s][c][480] with out_streams streams per tick row (fvad_synth.cpp)
+int fvad_synth_group(uint32_t base, int s0, int ns, int n_channels, int total_ticks, int tick0, int n_ticks,
+                     float *out, std::size_t out_streams);

@@ -62,14 +62,11 @@ constexpr int kPcF = 8;                // frames per workgroup (a quarter tile h
 constexpr int kPcL = 32;               // lanes per frame in Q1 (16: 188 VGPRs, 2 waves per SIMD, 3 % slower)
 constexpr int kPcNT = kPcL * kPcF;
 static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
-#ifndef FVAD_Q1_B64
-#define FVAD_Q1_B64 0
-#endif
+// FVAD_DIAG_SKIP (bit 1 Q1, 2 Q3, 4 Q5): diagnostic flavours without that
+// phase's sums, for the per-phase LDS attribution (`make diag`,
+// tools/lds_attr.sh); never set in the product build
 #ifndef FVAD_DIAG_SKIP
 #define FVAD_DIAG_SKIP 0
-#endif
-#ifndef FVAD_Q5_COMPACT
-#define FVAD_Q5_COMPACT 1
 #endif
 constexpr int kPcXS = 870;  // xf row pitch: even (8-byte aligned pairs in Q5), = 6 mod 8 (conflict-free Q0 stores)
 constexpr int kPcSP = 153;  // coarse xcorr / Syy row pitch (odd; >= 147 rounded up to the scan block)
@@ -238,22 +235,9 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         const float *X = xf[fr] + (kPitchMax >> 1);
         const float *Y = xf[fr] + 2 * k0;
         float win[R];
-#if FVAD_Q1_B64
-        // y values as the low half of an 8-byte read: lanes 10 floats apart
-        // fall on distinct 64-bank pairs (ds_read_b64), where 4-byte reads
-        // (32-bank map) collide two to a bank
-        auto yld = [&](int m) -> float {
-          float2 p = *reinterpret_cast<const float2 *>(Y + 2 * m);
-          asm volatile("" : "+v"(p));
-          return p.x;
-        };
-#else
         auto yld = [&](int m) -> float { return Y[2 * m]; };
-#endif
 #pragma unroll
         for (int r = 0; r < R; r++) win[r] = yld(r);
-        // (FVAD_DIAG_SKIP & 1: diagnostic builds without this phase's sums, for
-        // the per-phase LDS attribution of tools/_r4_ldsattr.sh; never the product)
         for (int jb = 0; jb < ((FVAD_DIAG_SKIP & 1) ? 0 : 240); jb += R) {
 #pragma unroll
           for (int u = 0; u < R; u++) {
@@ -533,7 +517,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
     // waits for LDS only (not for this group's record stores)
     long long g_next = 0;
     if (tq == 0) g_next = take_group(a, kWorkPcorr);
-#if FVAD_Q5_COMPACT
     // items packed in frame order from lane 0 (window items c = 0..nv on
     // waves 0-1, T1b items c = 1..nv on waves 2-3): ~7.6 items per frame fill
     // one wave of each pair, the other usually has none and skips the walk
@@ -552,10 +535,6 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
         base += n;
       }
     }
-#else
-    const int q5f = q5i / 15, q5c = q5i - 15 * q5f;
-    const bool q5on = q5i < 15 * kPcF && fval[q5f] && (q5c == 0 ? !q5b : q5c - 1 < nvs[q5f]);
-#endif
     float aM = 0, a0 = 0, aP = 0;
     int q5T0 = 0, q5Tc = 0, q5Tb = 0;
     if ((FVAD_PC_PRIO & 1) && q5on) __builtin_amdgcn_s_setprio(2);

@@ -109,7 +109,6 @@ struct StagedArgs {
   int n_bands;
   int nfft_b;                  // FFT B size (fft_size)
   int use_denoiser;            // 0: raw fft_size frames straight to FFT B (launch_nodenoise)
-  int wave_static;             // wave kernels with static batch striding: bit 1 << WaveKernel
   int band_lo[kMaxBandCfg], band_hi[kMaxBandCfg];
   int bin_lo_all, bin_hi_all;
   // per (tick, stream): out_vad, out_win_flag (windows completed in the tick,
@@ -120,10 +119,6 @@ struct StagedArgs {
   int raw_s16;
   VadmArgs vadm;
   unsigned *work;          // [kWorkCounters] dynamic group counters of the persistent kernels
-  // fp16 overlap (FVAD_MODE_FP16, engine option): null, or [0] the gated
-  // synthesis queue and [1 + g] GRU workgroup g's progress (frames whose gains
-  // are final), zeroed before the push's k_gru16 / k_synthw
-  unsigned *gate;
   unsigned long long *stamps;  // diagnostic build only (FVAD_STAMPS): per-phase cycles of k_rnn3
 };
 
@@ -137,17 +132,7 @@ constexpr int kStagedTime[kStagedKernels][2] = {{0, 1}, {2, 3},   {14, 4},  {4, 
 hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev);
 // Launch the other 10 kernels; when ev != nullptr their timing events are
 // recorded.
-// fp16 overlap (FVAD_MODE_FP16): k_gru16 on stream g (a CU mask of its own),
-// the gated k_synthw beside it on stream s (the other CUs, n_cu_s of them),
-// then a second k_synthw instance on every CU once the GRU is done; a.gate set
-struct Overlap {
-  hipStream_t g, s;
-  hipEvent_t ev_p, ev_g, ev_s;
-  int n_cu_s;
-  size_t gate_bytes;
-};
-hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev,
-                         const Overlap *ov = nullptr);
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev);
 // k_pcorr over `tiles` pitch tiles (fvad_pitch.hip)
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream);
 const char *staged_kernel_name(int i);

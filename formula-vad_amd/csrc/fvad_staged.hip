@@ -1001,21 +1001,6 @@ __device__ __forceinline__ void rnn_cand(const int8_t *W, const RnnIn &in, const
 #ifndef FVAD_PRIO
 #define FVAD_PRIO 134
 #endif
-#ifndef FVAD_GVPRE
-#define FVAD_GVPRE 1
-#endif
-// FVAD_FD4: the denoise GRU one step further behind (frame t-4 at step t), so
-// the denoise candidates' whole input prefix (b + the 114 input terms) runs in
-// the P2 before its step, beside the lighter candidate roles, and the denoise
-// z|r gates' first segment moves to P1's freed waves (zpre double-buffered).
-// Bit-exact, but measured k_rnn3 1.12 -> 1.21 ms (P2 lengthens more than P1
-// shortens): off
-#ifndef FVAD_FD4
-#define FVAD_FD4 0
-#endif
-#if FVAD_FD4 && !FVAD_GVPRE
-#error "FVAD_FD4 needs FVAD_GVPRE"
-#endif
 constexpr int kR3S = 8, kR3G = 2, kR3NT = 1024;
 __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   constexpr int S = kR3S, G = kR3G, NT = kR3NT;
@@ -1027,7 +1012,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     alignas(16) float gdT[2][96 * S];
     alignas(16) float zrv[48 * S], zrn[96 * S], zrd[192 * S];
     alignas(16) float dhp[2][96 * S];  // denoise candidate input prefixes of frame f in slot f & 1
-    alignas(16) float zpre[2][192 * S];  // denoise z|r: b + the vad-state segment of frame f in slot f & 1
+    alignas(16) float zpre[192 * S];  // denoise z|r: b + the vad-state segment of the frame P1 continues
     alignas(16) float gout[2][22 * S];  // denoise_output of frame f in slot f & 1
     alignas(16) float vo[S];  // vad_output of the frame P2 computed last
     float tt[204];
@@ -1178,8 +1163,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
   // dense of frame t wave 7 (48), vad_output wave 8 (2 lanes), features of
   // frame t+1 waves 9..11 (296 items, two per lane on the first 104), the
   // denoise z|r first segments of frame t-2 waves 12..14 (384 tasks, two per
-  // lane), the denoise candidates' wave 15 (192, three per lane); without
-  // FVAD_GVPRE the features take waves 9..13.  (Denoise h with 2 streams per lane on
+  // lane), the denoise candidates' wave 15 (192, three per lane).  (Denoise h with 2 streams per lane on
   // 6 waves shortened its chain to 11.1 k cycles but the extra waves
   // stretched the other roles: 15.3 vs 14.6 k per phase.)
   [[maybe_unused]] constexpr int kP2Den = 0, kP2Noise = 192, kP2Vad = 320, kP2Dense = 448, kP2Out = 256, kP2VadOut = 512,
@@ -1228,13 +1212,13 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       a.gs[f * kBands + i] = gsm;
     }
   };
-  for (int t = 0; t <= maxnf + 4 + FVAD_FD4; t++) {
+  for (int t = 0; t <= maxnf + 4; t++) {
     // per-step opaque thread id: the roles' per-thread offsets are recomputed
     // each step instead of hoisted out of the frame loop, where they spilled
     // (128 VGPRs + 34 spilled -> 112, no scratch: 1.27 -> 1.23-1.24 ms)
     int tq = tid;
     asm volatile("" : "+v"(tq));
-    const int fv = t - 1, fn = t - 2, fd = t - 3 - FVAD_FD4;
+    const int fv = t - 1, fn = t - 2, fd = t - 3;
     ROLE_BEGIN();
     // frame t+1's raw features, staged at the end of P1 for P2's feat_c:
     // issued here, so no load is outstanding across a step boundary (a
@@ -1244,9 +1228,8 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     const int wv = tq >> 6, ln = tq & 63;
     if (wv < 6) {
       if (fd >= 0 && fd < maxnf)
-        rnn_gates<5, S, G, 0, FVAD_GVPRE ? 5 : 0>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]},
-                                                  L.gdT[(fd + 1) & 1], L.zrd, kActSigmoid, L.tt, tq,
-                                                  L.zpre[FVAD_FD4 ? (fd & 1) : 0]);
+        rnn_gates<5, S, G, 0, 5>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, L.gdT[(fd + 1) & 1],
+                                 L.zrd, kActSigmoid, L.tt, tq, L.zpre);
     } else if (wv == 6 || wv == 7 || wv == 10) {
       if (fn >= 0 && fn < maxnf)
         rnn_gates<3, S, G, 0>(L.W, RnnIn{L.doutT[fn & 3], L.gvT[fn & 3], L.featT[fn & 7]}, L.gnT[(fn + 1) & 1], L.zrn,
@@ -1256,22 +1239,12 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
         rnn_gates<1, S, G, 0>(L.W, RnnIn{L.doutT[fv & 3], nullptr, nullptr}, L.gvT[(fv + 3) & 3], L.zrv, kActSigmoid,
                               L.tt, (wv == 14 ? 64 : 0) + ln);
     } else if (wv == 12 || wv == 13 || wv == 15) {
-#if FVAD_FD4
-      // denoise z|r first segment (b + the vad-state terms) of frame t-3,
-      // two tasks per lane, for the next step's P1
-      const int fz = t - 3;
-      if (fz >= 0 && fz < maxnf)
-        rnn_gates<5, S, G, 192, 3>(L.W, RnnIn{L.gvT[fz & 3], nullptr, nullptr}, nullptr, nullptr, kActSigmoid, L.tt,
-                                   (wv == 15 ? 128 : 64 * (wv - 12)) + ln, L.zpre[fz & 1]);
-#else
       // denoise candidate input prefixes of frame t-3
       if (fd >= 0 && fd < maxnf)
-        rnn_cand<6, S, G, 0, FVAD_GVPRE ? 4 : 1>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, nullptr,
-                                                 nullptr, nullptr, nullptr, 0, nullptr,
-                                                 (wv == 15 ? 128 : 64 * (wv - 12)) + ln, L.dhp[fd & 1]);
-#endif
-    } else if (wv == 8 && ln < 48) {  // gain smoothing of frame t-5 (t-6 with FVAD_FD4)
-      gains(t - 5 - FVAD_FD4, ln, 48);
+        rnn_cand<6, S, G, 0, 4>(L.W, RnnIn{L.gvT[fd & 3], L.gnT[fd & 1], L.featT[fd & 7]}, nullptr, nullptr, nullptr,
+                                nullptr, 0, nullptr, (wv == 15 ? 128 : 64 * (wv - 12)) + ln, L.dhp[fd & 1]);
+    } else if (wv == 8 && ln < 48) {  // gain smoothing of frame t-5
+      gains(t - 5, ln, 48);
     } else if (wv == 9 && ln < S) {  // spectral variability of frame t (features: P2 of step t-1)
       if (t < maxnf) feat_d(t, ln);
     } else if (wv == 8 && ln >= 48 && ln < 48 + S) {  // vad_output of frame t-3 (P2 of step t-1)
@@ -1284,7 +1257,7 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     RSTAMP(0);
     ROLE_BEGIN();
     // ---- P2
-    const int fo = t - 4 - FVAD_FD4;
+    const int fo = t - 4;
     if (wv < 3) {
       if (fd >= 0 && fd < maxnf)
         rnn_cand<6, S, G, 0, 2>(L.W, RnnIn{nullptr, nullptr, nullptr}, L.gdT[(fd + 1) & 1], L.zrd, L.gdT[fd & 1],
@@ -1315,25 +1288,13 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
       // vad_output(t-2) -> L.vo, stored by the next step's P1
       if (fn >= 0 && fn < maxnf)
         rnn_gates<8, S, G, 0>(L.W, RnnIn{L.gvT[fn & 3], nullptr, nullptr}, nullptr, L.vo, ra[8], L.tt, ln);
-#if FVAD_FD4
-    } else if (tq >= kP2Feat && tq < kP2Feat + 192) {  // features of t+1 on waves 9..11
-      for (int idx = tq - kP2Feat; t + 1 < maxnf && idx < kFeatItems; idx += 192) feat_c(t + 1, idx);
-    } else if (wv >= 12 && wv <= 14) {
-      // denoise candidates of frame t-3: b + the 114 input terms (they do not
-      // need the reset gate), one task per lane, for the next step's P2
-      const int fz = t - 3;
-      if (fz >= 0 && fz < maxnf)
-        rnn_cand<6, S, G, 192, 1>(L.W, RnnIn{L.gvT[fz & 3], L.gnT[fz & 1], L.featT[fz & 7]}, nullptr, nullptr, nullptr,
-                                  nullptr, 0, nullptr, tq - 768, L.dhp[fz & 1]);
-    }
-#elif FVAD_GVPRE
     } else if (tq >= kP2Feat && tq < kP2Feat + 192) {  // features of t+1 on waves 9..11
       for (int idx = tq - kP2Feat; t + 1 < maxnf && idx < kFeatItems; idx += 192) feat_c(t + 1, idx);
     } else if (wv >= 12 && wv <= 14) {  // denoise z|r of frame t-2: b + the vad-state segment
       const int fz = t - 2;
       if (fz >= 0 && fz < maxnf)
         rnn_gates<5, S, G, 192, 3>(L.W, RnnIn{L.gvT[fz & 3], nullptr, nullptr}, nullptr, nullptr, kActSigmoid, L.tt,
-                                   tq - 768, L.zpre[0]);
+                                   tq - 768, L.zpre);
     } else if (wv == 15) {  // denoise candidates of frame t-2: b + the vad-state segment
       const int fz = t - 2;
       if (FVAD_PRIO & 128) __builtin_amdgcn_s_setprio(2);
@@ -1342,11 +1303,6 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
                                  nullptr, ln, L.dhp[fz & 1]);
       if (FVAD_PRIO & 128) __builtin_amdgcn_s_setprio(0);
     }
-#else
-    } else if (tq >= kP2Feat && tq < kP2Feat + kFeatItems) {
-      if (t + 1 < maxnf) feat_c(t + 1, tq - kP2Feat);
-    }
-#endif
     ROLE_END(1);
     lds_sync();
     RSTAMP(1);
@@ -2256,7 +2212,7 @@ hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) 
   return hipSuccess;
 }
 
-hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev, const Overlap *ov) {
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev) {
   static const int p_plpc = blocks_per_cu(k_plpc, 256);
   const int g_plpc = p_plpc * n_cu;
   const long long frames = (long long)a.n_streams * a.V;
@@ -2291,31 +2247,12 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   REC(7);
   FVAD_LAUNCH_TRY(launch_wave(kWavePspec, a, n_cu, stream));
   REC(8);
-  if (ov) {
-    // fp16 overlap: the GRU on its own CUs, the synthesis of the frames whose
-    // gains it has published on the others meanwhile, the rest on every CU
-    // after it (the k_gru16 events bracket the GRU, the k_synthw ones the
-    // synthesis left once the GRU is done)
-    FVAD_LAUNCH_TRY(hipMemsetAsync(a.gate, 0, ov->gate_bytes, stream));
-    FVAD_LAUNCH_TRY(hipEventRecord(ov->ev_p, stream));
-    FVAD_LAUNCH_TRY(hipStreamWaitEvent(ov->g, ov->ev_p, 0));
-    FVAD_LAUNCH_TRY(hipStreamWaitEvent(ov->s, ov->ev_p, 0));
-    FVAD_LAUNCH_TRY(launch_gru16(a, ov->g));
-    if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[9], ov->g));
-    FVAD_LAUNCH_TRY(hipEventRecord(ov->ev_g, ov->g));
-    FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, ov->n_cu_s, ov->s));
-    FVAD_LAUNCH_TRY(hipEventRecord(ov->ev_s, ov->s));
-    FVAD_LAUNCH_TRY(hipStreamWaitEvent(stream, ov->ev_g, 0));
-    FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
-    FVAD_LAUNCH_TRY(hipStreamWaitEvent(stream, ov->ev_s, 0));
-  } else {
-    if (a.gru16_frags)  // FVAD_MODE_FP16: the GRU stack on the matrix cores (configs[4])
-      FVAD_LAUNCH_TRY(launch_gru16(a, stream));
-    else
-      FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
-    REC(9);
-    FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
-  }
+  if (a.gru16_frags)  // FVAD_MODE_FP16: the GRU stack on the matrix cores (configs[4])
+    FVAD_LAUNCH_TRY(launch_gru16(a, stream));
+  else
+    FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
+  REC(9);
+  FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
   REC(10);
   if (olafb_fused(a)) {
     // overlap-add, window bookkeeping and FFT B in one kernel (k_olafb);

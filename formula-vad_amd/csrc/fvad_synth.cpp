@@ -177,70 +177,53 @@ extern "C" long fvad_synth_stream(uint32_t stream_id, size_t n, int n_ch, float 
 // The same streams in the engine's push layout: ticks [tick0, tick0 + n_ticks)
 // of streams base .. base + n_streams - 1, each generated with length
 // total_ticks * 480 (the generator's output depends on the length), written
-// as out[t][s][c][480].  Generation runs on up to 16 host threads; the last
-// whole [total_ticks][streams][channels][480] block is cached, so the bench's
-// second engine (and its host-buffer leg) reuse it instead of regenerating
-// ~1 G samples.
+// as out[t][s][c][480].  Nothing is cached (a rank of an 8-GPU run would
+// otherwise hold its whole 7.9 GB synthetic block for the job): streams are
+// generated in groups on up to 16 host threads, each thread holding one
+// stream at a time.
 namespace {
-struct SynthCache {
-  std::mutex mu;
-  uint32_t base = 0;
-  int n_streams = 0, n_channels = 0, total_ticks = 0;
-  std::vector<float> data;  // [total_ticks][n_streams][n_channels][480]
-};
-SynthCache &synth_cache() {
-  static SynthCache c;
-  return c;
-}
+unsigned synth_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
 }  // namespace
+
+int fvad_synth_group(uint32_t base, int s0, int ns, int n_channels, int total_ticks, int tick0, int n_ticks,
+                     float *out, size_t out_streams) {
+  constexpr size_t F = fvad::kFrame;
+  const size_t C = (size_t)n_channels, n = (size_t)total_ticks * F;
+  const unsigned nthr = std::min<unsigned>(synth_threads(), (unsigned)ns);
+  std::vector<std::thread> pool;
+  bool oom = false;
+  std::mutex mu;
+  for (unsigned w = 0; w < nthr; w++) {
+    pool.emplace_back([&, w]() {
+      std::vector<float> one;
+      try {
+        one.resize(C * n);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu);
+        oom = true;
+        return;
+      }
+      for (int s = (int)w; s < ns; s += (int)nthr) {
+        fvad_synth_stream(base + (uint32_t)(s0 + s), n, (int)C, one.data(), nullptr, 0);
+        for (size_t t = 0; t < (size_t)n_ticks; t++)
+          for (size_t ch = 0; ch < C; ch++)
+            std::memcpy(out + ((t * out_streams + (size_t)s) * C + ch) * F, one.data() + ch * n + (tick0 + t) * F,
+                        F * sizeof(float));
+      }
+    });
+  }
+  for (auto &th : pool) th.join();
+  return oom ? FVAD_ENOMEM : FVAD_OK;
+}
 
 extern "C" int fvad_synth_ticks(uint32_t base, int n_streams, int n_channels, int total_ticks, int tick0,
                                 int n_ticks, float *out) {
   if (n_streams < 1 || n_channels < 1 || total_ticks < 1 || tick0 < 0 || n_ticks < 0 ||
       tick0 + n_ticks > total_ticks || (!out && n_ticks))
     return FVAD_EINVAL;
-  constexpr size_t F = fvad::kFrame;
-  const size_t B = (size_t)n_streams, C = (size_t)n_channels, n = (size_t)total_ticks * F;
-  SynthCache &sc = synth_cache();
-  std::lock_guard<std::mutex> lock(sc.mu);
-  if (sc.base != base || sc.n_streams != n_streams || sc.n_channels != n_channels || sc.total_ticks != total_ticks ||
-      sc.data.empty()) {
-    sc.data.clear();
-    sc.data.shrink_to_fit();
-    try {
-      sc.data.resize((size_t)total_ticks * B * C * F);
-    } catch (...) {
-      sc.n_streams = 0;
-      return FVAD_ENOMEM;
-    }
-    unsigned nthr = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::thread> pool;
-    float *dst = sc.data.data();
-    for (unsigned w = 0; w < nthr; w++) {
-      pool.emplace_back([=]() {
-        std::vector<float> one(C * n);
-        for (size_t s = w; s < B; s += nthr) {
-          fvad_synth_stream(base + (uint32_t)s, n, (int)C, one.data(), nullptr, 0);
-          for (size_t t = 0; t < (size_t)total_ticks; t++)
-            for (size_t ch = 0; ch < C; ch++)
-              std::memcpy(dst + ((t * B + s) * C + ch) * F, one.data() + ch * n + t * F, F * sizeof(float));
-        }
-      });
-    }
-    for (auto &th : pool) th.join();
-    sc.base = base;
-    sc.n_streams = n_streams;
-    sc.n_channels = n_channels;
-    sc.total_ticks = total_ticks;
-  }
-  if (n_ticks) std::memcpy(out, sc.data.data() + (size_t)tick0 * B * C * F, (size_t)n_ticks * B * C * F * sizeof(float));
-  return FVAD_OK;
+  if (!n_ticks) return FVAD_OK;
+  return fvad_synth_group(base, 0, n_streams, n_channels, total_ticks, tick0, n_ticks, out, (size_t)n_streams);
 }
 
-extern "C" void fvad_synth_cache_clear(void) {
-  SynthCache &sc = synth_cache();
-  std::lock_guard<std::mutex> lock(sc.mu);
-  sc.data.clear();
-  sc.data.shrink_to_fit();
-  sc.n_streams = 0;
-}
+// (kept for the ABI: nothing is cached since r5)
+extern "C" void fvad_synth_cache_clear(void) {}

@@ -30,14 +30,13 @@ namespace fvad {
 constexpr int kWB = 8;   // frames per wave batch
 constexpr int kWNW = 4;  // waves per workgroup
 constexpr int kWOcc = 3;  // workgroups per CU (<= 168 VGPRs, <= 53 KB LDS)
-constexpr int kGruS = 16;  // streams per k_gru16 workgroup (fvad_gru16.hip kGS)
-
 
 // Batches of a wave: dynamic (per-XCD queues, wave_take) or static striding
-// over the grid's waves, per kernel (a.wave_static bit 1 << kind).  k_fftAw
+// over the grid's waves, per kernel (bit 1 << kind of kWaveStatic).  k_fftAw
 // runs beside the next push's k_prep3 and balances better dynamically; the
 // others run alone, where static striding saves the queue atomics.
-__device__ __forceinline__ bool wave_is_static(const StagedArgs &a, WaveKernel k) { return (a.wave_static >> k) & 1; }
+constexpr int kWaveStatic = (1 << kWavePspec) | (1 << kWaveSynth);
+__device__ __forceinline__ bool wave_is_static(const StagedArgs &, WaveKernel k) { return (kWaveStatic >> k) & 1; }
 __device__ __forceinline__ long long wave_first(const StagedArgs &a, WaveKernel k, int slot, int lane) {
   return wave_is_static(a, k) ? (long long)blockIdx.x * kWNW + (threadIdx.x >> 6) : wave_take(a, slot, lane);
 }
@@ -314,36 +313,9 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
   float *tr = reinterpret_cast<float *>(R);
   float *rr = bp[wv][0], *nrm = bp[wv][1], *gsm = bp[wv][2];
   const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
-  // fp16 overlap (a.gate): batches tick-major from one queue -- batch b is
-  // frames 8 (b / B) .. + 7 of stream b % B -- each once its GRU workgroup has
-  // published their gains; this kernel runs on the CUs k_gru16 does not use,
-  // and a second instance on every CU after it
-  const int C = a.n_channels, B = a.n_streams, nvb = (a.n_ticks * C + kWB - 1) / kWB;
-  const long long nbg = (long long)B * nvb;
-  auto gate_take = [&]() -> long long {
-    unsigned v = 0;
-    if (lane == 0) v = atomicAdd(&a.gate[0], 1u);
-    return __shfl(v, 0);
-  };
-  auto gate_frames = [&](long long b) -> int {
-    const int s = (int)(b % B), vb = (int)(b / B);
-    const int nf = ticks_of(a, s) * C, v = vb * kWB + lane;
-    if (lane == 0) {
-      const unsigned need = (unsigned)min(vb * kWB + kWB, nf);
-      const unsigned *pg = a.gate + 1 + s / kGruS;
-      while (__hip_atomic_load(pg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) __builtin_amdgcn_s_sleep(8);
-    }
-    // the gains are read with coherent (sc1) loads below; this only keeps
-    // the compiler from moving them above the wait (an agent-scope acquire
-    // would invalidate the XCD's L2 for every batch)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    return (lane < kWB && v < nf) ? (int)((long long)s * a.V + v) : -1;
-  };
-  const bool gated = a.gate != nullptr;
-  for (long long g = gated ? gate_take() : wave_first(a, kWaveSynth, kWorkSynth, lane); g < (gated ? nbg : nb);
-       g = gated ? gate_take() : wave_next(a, kWaveSynth, kWorkSynth, lane, g)) {
+  for (long long g = wave_first(a, kWaveSynth, kWorkSynth, lane); g < nb; g = wave_next(a, kWaveSynth, kWorkSynth, lane, g)) {
     // the batch's frames and silence flags, lane per frame
-    const int fl = gated ? gate_frames(g) : batch_frames(a, g, lane);
+    const int fl = batch_frames(a, g, lane);
     const int sl = fl >= 0 ? a.silence[fl] : 0;
     settle(sl);
     for (int fr = 0; fr < kWB; fr++) {
@@ -364,9 +336,7 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
       for (int r = 0; r < 8; r++) pv[r] = P[min(64 * r + lane, kFreq - 1)];
       const size_t o = (size_t)f * kBands + min(lane, kBands - 1);
       const float Exp = a.Exp[o], Ex = a.Ex[o], Ep = a.Ep[o];
-      // gains: written by k_gru16 during this kernel under the fp16 overlap
-      const float gg = gated ? __hip_atomic_load(&a.gr[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.gr[o];
-      const float gs = gated ? __hip_atomic_load(&a.gs[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.gs[o];
+      const float gg = a.gr[o], gs = a.gs[o];
       if (fil) {
         if (lane < kBands) {
           float r;
@@ -895,7 +865,7 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
   // the grid covers min(batches, 8) blocks at least; static mode: batches /
   // kWNW blocks suffice
   auto grid = [&](int resident) {
-    const long long want = ((a.wave_static >> which) & 1) ? (batches + kWNW - 1) / kWNW : batches;
+    const long long want = ((kWaveStatic >> which) & 1) ? (batches + kWNW - 1) / kWNW : batches;
     return dim3((unsigned)std::min<long long>(std::max<long long>(want, 1), resident));
   };
   if (which == kWaveFftA)

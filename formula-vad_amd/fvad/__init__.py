@@ -35,7 +35,7 @@ class EngineConfig(C.Structure):
     _fields_ = [("n_streams", C.c_int), ("n_channels", C.c_int), ("device", C.c_int), ("sample_rate", C.c_int),
                 ("fft_size", C.c_int), ("max_ticks", C.c_int), ("n_bands", C.c_int),
                 ("band_lo", C.c_int * MAX_BANDS), ("band_hi", C.c_int * MAX_BANDS), ("want_denoised", C.c_int),
-                ("mode", C.c_int), ("use_denoiser", C.c_int), ("cu_mask", C.c_uint32 * 8)]
+                ("mode", C.c_int), ("use_denoiser", C.c_int)]
 
 
 MODE_STAGED, MODE_FUSED, MODE_FP16 = 0, 1, 2
@@ -170,7 +170,6 @@ SYMBOLS = [
     ("fvad_engine_kernel_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("fvad_engine_kernel_name", C.c_char_p, [C.c_void_p, C.c_int]),
     ("fvad_engine_windows_per_tick", C.c_int, [C.c_void_p]),
-    ("fvad_engine_fp16_overlap", C.c_int, [C.c_void_p]),
     ("fvad_engine_attach_vadm", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     ("fvad_engine_segments", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
     ("fvad_engine_segments_range", C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_size_t]),
@@ -295,7 +294,7 @@ class Engine:
     """Batched hot path for a partition of streams on one GPU."""
 
     def __init__(self, model, n_streams, n_channels=2, device=0, max_ticks=100, fft_size=2048, bands=((4, 64),),
-                 want_denoised=False, mode="staged", use_denoiser=True, cu_mask=None):
+                 want_denoised=False, mode="staged", use_denoiser=True):
         cfg = EngineConfig()
         lib().fvad_engine_config_default(C.byref(cfg), n_streams, n_channels)
         cfg.device = device
@@ -308,9 +307,6 @@ class Engine:
         cfg.want_denoised = int(want_denoised)
         cfg.mode = {"staged": MODE_STAGED, "fused": MODE_FUSED, "fp16": MODE_FP16}[mode]
         cfg.use_denoiser = int(use_denoiser)
-        if cu_mask is not None:  # CU ids the engine may use (fvad_engine_config.cu_mask)
-            for cu in cu_mask:
-                cfg.cu_mask[cu // 32] |= 1 << (cu % 32)
         self.cfg = cfg
         self.model = model
         h = C.c_void_p()
@@ -321,7 +317,6 @@ class Engine:
         # window slots per (tick, stream): 1 for fft_size >= 480, else several
         # (VAD.zig:307-347); with W > 1 the window outputs get a slot axis
         self.wpt = lib().fvad_engine_windows_per_tick(h)
-        self.overlap = bool(lib().fvad_engine_fp16_overlap(h))
 
     def _alloc_out(self, n_ticks, denoised):
         T, B, Ch, nb, W = n_ticks, self.B, self.C, self.nb, self.wpt

@@ -116,10 +116,6 @@ typedef struct {
   int use_denoiser;     /* VAD.Config.use_denoiser (default 1).  0: fft_size frames of raw input go
                          * straight to FFT B (VAD.zig:206-212,239-249); per-tick vad / ratio are -1,
                          * the window ratio is preAnalyzeSegment's over the frame, window vad -1 */
-  uint32_t cu_mask[8];  /* CUs the engine's kernels may use (bit i of word i / 32 = CU i, as
-                         * hipExtStreamCreateWithCUMask); all zero = every CU.  Engines with disjoint
-                         * masks on one GPU run side by side without sharing a CU; persistent grids are
-                         * sized to the mask's CU count */
 } fvad_engine_config;
 
 /* staged: time-parallel frame kernels + a thin per-stream recurrence kernel;
@@ -161,13 +157,6 @@ typedef struct {
  * 480, else floor((fft_size - 1 + 480) / fft_size) -- the most windows one
  * tick can complete */
 int fvad_engine_windows_per_tick(const fvad_engine *e);
-
-/* 1 when an FVAD_MODE_FP16 engine overlaps its GRU with the synthesis: k_gru16
- * on one half of the CUs, the synthesis of the frames whose gains it has
- * published on the other half, the rest on every CU after it (same results;
- * opt-in with FVAD_FP16_OVERLAP=1 for an engine with the whole GPU: measured
- * slower than the sequential schedule) */
-int fvad_engine_fp16_overlap(const fvad_engine *e);
 
 /* pcm: host [ticks][streams][channels][480] normalised f32.  ticks_valid
  * (nullable): stream s only consumes its first ticks_valid[s] ticks (ragged

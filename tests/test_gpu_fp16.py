@@ -180,49 +180,3 @@ def test_fp16_fft_size_1000_segments(fvad_mod, oracle_mod, models):
         assert float(np.abs(b_ref - b_got).max() / np.abs(b_ref).max()) <= BAND_REL
         assert [(a, b) for a, b, _, _ in eng.segments(s)] == [(a, b) for a, b, _, _ in p.segments()]
 
-
-def _overlap_run(n_streams=300, pushes=3, ticks=50):
-    """The fp16 engine on resident synthetic input (ids 0.., digital silence
-    every 20th), device VADMachine: every push's outputs and the segments."""
-    import fvad
-    eng = fvad.Engine(fvad.Model(seed=1), n_streams, 2, max_ticks=ticks, mode="fp16")
-    eng.attach_vadm()
-    eng.load_synthetic(ticks, base=0, pushes=pushes)
-    outs = []
-    for _ in range(pushes):
-        eng.run_resident(ticks)
-        eng.sync()
-        outs.append(eng.fetch(ticks))
-    out = {k: np.stack([o[k] for o in outs]) for k in outs[0]}
-    segs = [eng.segments(s) for s in range(n_streams)]
-    return eng.overlap, out, segs
-
-
-def test_fp16_overlap_identical(fvad_mod, tmp_path):
-    """The fp16 overlap (opt-in, FVAD_FP16_OVERLAP=1: k_gru16 on half the CUs,
-    the gated synthesis of the frames it has finished on the other half, then
-    the rest on every CU) only schedules the same kernels differently: every
-    output and segment of a run with it (in a child process) equals the
-    sequential run's bit for bit, on 300 streams (19 GRU workgroups, ragged
-    last one) x 3 pushes."""
-    import os
-    import pickle
-    import subprocess
-    import sys
-    if os.environ.get("FVAD_FP16_OVERLAP", "0") not in ("", "0"):
-        pytest.skip("the parent process must run the sequential schedule")
-    on0, out0, segs0 = _overlap_run()
-    assert not on0
-    res = tmp_path / "overlap.pkl"
-    code = ("import sys, pickle; sys.path[:0] = %r; import test_gpu_fp16 as t; "
-            "r = t._overlap_run(); pickle.dump(r, open(%r, 'wb'))" % (sys.path[:6], str(res)))
-    env = dict(os.environ, FVAD_FP16_OVERLAP="1")
-    r = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(os.path.abspath(__file__)), env=env,
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout + r.stderr
-    on, out, segs = pickle.load(open(res, "rb"))
-    assert on, "overlap not active on a whole-GPU fp16 engine with FVAD_FP16_OVERLAP=1"
-    for k in out:
-        assert np.array_equal(out[k], out0[k]), k
-    assert segs == segs0
-    assert out["win_flag"].sum() > 0 and (out["vad"] > 0).mean() > 0.5

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "formula-vad_amd")
 
 
 def test_abi_exports_every_declared_symbol(fvad_mod):
@@ -162,3 +163,30 @@ def test_kiss_fftr_alloc_lenmem_protocol(fvad_mod, n):
     got = C.c_size_t(lenmem.value)
     assert L.kiss_fftr_alloc(n, 0, mem, C.byref(got)) == C.addressof(mem)
     assert L.kiss_fftr_alloc(n + 1, 0, None, C.byref(C.c_size_t(1))) is None  # odd sizes refused
+
+
+def test_synth_ticks_host_memory_bounded():
+    """fvad_synth_ticks / fvad_engine_load_synthetic_ex keep no whole-block
+    cache (a rank of an 8-GPU run held its 7.9 GB block): the
+    peak RSS of a process that takes 50 ticks of 256 streams x 10 s (the
+    generator runs the full length per stream) grows by the output plus the
+    generator threads' per-stream scratch, not by the 0.98 GB block."""
+    import subprocess
+    import sys
+    code = r'''
+import resource, sys
+sys.path.insert(0, %r)
+import fvad
+fvad.lib()
+r0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+x = fvad.synth_ticks(0, 256, 2, 1000, 0, 50)
+y = fvad.synth_ticks(0, 256, 2, 1000, 950, 50)
+r1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+assert x.shape == (50, 256, 2, 480) and y.shape == x.shape and float(abs(x).max()) > 0
+print((r1 - r0) / 1024.0)
+''' % PKG
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    grew_mb = float(out.stdout.strip().splitlines()[-1])
+    out_mb = 2 * 50 * 256 * 2 * 480 * 4 / 2 ** 20  # 93.75
+    assert grew_mb < out_mb + 16 * 3.84 * 2 + 64, grew_mb  # < ~280 MB, against ~1 GB with a block cache

@@ -1,4 +1,4 @@
-"""Push timeline from a rocprofv3 kernel-trace database (tools/_r4_trace.sh):
+"""Push timeline from a rocprofv3 kernel-trace database (a rocprofv3 --kernel-trace run of bench.py, e.g. tools/profile.sh):
 per-boundary gaps of the main-stream chain, push period, main-chain busy
 time, and what the side kernels overlap.  Usage: trace_gaps.py <run_results.db>"""
 import collections
