@@ -482,6 +482,9 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks):
     kernels = {}
     for name, ms in kt["kernels"].items():
         c = per_k[name]
+        if ms <= 0:  # not run (or not timed) in the timed pushes
+            kernels[name] = {"ms": 0.0, "tflops": None, "gbs": None, "intensity": None}
+            continue
         sec = ms / 1000.0
         kernels[name] = {"ms": round(ms, 4), "tflops": round(c["flops"] * frames_launch / sec / 1e12, 3),
                          "gbs": round(c["bytes"] * frames_launch / sec / 1e9, 1),

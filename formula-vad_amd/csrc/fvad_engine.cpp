@@ -655,7 +655,9 @@ int vadm_flush(fvad_engine *e, bool fast = true) {
   // the push's end: ev_buf_free of its parity (recorded after its kernels and
   // ticks copy; re-recorded only by the push after next)
   HIP_TRY(hipStreamWaitEvent(e->side, e->ev_buf_free[e->vpend_b], 0));
-  return enqueue_vadm(e, e->vpend_args, e->vpend_b, e->vpend_timed, fast);
+  // a flush at a sync point (k_vadm_par, the job's drain) is always timed:
+  // its event pair sits on the side stream, after everything else
+  return enqueue_vadm(e, e->vpend_args, e->vpend_b, e->vpend_timed || fast, fast);
 }
 
 namespace {

@@ -64,7 +64,10 @@ constexpr int kPcNT = kPcL * kPcF;
 static_assert(ptile::kQuarter % kPcF == 0 && kPcF % 4 == 0, "k_pcorr groups");
 // FVAD_DIAG_SKIP (bit 1 Q1, 2 Q3, 4 Q5): diagnostic flavours without that
 // phase's sums, for the per-phase LDS attribution (`make diag`,
-// tools/lds_attr.sh); never set in the product build
+// tools/lds_attr.sh); bit 8: Q1's y reads at a lane stride of 5 words instead
+// of 10 (wrong values, the same instructions; 32 distinct banks per 32-lane
+// group instead of 16): the upper bound of a conflict-free Q1 layout.  Never
+// set in the product build
 #ifndef FVAD_DIAG_SKIP
 #define FVAD_DIAG_SKIP 0
 #endif
@@ -233,7 +236,7 @@ __global__ void __launch_bounds__(kPcNT) k_pcorr(StagedArgs a) {
       for (int r = 0; r < R; r++) acc[r] = 0.0f;
       if (k0 < 147) {
         const float *X = xf[fr] + (kPitchMax >> 1);
-        const float *Y = xf[fr] + 2 * k0;
+        const float *Y = xf[fr] + ((FVAD_DIAG_SKIP & 8) ? k0 : 2 * k0);
         float win[R];
         auto yld = [&](int m) -> float { return Y[2 * m]; };
 #pragma unroll

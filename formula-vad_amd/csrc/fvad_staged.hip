@@ -40,6 +40,7 @@
 #include <type_traits>
 
 #include "fvad_device.h"
+#include "fvad_exact.h"
 #include "fvad_internal.h"
 #include "fvad_staged.h"
 #include "fvad_staged_dev.h"
@@ -1640,9 +1641,10 @@ __device__ __forceinline__ double lt_sum(double acc, const float *buf, size_t bs
   for (; i < i1; i++) acc += (double)buf[(size_t)i * bs] * scalar;
   return acc;
 }
+// entries never written hold the initial average: n adds of one term, done
+// per binade (fvad_exact.h: the loop's bits)
 __device__ __forceinline__ double lt_sum_init(double acc, double term, unsigned n) {
-  for (unsigned i = 0; i < n; i++) acc += term;
-  return acc;
+  return add_const_n(acc, term, n);
 }
 template <int kL = FVAD_LT_BLOCK>
 __device__ __forceinline__ double lt_range(double acc, const float *buf, size_t bs, unsigned p, unsigned q,

@@ -190,3 +190,18 @@ print((r1 - r0) / 1024.0)
     grew_mb = float(out.stdout.strip().splitlines()[-1])
     out_mb = 2 * 50 * 256 * 2 * 480 * 4 / 2 ** 20  # 93.75
     assert grew_mb < out_mb + 16 * 3.84 * 2 + 64, grew_mb  # < ~280 MB, against ~1 GB with a block cache
+
+
+def test_add_const_n_exact(tmp_path):
+    """fvad_exact.h's add_const_n (the long-term RollingAverage's recompute over
+    entries still holding the initial average, RollingAverage.zig:45-56, per
+    binade instead of per add) returns the plain loop's bits on 200 000 random
+    and edge cases (acc 0 / negative / at a binade edge, ties, tiny and large
+    terms), compiled here as plain C++ (the kernels include the same header)."""
+    import subprocess
+    exe = tmp_path / "exact"
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-std=c++20", "-I",
+                           os.path.join(PKG, "csrc"), os.path.join(ROOT, "tests", "exact_harness.cpp"), "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 / 200000 mismatches" in out.stdout
