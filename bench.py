@@ -146,6 +146,19 @@ def stream_partition(rank, streams_per_gpu):
     return rank * streams_per_gpu, streams_per_gpu
 
 
+RSS_STAGES = {}
+
+
+def rss_stage(name):
+    """Current resident set (MB) of this process at a named stage (host_memory.stages)."""
+    try:
+        with open("/proc/self/status") as f:
+            kb = next(int(ln.split()[1]) for ln in f if ln.startswith("VmRSS:"))
+        RSS_STAGES[name] = round(kb / 1024.0, 1)
+    except (OSError, StopIteration):
+        pass
+
+
 def aggregate_rate(frames_per_rank_step, world, steps, elapsed_max):
     """Whole-job channel-frames/s: every rank's frames over the slowest rank's time."""
     return frames_per_rank_step * world * steps / elapsed_max
@@ -273,22 +286,32 @@ def host_rate(eng, args, rank, dist, torch, base):
     import numpy as np
     e = eng
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
-    src = fvad.synth_ticks(base, B, Ch, args.resident_pushes * T, 0, 2 * T)
-    halves = (src[:T], src[T:])
-    del src
-    q16 = [np.clip(np.round(h * 32768.0), -32768, 32767).astype(np.int16) for h in halves]
+    # host memory stays bounded: the two pushes are generated straight into the
+    # pinned slots, the 16-bit slots are converted from them a tick at a time,
+    # and the pageable leg's two host arrays live only during that leg
+    slots = []
+    for k in range(DEPTH):  # slot k holds push k & 1
+        sl = e.input_slot()[:T]
+        if k < 2:
+            fvad.synth_ticks(base, B, Ch, args.resident_pushes * T, k * T, T, out=sl)
+        else:
+            sl[...] = slots[0]
+        slots.append(sl)
+        e.submit(sl)
+    for _ in range(DEPTH):
+        e.collect(want=False)
+    e.sync()
     res = {}
     for kind in ("pinned", "pageable", "pinned_i16"):
-        if kind.startswith("pinned"):
-            for k in range(DEPTH):  # every slot holds one of the two pushes
-                if kind == "pinned":
-                    sl = e.input_slot()
-                    sl[:T] = halves[k & 1]
-                    e.submit(sl[:T])
-                else:
-                    sl = e.input_slot_i16()
-                    sl[:T] = q16[k & 1]
-                    e.submit_i16(sl[:T])
+        pages = None
+        if kind == "pageable":
+            pages = [np.array(slots[0]), np.array(slots[1])]
+        elif kind == "pinned_i16":
+            for k in range(DEPTH):  # the same audio as 16-bit samples, slot by slot
+                sl16 = e.input_slot_i16()[:T]
+                for t in range(T):
+                    sl16[t] = np.clip(np.round(slots[k][t] * np.float32(32768.0)), -32768, 32767)
+                e.submit_i16(sl16)
             for _ in range(DEPTH):
                 e.collect(want=False)
         e.sync()
@@ -302,7 +325,7 @@ def host_rate(eng, args, rank, dist, torch, base):
             if kind == "pinned_i16":
                 e.submit_i16(e.input_slot_i16()[:T])
             else:
-                e.submit(e.input_slot()[:T] if kind == "pinned" else halves[k & 1])
+                e.submit(e.input_slot()[:T] if kind == "pinned" else pages[k & 1])
             inflight += 1
         while inflight:
             e.collect(want=True)
@@ -315,7 +338,7 @@ def host_rate(eng, args, rank, dist, torch, base):
     return {"value": round(res["pinned"][0], 1), "unit": "frames/s", "ms_per_step": round(res["pinned"][1], 3),
             "pageable_value": round(res["pageable"][0], 1), "pageable_ms_per_step": round(res["pageable"][1], 3),
             "i16_value": round(res["pinned_i16"][0], 1), "i16_ms_per_step": round(res["pinned_i16"][1], 3),
-            "input_bytes_per_step": int(halves[0].nbytes), "i16_input_bytes_per_step": int(q16[0].nbytes),
+            "input_bytes_per_step": int(slots[0].nbytes), "i16_input_bytes_per_step": int(slots[0].nbytes // 2),
             "note": "streaming submit/collect, 3 pushes in flight, input = the first two pushes of the synthetic "
                     "streams alternating: from pinned host slots (value) or pageable host memory (pageable_value), "
                     "H2D over PCIe inside the timed region and overlapped with the previous push; per-tick "
@@ -361,9 +384,11 @@ def main():
     def measure(mode):
         """warmup, then exactly args.steps pushes between barriers; max over ranks"""
         e = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=mode)
+        rss_stage("engine_%s" % mode)
         if mode != "fused" and not args.no_vadm:
             e.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
         e.load_synthetic(T, base=base, pushes=P)
+        rss_stage("resident_input_%s" % mode)
         for _ in range(args.warmup):
             e.run_resident(T)
         e.sync()
@@ -377,12 +402,15 @@ def main():
         elapsed = max_over_ranks(time.perf_counter() - t0, dist, torch)
         return e, elapsed, e.kernel_times()
 
+    rss_stage("start")
     eng, elapsed, kt_local = measure(args.mode)
+    rss_stage("after_timed_%s" % args.mode)
     kt, ranks = gather_kernel_tables(kt_local, dist, torch, rank)
     value = aggregate_rate(B * Ch * T, world, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
     host = host_rate(eng, args, rank, dist, torch, base) if args.host_rate else None
+    rss_stage("after_host_buffers")
     variants = None
     if args.variants and args.mode == "staged":
         del eng  # one engine's buffers at a time
@@ -405,7 +433,7 @@ def main():
     import resource
     host_mem = {"peak_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1),
                 "pinned_slots_mb": round(DEPTH * (B * Ch * T * 480 * 6 + B * T * 4 * 8) / 2 ** 20, 1)
-                if args.host_rate else 0.0}
+                if args.host_rate else 0.0, "stages_rss_mb": dict(RSS_STAGES)}
     host_mem_all = None
     if dist is not None:
         host_mem_all = [None] * world

@@ -113,6 +113,7 @@ struct fvad_engine {
   int vadm_kind[2] = {};
   int vadm_slot = 0;
   bool dbg_always_par = false;  // test hook FVAD_DEBUG_VADM_ALWAYS_PAR
+  bool dbg_lt_full = false;     // test hook FVAD_DEBUG_VADM_LT_FULL
   // test hook (fvad_engine_output_log): the per-tick outputs of the next
   // log_cap pushes, copied on the engine stream as each push ends
   float *d_log = nullptr;
@@ -941,50 +942,59 @@ void par_copy(void *dst, const void *src, size_t bytes) {
   for (auto &t : pool) t.join();
 }
 
-int ensure_slots(fvad_engine *e) {
-  if (e->slots_ready) return FVAD_OK;
+// The copy stream, and slot i's pinned buffers on first use: a caller that
+// keeps k pushes in flight pins k slots, not FVAD_MAX_IN_FLIGHT
+int ensure_slots(fvad_engine *e, int i) {
   const fvad_engine_config &c = e->cfg;
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t TB = T * B, TBW = TB * e->wpt, frames = TB * C * fvad::kFrame;
-  // the copy stream at the highest priority: its own hardware queue, so the
-  // 16-bit ingest's k_pcm16 does not queue behind a long kernel of a stream
-  // sharing its queue (it waited for k_vadm_hbm at the default priority)
-  int lo_prio = 0, hi_prio = 0;
-  if (!e->cstream && (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
-                      hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, hi_prio) != hipSuccess))
-    return fail(FVAD_EDEVICE, "copy stream creation failed");
+  if (!e->slots_ready) {
+    // the copy stream at the highest priority: its own hardware queue, so the
+    // 16-bit ingest's k_pcm16 does not queue behind a long kernel of a stream
+    // sharing its queue (it waited for k_vadm_hbm at the default priority)
+    int lo_prio = 0, hi_prio = 0;
+    if (!e->cstream && (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
+                        hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, hi_prio) != hipSuccess))
+      return fail(FVAD_EDEVICE, "copy stream creation failed");
+    e->slots_ready = true;
+  }
+  auto &sl = e->slots[i];
+  if (sl.done) return FVAD_OK;  // allocated (the events come last)
   auto host = [&](auto **p, size_t count) -> int {
-    if (hipHostMalloc(reinterpret_cast<void **>(p), std::max<size_t>(count, 1) * 4, 0) != hipSuccess)
+    if (*p) return FVAD_OK;  // kept from an earlier, partly failed call
+    if (hipHostMalloc(reinterpret_cast<void **>(p), std::max<size_t>(count, 1) * 4, 0) != hipSuccess) {
+      *p = nullptr;
       return fail(FVAD_ENOMEM, "hipHostMalloc failed (pinned input / output slots)");
+    }
     return FVAD_OK;
   };
-  for (auto &sl : e->slots) {
-    int rc;
-    if ((rc = host(&sl.in, frames)) || (rc = host(&sl.ticks, 2 * B)) || (rc = host(&sl.vad, TB)) ||
-        (rc = host(&sl.ratio, TB)) || (rc = host(&sl.wflag, TB)) || (rc = host(&sl.wratio, TBW)) ||
-        (rc = host(&sl.wvad, TBW)) || (rc = host(&sl.band, TBW * C * c.n_bands)) ||
-        (c.want_denoised && (rc = host(&sl.den, frames))))
-      return rc;
-    if (hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
-      return fail(FVAD_EDEVICE, "hipEventCreate failed");
+  int rc;
+  if ((rc = host(&sl.in, frames)) || (rc = host(&sl.ticks, 2 * B)) || (rc = host(&sl.vad, TB)) ||
+      (rc = host(&sl.ratio, TB)) || (rc = host(&sl.wflag, TB)) || (rc = host(&sl.wratio, TBW)) ||
+      (rc = host(&sl.wvad, TBW)) || (rc = host(&sl.band, TBW * C * c.n_bands)) ||
+      (c.want_denoised && (rc = host(&sl.den, frames))))
+    return rc;
+  if ((!sl.h2d && hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) != hipSuccess) ||
+      hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+    sl.done = nullptr;
+    return fail(FVAD_EDEVICE, "hipEventCreate failed");
   }
-  e->slots_ready = true;
   return FVAD_OK;
 }
 
-// the 16-bit ingest's pinned slots and device staging buffer, on first use
-int ensure_slots16(fvad_engine *e) {
-  if (e->d_pcm16) return FVAD_OK;
+// slot i's pinned 16-bit input and the device staging buffer, on first use
+int ensure_slots16(fvad_engine *e, int i) {
   const fvad_engine_config &c = e->cfg;
   const size_t n = (size_t)c.max_ticks * c.n_streams * c.n_channels * fvad::kFrame;
-  for (auto &sl : e->slots)  // a slot allocated by an earlier, partly failed call is kept
-    if (!sl.in16 && hipHostMalloc(reinterpret_cast<void **>(&sl.in16), n * sizeof(int16_t), 0) != hipSuccess) {
-      sl.in16 = nullptr;
-      return fail(FVAD_ENOMEM, "hipHostMalloc failed (16-bit input slots)");
-    }
-  if (hipMalloc(reinterpret_cast<void **>(&e->d_pcm16), n * sizeof(int16_t)) != hipSuccess)
+  auto &sl = e->slots[i];
+  if (!sl.in16 && hipHostMalloc(reinterpret_cast<void **>(&sl.in16), n * sizeof(int16_t), 0) != hipSuccess) {
+    sl.in16 = nullptr;
+    return fail(FVAD_ENOMEM, "hipHostMalloc failed (16-bit input slot)");
+  }
+  if (!e->d_pcm16 && hipMalloc(reinterpret_cast<void **>(&e->d_pcm16), n * sizeof(int16_t)) != hipSuccess) {
+    e->d_pcm16 = nullptr;
     return fail(FVAD_ENOMEM, "hipMalloc failed (16-bit input staging)");
+  }
   return FVAD_OK;
 }
 
@@ -1035,7 +1045,7 @@ extern "C" float *fvad_engine_input_slot(fvad_engine *e) {
     fail(FVAD_EINVAL, "null engine");
     return nullptr;
   }
-  if (hipSetDevice(e->cfg.device) != hipSuccess || ensure_slots(e)) return nullptr;
+  if (hipSetDevice(e->cfg.device) != hipSuccess || ensure_slots(e, e->sub_next)) return nullptr;
   auto &sl = e->slots[e->sub_next];
   if (sl.h2d_busy) {
     if (hipEventSynchronize(sl.h2d) != hipSuccess) {
@@ -1069,10 +1079,10 @@ int submit_any(fvad_engine *e, const Sample *pcm, int n_ticks, const int32_t *ti
   std::vector<int32_t> tt;
   if ((rc = tail_ticks(e, ticks_valid, last_tick_samples, n_ticks, tt))) return rc;
   HIP_TRY(hipSetDevice(c.device));
-  if ((rc = ensure_slots(e))) return rc;
-  if constexpr (k16)
-    if ((rc = ensure_slots16(e))) return rc;
   const int si = e->sub_next;
+  if ((rc = ensure_slots(e, si))) return rc;
+  if constexpr (k16)
+    if ((rc = ensure_slots16(e, si))) return rc;
   auto &sl = e->slots[si];
   if (sl.pending) return fail(FVAD_EINVAL, "FVAD_MAX_IN_FLIGHT pushes in flight: collect the oldest one first");
   const size_t B = c.n_streams, TB = (size_t)n_ticks * B, TBW = TB * e->wpt;
@@ -1149,7 +1159,8 @@ extern "C" int16_t *fvad_engine_input_slot_i16(fvad_engine *e) {
     fail(FVAD_EINVAL, "null engine");
     return nullptr;
   }
-  if (hipSetDevice(e->cfg.device) != hipSuccess || ensure_slots(e) || ensure_slots16(e)) return nullptr;
+  if (hipSetDevice(e->cfg.device) != hipSuccess || ensure_slots(e, e->sub_next) || ensure_slots16(e, e->sub_next))
+    return nullptr;
   auto &sl = e->slots[e->sub_next];
   if (sl.h2d_busy) {
     if (hipEventSynchronize(sl.h2d) != hipSuccess) {
@@ -1372,9 +1383,20 @@ double initial_avg(size_t n, double init) {
 
 int vadm_reset(fvad_engine *e) {
   std::vector<float> buf(e->vadm_buf_len, 0.0f);  // initial entries are K.init, tracked by lt_nw
+  std::vector<fvad::VadmState> st = e->vadm_init;
+  if (e->dbg_lt_full) {
+    // test hook FVAD_DEBUG_VADM_LT_FULL: every long-term entry counts as pushed
+    // (holding (float)init), the state of a stream past its first
+    // long_term_speech_avg_sec -- timing only, not the reference's values
+    const int B = e->cfg.n_streams;
+    for (int m = 0; m < e->vadm.n; m++) {
+      const fvad::VadmConst &K = e->vadm.c[m];
+      for (long long i = 0; i < (long long)K.n_lt * B; i++) buf[K.lt_off + i] = (float)K.init;
+      for (int s = 0; s < B; s++) st[(size_t)m * B + s].lt_nw = (unsigned)K.n_lt;
+    }
+  }
   HIP_TRY(hipMemcpy(e->vadm.buf, buf.data(), buf.size() * sizeof(float), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->vadm.st, e->vadm_init.data(), e->vadm_init.size() * sizeof(fvad::VadmState),
-                    hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->vadm.st, st.data(), st.size() * sizeof(fvad::VadmState), hipMemcpyHostToDevice));
   return FVAD_OK;
 }
 
@@ -1586,6 +1608,11 @@ extern "C" int fvad_engine_set_debug(fvad_engine *e, int key, int value) {
     case FVAD_DEBUG_VADM_ALWAYS_PAR:
       e->dbg_always_par = value != 0;
       return FVAD_OK;
+    case FVAD_DEBUG_VADM_LT_FULL:
+      if (e->vadm.n == 0) return fail(FVAD_EINVAL, "no VADMachines attached");
+      e->dbg_lt_full = value != 0;
+      if (const int rc = fvad_engine_sync(e)) return rc;
+      return vadm_reset(e);
     default:
       return fail(FVAD_EINVAL, "unknown debug key");
   }

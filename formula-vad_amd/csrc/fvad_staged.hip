@@ -1772,6 +1772,26 @@ __device__ __forceinline__ void vadm_fsm(VadmState &S, const VadmConst &K, unsig
 
 // One machine over all completed windows of the push for one stream; `lt`
 // points at entry 0 of the stream's long-term buffer, `lts` is its stride.
+//
+// Lazy long-term folds.  Once the long-term buffer is full (from the start
+// with an initial average) every window that pushes re-folds ~n - w entries
+// (RollingAverage.zig:45-56), ~12 folds per push: 7 ms per push at 2048
+// streams once a stream is past its first long_term_speech_avg_sec (a full
+// buffer of pushed values, measured with FVAD_DEBUG_VADM_LT_FULL).  But a
+// window's average is only *observed* through the next window's test
+// st_avg > RN(lt_last * factor), and the last one through the state.  So the
+// walk keeps a running estimate of the average (approx += t_new - t_old per
+// push, t = RN(entry * 1/n)) with a rigorous bound E on its distance to the
+// fold's result -- the fold of nonnegative terms is within (n-1) u of their
+// exact sum (u = 2^-53), each estimate update adds <= 2u -- decides every test
+// whose outcome the bound settles, runs the exact fold (the same adds in the
+// same order as the reference) only for a test it does not settle, and folds
+// once at the end of the push for the state.  The cached prefix P_w advances
+// by one add per push, as in k_vadm_par.  Every decision and every stored value
+// is the reference's; typically one fold per push instead of one per window.
+// Used when the buffer is full, the terms are nonnegative (band energies,
+// a nonnegative initial average) and the threshold factor is nonnegative;
+// otherwise each pushing window folds at once (ra_push_long).
 __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t lts) {
   const int B = a.n_streams, C = a.n_channels, nb = a.n_bands;
   const int nt = ticks_of(a, s);
@@ -1780,6 +1800,21 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
   VadmState S = a.vadm.st[(size_t)m * B + s];
   float *st = a.vadm.buf + K.st_off + s, *rb = a.vadm.buf + K.r_off + s;
   VadmSeg *seg = a.vadm.seg + ((size_t)m * B + s) * a.vadm.seg_cap;
+  const unsigned n = (unsigned)K.n_lt;
+  const double f = (double)K.thr_factor, scalar = 1.0 / (double)n;
+  const bool lazy = S.lt_count == n && S.lt_pre_ok && S.lt_has && n > 1 && f >= 0.0 && !(K.has_init && !(K.init >= 0.0));
+  double approx = S.lt_last, amax = fabs(S.lt_last), fpre = 0.0;
+  int pending = 0;  // pushes since lt_last was last folded exactly
+  // the exact average of the current buffer: the fold through the last pushed
+  // index (fpre) continued over the entries after it, C order
+  auto fold = [&]() {
+    double acc = fpre;
+    if (S.lt_widx != 0) acc = lt_range(acc, lt, lts, S.lt_widx, n, S.lt_nw, K.init, scalar);
+    S.lt_last = acc;
+    approx = acc;
+    amax = fabs(acc);
+    pending = 0;
+  };
   // every window of the push in order: ticks, then a tick's slots (several
   // when fft_size < 480)
   for (int t = 0; t < nt; t++)
@@ -1795,12 +1830,52 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
       }
       // fft_input.vad orelse 0 (VADMachine.zig:240-246): no vad without the denoiser
       const float vad = a.use_denoiser ? a.out_win_vad[o] : 0.0f, vr = a.out_win_ratio[o];
-      const bool met = vadm_short(S, K, st, rb, B, min_v, vr);
-      if (!met)
-        ra_push_long(lt, lts, K.n_lt, S.lt_widx, S.lt_count, S.lt_nw, K.init, S.lt_last, S.lt_has, S.lt_pre,
-                     S.lt_pre_ok, min_v);
+      bool met;
+      if (!lazy) {
+        met = vadm_short(S, K, st, rb, B, min_v, vr);
+        if (!met)
+          ra_push_long(lt, lts, K.n_lt, S.lt_widx, S.lt_count, S.lt_nw, K.init, S.lt_last, S.lt_has, S.lt_pre,
+                       S.lt_pre_ok, min_v);
+      } else {
+        const double st_avg = ra_push(st, B, K.n_st, S.st_widx, S.st_count, S.st_last, S.st_has, min_v);
+        const double r_avg = ra_push(rb, B, K.n_r, S.r_widx, S.r_count, S.r_last, S.r_has, vr);
+        met = false;
+        if (r_avg > (double)K.ratio_thr) {  // else met is false whatever the long-term average
+          if (pending == 0) {
+            met = st_avg > S.lt_last * f;
+          } else {
+            // |approx - fold| <= E (the fold's (n-1) u, twice, and 2u per
+            // estimate update, on the largest estimate; doubled for the
+            // rounding of approx -+ E itself)
+            const double E = (2.0 * n + 4.0 * pending + 64.0) * 0x1p-53 * amax * 2.0;
+            const double lo = (approx - 2.0 * E) * f, hi = (approx + 2.0 * E) * f;
+            if (st_avg > hi) {
+              met = true;
+            } else if (st_avg <= lo) {
+              met = false;
+            } else {  // not settled by the bound: the exact fold
+              fold();
+              met = st_avg > S.lt_last * f;
+            }
+          }
+        }
+        if (!met) {  // push min_v into the long-term buffer (ra_push_long's state, the fold deferred)
+          const unsigned wi = S.lt_widx;
+          const double t_old = (wi < S.lt_nw ? (double)lt[(size_t)wi * lts] : K.init) * scalar;
+          lt[(size_t)wi * lts] = min_v;
+          const double t_new = (double)min_v * scalar;
+          fpre = S.lt_pre + t_new;  // the fold through index wi
+          S.lt_widx = (wi + 1) % n;
+          if (S.lt_nw < n) S.lt_nw++;
+          S.lt_pre = S.lt_widx == 0 ? 0.0 : fpre;
+          approx = (approx + t_new) - t_old;
+          amax = fmax(amax, fabs(approx));
+          pending++;
+        }
+      }
       vadm_fsm(S, K, index, met, vad, vr, seg, a.vadm.seg_cap);
     }
+  if (pending) fold();
   a.vadm.st[(size_t)m * B + s] = S;
 }
 

@@ -95,7 +95,7 @@ class VadmSnapshot(C.Structure):
                 for n, _ in self._fields_}
 
 
-DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR = 1, 2
+DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR, DEBUG_VADM_LT_FULL = 1, 2, 3
 
 READ_FN = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.c_int, C.POINTER(F32P), C.c_size_t)
 
@@ -276,11 +276,16 @@ def synth_stream(stream_id, n_samples, n_channels=2, label_cap=4096):
     return out, lab[: 2 * min(n, label_cap)].reshape(-1, 2).copy()
 
 
-def synth_ticks(base, n_streams, n_channels, total_ticks, tick0=0, n_ticks=None):
+def synth_ticks(base, n_streams, n_channels, total_ticks, tick0=0, n_ticks=None, out=None):
     """fvad_synth_ticks: [n_ticks][n_streams][n_channels][480] of the streams
-    base.. generated at total_ticks * 480 samples (cached in the library)."""
+    base.. generated at total_ticks * 480 samples (nothing cached); into `out`
+    (a C-contiguous float32 array of that shape, e.g. a pinned input slot) if given."""
     n_ticks = total_ticks - tick0 if n_ticks is None else n_ticks
-    out = np.zeros((n_ticks, n_streams, n_channels, FRAME), np.float32)
+    shape = (n_ticks, n_streams, n_channels, FRAME)
+    if out is None:
+        out = np.zeros(shape, np.float32)
+    elif out.shape != shape or out.dtype != np.float32 or not out.flags.c_contiguous:
+        raise ValueError("synth_ticks: out must be C-contiguous float32 %s" % (shape,))
     _check(lib().fvad_synth_ticks(base, n_streams, n_channels, total_ticks, tick0, n_ticks, fptr(out)),
            "fvad_synth_ticks")
     return out

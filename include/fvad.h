@@ -314,9 +314,14 @@ long fvad_engine_vadm_rolling(fvad_engine *e, int stream, int machine, int which
  *     stream s with s % k == 0 to its in-kernel serial walk (the fallback for a
  *     machine outside the window-parallel case); 0: never (default)
  *   FVAD_DEBUG_VADM_ALWAYS_PAR  value 1: every push's VADMachine runs as
- *     k_vadm_par, not only the one flushed at a sync point */
+ *     k_vadm_par, not only the one flushed at a sync point
+ *   FVAD_DEBUG_VADM_LT_FULL  value 1: the machines restart (as by a reset)
+ *     with every long-term entry counted as pushed, holding (float)init: the
+ *     long-term walk of a stream past its first long_term_speech_avg_sec, for
+ *     timing (tools/vadm_steady.py); the values then differ from the reference */
 #define FVAD_DEBUG_VADM_PAR_SERIAL_EVERY 1
 #define FVAD_DEBUG_VADM_ALWAYS_PAR 2
+#define FVAD_DEBUG_VADM_LT_FULL 3
 int fvad_engine_set_debug(fvad_engine *e, int key, int value);
 /* Output log: the per-tick outputs (fvad_outputs without denoised) of the next
  * n_pushes pushes are copied into device memory on the engine stream as each
