@@ -381,12 +381,17 @@ def main():
     model = fvad.Model(seed=1)
     base, _ = stream_partition(rank, B)
 
-    def measure(mode):
-        """warmup, then exactly args.steps pushes between barriers; max over ranks"""
+    def measure(mode, lt_full=False):
+        """warmup, then exactly args.steps pushes between barriers; max over ranks.
+        lt_full: the device VADMachines start as in a stream past its first
+        long_term_speech_avg_sec (every long-term entry pushed; timing hook
+        FVAD_DEBUG_VADM_LT_FULL, values not the reference's)"""
         e = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=mode)
         rss_stage("engine_%s" % mode)
         if mode != "fused" and not args.no_vadm:
             e.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
+            if lt_full:
+                e.set_debug(fvad.DEBUG_VADM_LT_FULL, 1)
         e.load_synthetic(T, base=base, pushes=P)
         rss_stage("resident_input_%s" % mode)
         for _ in range(args.warmup):
@@ -427,6 +432,22 @@ def main():
                       "1239 segment lists identical on this workload; tests/test_gpu_fp16.py, test_gpu_fullsize.py)",
             "note": "BASELINE configs[4]'s fp16-GRU variant on the same workload and clock (bench.py --mode fp16 "
                     "gives its full line)"}}
+        if not args.no_vadm:
+            # the same workload with the VADMachines in their long-running
+            # regime: a stream past its first 180 s re-folds a long-term
+            # buffer of pushed values; timing only
+            elt, ellt, ktlt = measure("staged", lt_full=True)
+            del elt
+            ktlt, _ = gather_kernel_tables(ktlt, dist, torch, rank)
+            variants["long_running_streams"] = {
+                "value": round(aggregate_rate(B * Ch * T, world, args.steps, ellt), 1), "unit": "frames/s",
+                "ms_per_step": round(1000.0 * ellt / args.steps, 3),
+                "kernels_ms": {k: round(v, 4) for k, v in ktlt["kernels"].items()},
+                "note": "staged mode, the same input and clock, the device VADMachines started as in streams past "
+                        "their first long_term_speech_avg_sec (180 s: every long-term entry a pushed value, timing "
+                        "hook FVAD_DEBUG_VADM_LT_FULL; the VADMachine's values then are not the reference's).  "
+                        "`value` covers streams in their first seconds, where the long-term buffer still holds "
+                        "initial entries"}
     # host memory of this rank after its GPU legs (bounded: the synthetic input
     # is generated and uploaded 64 streams at a time, nothing cached; the
     # pinned slots of the streaming leg are FVAD_MAX_IN_FLIGHT pushes each way)

@@ -503,6 +503,17 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t frames = T * B * C * fvad::kFrame;
   const size_t TBW = T * B * e->wpt;  // window slots
+  {
+    // a streaming slot pins one push of input and outputs (fvad_engine_submit,
+    // up to FVAD_MAX_IN_FLIGHT of them); the window outputs grow with W =
+    // windows_per_tick (up to 240 at fft_size 2): refuse configurations whose
+    // slot would not be a sane pinned allocation
+    const double slot = 4.0 * ((double)frames * (c.want_denoised ? 2 : 1) + 3.0 * T * B + 2.0 * TBW +
+                               (double)TBW * C * c.n_bands);
+    if (slot > 16.0 * (1ull << 30))
+      return bail(fail(FVAD_ENOMEM, "a push of max_ticks x n_streams needs > 16 GiB of pinned slot memory "
+                                    "(outputs scale with windows_per_tick): lower max_ticks or n_streams"));
+  }
   if ((rc = dalloc(&e->d_state, B * fvad::st::kWords)) || (rc = dalloc(&e->d_ring, B * C * e->ring_len)) ||
       (rc = dalloc(&e->d_pcm_b[0], frames)) || (rc = dalloc(&e->d_pcm_b[1], frames)) ||
       (rc = dalloc(&e->d_ratio_b[0], T * B)) ||

@@ -18,8 +18,11 @@ B, C, T, P = 2048, 2, 50, 20
 m = fvad.Model(seed=1)
 out = {}
 PAR = int(os.environ.get("VADM_PAR_BOTH", "0"))
-for name, full, par in (("bench_first_seconds", 0, 0), ("long_term_full", 1, 0),
-                        ("bench_first_seconds_par", 0, 1), ("long_term_full_par", 1, 1))[:4 if PAR else 2]:
+RUNS = (("bench_first_seconds", 0, 0), ("long_term_full", 1, 0), ("bench_first_seconds_par", 0, 1),
+        ("long_term_full_par", 1, 1))[:4 if PAR else 2]
+if os.environ.get("VADM_ONLY_FULL"):
+    RUNS = [r for r in RUNS if r[1]]
+for name, full, par in RUNS:
     e = fvad.Engine(m, B, C, max_ticks=T)
     e.attach_vadm()
     if full:
