@@ -1402,7 +1402,8 @@ int vadm_reset(fvad_engine *e) {
     const int B = e->cfg.n_streams;
     for (int m = 0; m < e->vadm.n; m++) {
       const fvad::VadmConst &K = e->vadm.c[m];
-      for (long long i = 0; i < (long long)K.n_lt * B; i++) buf[K.lt_off + i] = (float)K.init;
+      for (int s = 0; s < B; s++)
+        for (int i = 0; i < K.n_lt; i++) buf[K.lt_off + (size_t)s * K.lt_pitch + i] = (float)K.init;
       for (int s = 0; s < B; s++) st[(size_t)m * B + s].lt_nw = (unsigned)K.n_lt;
     }
   }
@@ -1437,8 +1438,10 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
     K.n_lt = (int)len_of(c.long_term_speech_avg_sec);
     K.n_st = (int)len_of(c.short_term_speech_avg_sec);
     K.n_r = (int)len_of(c.channel_vol_ratio_avg_sec);
+    K.lt_pitch = (K.n_lt + 3) & ~3;  // 16-byte rows
+    off = (off + 3) & ~3LL;
     K.lt_off = off;
-    off += (long long)K.n_lt * B;
+    off += (long long)K.lt_pitch * B;
     K.st_off = off;
     off += (long long)K.n_st * B;
     K.r_off = off;
@@ -1597,10 +1600,14 @@ extern "C" long fvad_engine_vadm_rolling(fvad_engine *e, int stream, int machine
   const long long off = which == 0 ? K.lt_off : which == 1 ? K.st_off : K.r_off;
   const size_t B = e->cfg.n_streams, k = std::min<size_t>((size_t)n, cap);
   if (out && k) {
-    // entries are [i][stream]: one strided 2D copy of the stream's column
+    // long-term entries: the stream's row; the others [i][stream]: a strided 2D copy of its column
     std::vector<float> col(k);
-    HIP_TRY(hipMemcpy2D(col.data(), sizeof(float), e->vadm.buf + off + stream, B * sizeof(float), sizeof(float), k,
+    if (which == 0)
+      HIP_TRY(hipMemcpy(col.data(), e->vadm.buf + off + (size_t)stream * K.lt_pitch, k * sizeof(float),
                         hipMemcpyDeviceToHost));
+    else
+      HIP_TRY(hipMemcpy2D(col.data(), sizeof(float), e->vadm.buf + off + stream, B * sizeof(float), sizeof(float), k,
+                          hipMemcpyDeviceToHost));
     for (size_t i = 0; i < k; i++)
       // long-term entries never written since the machine started hold the
       // initial average, a double (RollingAverage.zig:16-32; lt_nw counts the written)

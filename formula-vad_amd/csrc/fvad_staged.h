@@ -32,7 +32,8 @@ constexpr int kRows = kXx + 1;
 // Device VADMachine (VADMachine.zig:126-230), one lane per stream.
 struct VadmConst {
   int n_lt, n_st, n_r, slot;           // RollingAverage lengths, engine band slot
-  long long lt_off, st_off, r_off;     // buffer offsets (doubles), layout [i][stream]
+  long long lt_off, st_off, r_off;     // buffer offsets (floats): long-term [stream][lt_pitch] (a stream's
+  int lt_pitch;                        //   fold walks its own row), short-term and ratio [i][stream]
   unsigned long long min_open, max_gap, rec_pad;
   float thr_factor, ratio_thr, min_dur, sr;
   int has_init;

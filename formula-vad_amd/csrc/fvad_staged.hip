@@ -1641,6 +1641,52 @@ __device__ __forceinline__ double lt_sum(double acc, const float *buf, size_t bs
   for (; i < i1; i++) acc += (double)buf[(size_t)i * bs] * scalar;
   return acc;
 }
+// The same over a stream's own contiguous row (the long-term buffers'
+// layout, bs == 1): 16-byte loads, blocks of kV of them double-buffered.
+template <int kV = FVAD_LT_BLOCK / 4>
+__device__ __forceinline__ double lt_sum_row(double acc, const float *row, unsigned i0, unsigned i1, double scalar) {
+  unsigned i = i0;
+  for (; i < i1 && (i & 3u); i++) acc += (double)row[i] * scalar;  // to a 16-byte boundary
+  const float4 *r4 = reinterpret_cast<const float4 *>(row);
+  unsigned q = i >> 2;
+  const unsigned qe = i < i1 ? i1 >> 2 : q;  // whole float4 in [i, i1)
+  if (q + kV <= qe) {
+    float4 cur[kV];
+#pragma unroll
+    for (int u = 0; u < kV; u++) cur[u] = r4[q + u];
+    for (; q + 2 * kV <= qe; q += kV) {
+      float4 nxt[kV];
+#pragma unroll
+      for (int u = 0; u < kV; u++) nxt[u] = r4[q + kV + u];
+#pragma unroll
+      for (int u = 0; u < kV; u++) {
+        acc += (double)cur[u].x * scalar;
+        acc += (double)cur[u].y * scalar;
+        acc += (double)cur[u].z * scalar;
+        acc += (double)cur[u].w * scalar;
+      }
+#pragma unroll
+      for (int u = 0; u < kV; u++) cur[u] = nxt[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kV; u++) {
+      acc += (double)cur[u].x * scalar;
+      acc += (double)cur[u].y * scalar;
+      acc += (double)cur[u].z * scalar;
+      acc += (double)cur[u].w * scalar;
+    }
+    q += kV;
+  }
+  for (; q < qe; q++) {
+    const float4 v = r4[q];
+    acc += (double)v.x * scalar;
+    acc += (double)v.y * scalar;
+    acc += (double)v.z * scalar;
+    acc += (double)v.w * scalar;
+  }
+  for (i = i < i1 ? (qe << 2 > i ? qe << 2 : i) : i1; i < i1; i++) acc += (double)row[i] * scalar;  // the tail
+  return acc;
+}
 // entries never written hold the initial average: n adds of one term, done
 // per binade (fvad_exact.h: the loop's bits)
 __device__ __forceinline__ double lt_sum_init(double acc, double term, unsigned n) {
@@ -1650,7 +1696,7 @@ template <int kL = FVAD_LT_BLOCK>
 __device__ __forceinline__ double lt_range(double acc, const float *buf, size_t bs, unsigned p, unsigned q,
                                            unsigned nw, double init, double scalar) {
   const unsigned mid = min(max(nw, p), q);  // [p, mid) written, [mid, q) initial
-  acc = lt_sum<kL>(acc, buf, bs, p, mid, scalar);
+  acc = bs == 1 ? lt_sum_row<(kL >= 8 ? kL / 4 : 2)>(acc, buf, p, mid, scalar) : lt_sum<kL>(acc, buf, bs, p, mid, scalar);
   return lt_sum_init(acc, init * scalar, q - mid);
 }
 
@@ -1927,8 +1973,8 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
   const int self = threadIdx.x;
   for (int m = 0; m < a.vadm.n; m++) {
     const VadmConst &K = a.vadm.c[m];
-    float *lt = a.vadm.buf + K.lt_off + (sok ? s : 0);
-    const size_t lts = (size_t)B;
+    float *lt = a.vadm.buf + K.lt_off + (size_t)(sok ? s : 0) * K.lt_pitch;  // the stream's row
+    const size_t lts = 1;
     // the push's windows in order -> LDS (16 ticks at a time, positions by a
     // prefix count over the group's lanes)
     int Kw = 0;
@@ -2361,7 +2407,7 @@ __global__ void __launch_bounds__(64) k_vadm_hbm(StagedArgs a) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.n_streams || ticks_of(a, s) <= 0) return;
   for (int m = 0; m < a.vadm.n; m++)
-    vadm_stream(a, m, s, a.vadm.buf + a.vadm.c[m].lt_off + s, (size_t)a.n_streams);
+    vadm_stream(a, m, s, a.vadm.buf + a.vadm.c[m].lt_off + (size_t)s * a.vadm.c[m].lt_pitch, 1);
 }
 
 hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream) {
