@@ -288,7 +288,8 @@ def host_rate(eng, args, rank, dist, torch, base):
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     # host memory stays bounded: the two pushes are generated straight into the
     # pinned slots, the 16-bit slots are converted from them a tick at a time,
-    # and the pageable leg's two host arrays live only during that leg
+    # and the pageable leg's one host array (push 0's audio, submitted every
+    # step) lives only during that leg
     slots = []
     for k in range(DEPTH):  # slot k holds push k & 1
         sl = e.input_slot()[:T]
@@ -305,7 +306,7 @@ def host_rate(eng, args, rank, dist, torch, base):
     for kind in ("pinned", "pageable", "pinned_i16"):
         pages = None
         if kind == "pageable":
-            pages = [np.array(slots[0]), np.array(slots[1])]
+            pages = np.array(slots[0])
         elif kind == "pinned_i16":
             for k in range(DEPTH):  # the same audio as 16-bit samples, slot by slot
                 sl16 = e.input_slot_i16()[:T]
@@ -325,7 +326,7 @@ def host_rate(eng, args, rank, dist, torch, base):
             if kind == "pinned_i16":
                 e.submit_i16(e.input_slot_i16()[:T])
             else:
-                e.submit(e.input_slot()[:T] if kind == "pinned" else pages[k & 1])
+                e.submit(e.input_slot()[:T] if kind == "pinned" else pages)
             inflight += 1
         while inflight:
             e.collect(want=True)
@@ -333,6 +334,7 @@ def host_rate(eng, args, rank, dist, torch, base):
         e.sync()
         barrier(dist, torch)
         sec = max_over_ranks(time.perf_counter() - t0, dist, torch)
+        rss_stage("host_" + kind)
         res[kind] = (aggregate_rate(B * Ch * T, 1 if dist is None else dist.get_world_size(), args.steps, sec),
                      1000.0 * sec / args.steps)
     return {"value": round(res["pinned"][0], 1), "unit": "frames/s", "ms_per_step": round(res["pinned"][1], 3),
@@ -340,7 +342,7 @@ def host_rate(eng, args, rank, dist, torch, base):
             "i16_value": round(res["pinned_i16"][0], 1), "i16_ms_per_step": round(res["pinned_i16"][1], 3),
             "input_bytes_per_step": int(slots[0].nbytes), "i16_input_bytes_per_step": int(slots[0].nbytes // 2),
             "note": "streaming submit/collect, 3 pushes in flight, input = the first two pushes of the synthetic "
-                    "streams alternating: from pinned host slots (value) or pageable host memory (pageable_value), "
+                    "streams alternating: from pinned host slots (value) or one pageable host array holding the first push (pageable_value), "
                     "H2D over PCIe inside the timed region and overlapped with the previous push; per-tick "
                     "outputs copied back every push; i16_value: the same audio as 16-bit samples from the pinned "
                     "16-bit slot (fvad_engine_submit_i16, k / 32768 converted on the device)"}

@@ -299,22 +299,29 @@ __device__ __forceinline__ void fft960_run(const Fft960Tw &t, float2 (*W)[P], in
   __syncthreads();
 }
 
-// Band tables of one persistent workgroup, staged in LDS.
-struct BandTab {
+// Band tables of one persistent workgroup, staged in LDS: the band edges and
+// interpolation weights (every band sum and gain interpolation), plus the DCT
+// matrix for the kernels that compute cepstra (k_synthw keeps only the edges).
+struct BandEdges {
   float frac[400];
   int of[400];
   int e4[kBands + 2];
+};
+struct BandTab : BandEdges {
   float dct[kBands * kBands];
 };
-__device__ __forceinline__ void bandtab_load(BandTab &b, const Plan *__restrict__ P, int tid, int nt) {
+__device__ __forceinline__ void bandedges_load(BandEdges &b, const Plan *__restrict__ P, int tid, int nt) {
   for (int i = tid; i < 400; i += nt) {
     b.frac[i] = P->band_frac[i];
     b.of[i] = P->band_of[i];
   }
   for (int i = tid; i < kBands; i += nt) b.e4[i] = P->eband4[i];
+}
+__device__ __forceinline__ void bandtab_load(BandTab &b, const Plan *__restrict__ P, int tid, int nt) {
+  bandedges_load(b, P, tid, nt);
   for (int i = tid; i < kBands * kBands; i += nt) b.dct[i] = P->dct[i];
 }
-__device__ __forceinline__ float band_sum_t(const float2 *A, const float2 *B, const BandTab &T, int b) {
+__device__ __forceinline__ float band_sum_t(const float2 *A, const float2 *B, const BandEdges &T, int b) {
   float acc = 0;
   if (b >= 1) {
 #pragma unroll 4
@@ -341,13 +348,13 @@ __device__ __forceinline__ float band_sum_t(const float2 *A, const float2 *B, co
 //   hi[k] = frac[k] * tmp        (summed into band i + 1),  tmp = A.x*B.x + A.y*B.y,
 // with exactly band_sum_t's roundings; band_chain() then adds them in band_sum_t's
 // order.  Band edges are multiples of 4, so the chain reads 4 terms per load.
-__device__ __forceinline__ void band_terms(float2 A, float2 B, const BandTab &T, int k, float &lo, float &hi) {
+__device__ __forceinline__ void band_terms(float2 A, float2 B, const BandEdges &T, int k, float &lo, float &hi) {
   float tmp = A.x * B.x;
   tmp += A.y * B.y;
   hi = T.frac[k] * tmp;
   lo = (1 - T.frac[k]) * tmp;
 }
-__device__ __forceinline__ float band_chain(const float *lo, const float *hi, const BandTab &T, int b) {
+__device__ __forceinline__ float band_chain(const float *lo, const float *hi, const BandEdges &T, int b) {
   float acc = 0;
   if (b >= 1) {
     const float4 *h4 = reinterpret_cast<const float4 *>(hi);
@@ -373,7 +380,7 @@ __device__ __forceinline__ float band_chain(const float *lo, const float *hi, co
   return acc;
 }
 
-__device__ __forceinline__ float interp_gain_t(const float *bandE, const BandTab &T, int k) {
+__device__ __forceinline__ float interp_gain_t(const float *bandE, const BandEdges &T, int k) {
   if (k >= 400) return 0.0f;
   const int b = T.of[k];
   const float frac = T.frac[k];

@@ -1393,9 +1393,13 @@ double initial_avg(size_t n, double init) {
 }  // namespace
 
 int vadm_reset(fvad_engine *e) {
-  std::vector<float> buf(e->vadm_buf_len, 0.0f);  // initial entries are K.init, tracked by lt_nw
   std::vector<fvad::VadmState> st = e->vadm_init;
-  if (e->dbg_lt_full) {
+  if (!e->dbg_lt_full) {
+    // every entry 0.0f (initial entries are K.init, tracked by lt_nw): a device
+    // memset, no host image of the buffers (hundreds of MB at 2048 streams)
+    HIP_TRY(hipMemset(e->vadm.buf, 0, e->vadm_buf_len * sizeof(float)));
+  } else {
+    std::vector<float> buf(e->vadm_buf_len, 0.0f);
     // test hook FVAD_DEBUG_VADM_LT_FULL: every long-term entry counts as pushed
     // (holding (float)init), the state of a stream past its first
     // long_term_speech_avg_sec -- timing only, not the reference's values
@@ -1406,8 +1410,8 @@ int vadm_reset(fvad_engine *e) {
         for (int i = 0; i < K.n_lt; i++) buf[K.lt_off + (size_t)s * K.lt_pitch + i] = (float)K.init;
       for (int s = 0; s < B; s++) st[(size_t)m * B + s].lt_nw = (unsigned)K.n_lt;
     }
+    HIP_TRY(hipMemcpy(e->vadm.buf, buf.data(), buf.size() * sizeof(float), hipMemcpyHostToDevice));
   }
-  HIP_TRY(hipMemcpy(e->vadm.buf, buf.data(), buf.size() * sizeof(float), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->vadm.st, st.data(), st.size() * sizeof(fvad::VadmState), hipMemcpyHostToDevice));
   return FVAD_OK;
 }

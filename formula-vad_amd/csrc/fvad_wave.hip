@@ -37,11 +37,13 @@ constexpr int kWOcc = 3;  // workgroups per CU (<= 168 VGPRs, <= 53 KB LDS)
 // others run alone, where static striding saves the queue atomics.
 constexpr int kWaveStatic = (1 << kWavePspec) | (1 << kWaveSynth);
 __device__ __forceinline__ bool wave_is_static(const StagedArgs &, WaveKernel k) { return (kWaveStatic >> k) & 1; }
+template <int NW = kWNW>
 __device__ __forceinline__ long long wave_first(const StagedArgs &a, WaveKernel k, int slot, int lane) {
-  return wave_is_static(a, k) ? (long long)blockIdx.x * kWNW + (threadIdx.x >> 6) : wave_take(a, slot, lane);
+  return wave_is_static(a, k) ? (long long)blockIdx.x * NW + (threadIdx.x >> 6) : wave_take(a, slot, lane);
 }
+template <int NW = kWNW>
 __device__ __forceinline__ long long wave_next(const StagedArgs &a, WaveKernel k, int slot, int lane, long long g) {
-  return wave_is_static(a, k) ? g + (long long)gridDim.x * kWNW : wave_take(a, slot, lane);
+  return wave_is_static(a, k) ? g + (long long)gridDim.x * NW : wave_take(a, slot, lane);
 }
 
 // A batch's frame indices, lane fr < kWB holding slot fr's frame (or -1),
@@ -299,21 +301,35 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_synthw(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
-  __shared__ WaveTabs tb;
-  __shared__ float bp[kWNW][3][kBands + 2];  // r, nrm, smoothed gains of the wave's frame
+// k_synthw: kSNW waves per workgroup sharing one copy of the tables (band
+// edges without the DCT, twiddles, window): 2 workgroups = 16 waves per CU,
+// 4 per SIMD, within 160 KB of LDS and 128 VGPRs (the other wave kernels hold
+// 3 per SIMD: their VGPRs exceed 128)
+constexpr int kSNW = 8;
+constexpr int kSOcc = 4;  // waves per SIMD
+struct SynthTabs {
+  BandEdges T;
+  wfft::TwTab tw;
+  float hw[kFrame];
+};
+__global__ void __launch_bounds__(64 * kSNW, kSOcc) k_synthw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kSNW][wfft::kSlots];
+  __shared__ SynthTabs tb;
+  __shared__ float bp[kSNW][3][kBands + 2];  // r, nrm, smoothed gains of the wave's frame
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  wave_tabs_load(tb, a.plan, tid);
+  bandedges_load(tb.T, a.plan, tid, 64 * kSNW);
+  wfft::load_twtab(tb.tw, reinterpret_cast<const float2 *>(a.plan->tw960), tid, 64 * kSNW);
+  for (int i = tid; i < kFrame; i += 64 * kSNW) tb.hw[i] = a.plan->half_window[i];
   wfft::Tw tw;
   wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
   __syncthreads();
-  const BandTab &T = tb.T;
+  const BandEdges &T = tb.T;
   float2 *R = Rg[wv];
   float *tr = reinterpret_cast<float *>(R);
   float *rr = bp[wv][0], *nrm = bp[wv][1], *gsm = bp[wv][2];
   const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
-  for (long long g = wave_first(a, kWaveSynth, kWorkSynth, lane); g < nb; g = wave_next(a, kWaveSynth, kWorkSynth, lane, g)) {
+  for (long long g = wave_first<kSNW>(a, kWaveSynth, kWorkSynth, lane); g < nb;
+       g = wave_next<kSNW>(a, kWaveSynth, kWorkSynth, lane, g)) {
     // the batch's frames and silence flags, lane per frame
     const int fl = batch_frames(a, g, lane);
     const int sl = fl >= 0 ? a.silence[fl] : 0;
@@ -834,9 +850,9 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_olafb(StagedArgs a) {
 namespace {
 // workgroups of a kernel one CU holds (occupancy calculator, once per kernel)
 template <typename K>
-int wave_per_cu(K kernel) {
+int wave_per_cu(K kernel, int nw = kWNW) {
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64 * kWNW, 0) != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64 * nw, 0) != hipSuccess || per_cu < 1)
     per_cu = 1;
   return per_cu;
 }
@@ -844,7 +860,7 @@ int wave_per_cu(K kernel) {
 
 // n_cu: the CUs the engine's stream may use (all, or its CU mask's)
 hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream) {
-  static const int p_fftA = wave_per_cu(k_fftAw), p_pspec = wave_per_cu(k_pspecw), p_synth = wave_per_cu(k_synthw),
+  static const int p_fftA = wave_per_cu(k_fftAw), p_pspec = wave_per_cu(k_pspecw), p_synth = wave_per_cu(k_synthw, kSNW),
                    p_fftb = wave_per_cu(k_fftbw), p_olafb = wave_per_cu(k_olafb);
   const int g_fftA = p_fftA * n_cu, g_pspec = p_pspec * n_cu, g_synth = p_synth * n_cu, g_fftb = p_fftb * n_cu,
             g_olafb = p_olafb * n_cu;
@@ -864,8 +880,8 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
   // dynamic mode: queue x is served by the blocks with blockIdx % 8 == x, so
   // the grid covers min(batches, 8) blocks at least; static mode: batches /
   // kWNW blocks suffice
-  auto grid = [&](int resident) {
-    const long long want = ((kWaveStatic >> which) & 1) ? (batches + kWNW - 1) / kWNW : batches;
+  auto grid = [&](int resident, int nw = kWNW) {
+    const long long want = ((kWaveStatic >> which) & 1) ? (batches + nw - 1) / nw : batches;
     return dim3((unsigned)std::min<long long>(std::max<long long>(want, 1), resident));
   };
   if (which == kWaveFftA)
@@ -873,7 +889,7 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
   else if (which == kWavePspec)
     hipLaunchKernelGGL(k_pspecw, grid(g_pspec), dim3(64 * kWNW), 0, stream, a);
   else
-    hipLaunchKernelGGL(k_synthw, grid(g_synth), dim3(64 * kWNW), 0, stream, a);
+    hipLaunchKernelGGL(k_synthw, grid(g_synth, kSNW), dim3(64 * kSNW), 0, stream, a);
   return hipGetLastError();
 }
 
