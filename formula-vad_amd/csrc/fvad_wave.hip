@@ -29,7 +29,7 @@ namespace fvad {
 // ---------------------------------------------------------------------------
 constexpr int kWB = 8;   // frames per wave batch
 constexpr int kWNW = 4;  // waves per workgroup
-constexpr int kWOcc = 3;  // workgroups per CU (<= 168 VGPRs, <= 53 KB LDS)
+constexpr int kWOcc = 3;  // waves per SIMD (<= 168 VGPRs; 3 workgroups per CU at <= 53 KB LDS)
 
 // Batches of a wave: dynamic (per-XCD queues, wave_take) or static striding
 // over the grid's waves, per kernel (bit 1 << kind of kWaveStatic).  k_fftAw
@@ -79,11 +79,10 @@ __device__ __forceinline__ void wave_tabs_load(WaveTabs &w, const Plan *__restri
   for (int i = tid; i < kFrame; i += 64 * kWNW) w.hw[i] = P->half_window[i];
 }
 
-// A frame's raw window samples.  k_pspecw loads them one frame ahead (the
-// transform needs them first thing: without the prefetch each frame waited a
-// memory latency on them, 0.07 ms of k_pspecw's 0.55 and 0.1 of k_fftAw's
-// 0.66, measured by a build that skipped the loads; k_fftAw, at 141 VGPRs,
-// gained nothing from the same prefetch at its 168-register limit)
+// A frame's raw window samples.  (Loading them one frame ahead saved k_pspecw
+// 0.07 ms at 3 waves per SIMD; its 16 registers kept it there.  Without the
+// prefetch it fits 128 VGPRs and runs 4 waves per SIMD, which hide that
+// latency better: 0.531 -> 0.497 ms.)
 struct WinRaw {
   float x[16];
 };
@@ -209,11 +208,16 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
+// k_pspecw: as k_synthw, kPNW waves per workgroup on one table copy, 2
+// workgroups per CU = 4 waves per SIMD (<= 128 VGPRs, 79 KB of LDS)
+constexpr int kPNW = 8;
+__global__ void __launch_bounds__(64 * kPNW, 4) k_pspecw(StagedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 Rg[kPNW][wfft::kSlots];
   __shared__ WaveTabs tb;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  wave_tabs_load(tb, a.plan, tid);
+  bandtab_load(tb.T, a.plan, tid, 64 * kPNW);
+  wfft::load_twtab(tb.tw, reinterpret_cast<const float2 *>(a.plan->tw960), tid, 64 * kPNW);
+  for (int i = tid; i < kFrame; i += 64 * kPNW) tb.hw[i] = a.plan->half_window[i];
   wfft::Tw tw;
   wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
   __syncthreads();
@@ -221,19 +225,18 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
   float2 *R = Rg[wv];
   float *tr = reinterpret_cast<float *>(R);
   const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
-  for (long long g = wave_first(a, kWavePspec, kWorkPspec, lane); g < nb; g = wave_next(a, kWavePspec, kWorkPspec, lane, g)) {
+  for (long long g = wave_first<kPNW>(a, kWavePspec, kWorkPspec, lane); g < nb;
+       g = wave_next<kPNW>(a, kWavePspec, kWorkPspec, lane, g)) {
     // the batch's frames and their pitches, lane per frame
     const int fl = batch_frames(a, g, lane);
     const int pl = fl >= 0 ? a.pitch[fl] : 0;
     settle(pl);
     auto pwin = [&](int f, int fr) { return frame_pb(a, f) + (kPitchBuf - kWin - lane_val(pl, fr)); };
-    // frames in pairs, two sets of window registers: frame fr + 1's samples
-    // load while frame fr is transformed
-    auto frame = [&](int fr, WinRaw &cur, WinRaw &nxt) __attribute__((always_inline)) {
-      const int fn = fr + 1 < kWB ? lane_val(fl, fr + 1) : -1;
-      if (fn >= 0) win_load(nxt, pwin(fn, fr + 1), lane);
+    auto frame = [&](int fr) __attribute__((always_inline)) {
       const int f = lane_val(fl, fr);
       if (f < 0) return;
+      WinRaw cur;
+      win_load(cur, pwin(f, fr), lane);
       const int pit = lane_val(pl, fr);
       // X of bins < 400 (Exp terms) and the band's Ex, issued before the
       // transform (Ex loaded after the P stores waited for them)
@@ -287,17 +290,8 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_pspecw(StagedArgs a) {
       }
       wfft::wsync();
     };
-    WinRaw wa, wb;
-    {
-      const int f0 = lane_val(fl, 0);
-      if (f0 >= 0) win_load(wa, pwin(f0, 0), lane);
-    }
-    static_assert(kWB % 2 == 0, "frame pairs");
 #pragma unroll 1
-    for (int fr = 0; fr < kWB; fr += 2) {
-      frame(fr, wa, wb);
-      frame(fr + 1, wb, wa);
-    }
+    for (int fr = 0; fr < kWB; fr++) frame(fr);
   }
 }
 
@@ -860,7 +854,7 @@ int wave_per_cu(K kernel, int nw = kWNW) {
 
 // n_cu: the CUs the engine's stream may use (all, or its CU mask's)
 hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream) {
-  static const int p_fftA = wave_per_cu(k_fftAw), p_pspec = wave_per_cu(k_pspecw), p_synth = wave_per_cu(k_synthw, kSNW),
+  static const int p_fftA = wave_per_cu(k_fftAw), p_pspec = wave_per_cu(k_pspecw, kPNW), p_synth = wave_per_cu(k_synthw, kSNW),
                    p_fftb = wave_per_cu(k_fftbw), p_olafb = wave_per_cu(k_olafb);
   const int g_fftA = p_fftA * n_cu, g_pspec = p_pspec * n_cu, g_synth = p_synth * n_cu, g_fftb = p_fftb * n_cu,
             g_olafb = p_olafb * n_cu;
@@ -887,7 +881,7 @@ hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStrea
   if (which == kWaveFftA)
     hipLaunchKernelGGL(k_fftAw, grid(g_fftA), dim3(64 * kWNW), 0, stream, a);
   else if (which == kWavePspec)
-    hipLaunchKernelGGL(k_pspecw, grid(g_pspec), dim3(64 * kWNW), 0, stream, a);
+    hipLaunchKernelGGL(k_pspecw, grid(g_pspec, kPNW), dim3(64 * kPNW), 0, stream, a);
   else
     hipLaunchKernelGGL(k_synthw, grid(g_synth, kSNW), dim3(64 * kSNW), 0, stream, a);
   return hipGetLastError();
