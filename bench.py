@@ -147,15 +147,20 @@ def stream_partition(rank, streams_per_gpu):
 
 
 RSS_STAGES = {}
+RSS_ANON = {}
 
 
 def rss_stage(name):
-    """Current resident set (MB) of this process at a named stage (host_memory.stages)."""
+    """This process's resident set (MB) at a named stage (host_memory.stages):
+    VmRSS, and RssAnon (the heap: what the pinned slots, which the kernel
+    driver maps and counts as file / shared pages, are not part of)."""
     try:
         with open("/proc/self/status") as f:
-            kb = next(int(ln.split()[1]) for ln in f if ln.startswith("VmRSS:"))
-        RSS_STAGES[name] = round(kb / 1024.0, 1)
-    except (OSError, StopIteration):
+            kb = {ln.split(":")[0]: int(ln.split()[1]) for ln in f if ln.startswith(("VmRSS:", "RssAnon:"))}
+        RSS_STAGES[name] = round(kb["VmRSS"] / 1024.0, 1)
+        if "RssAnon" in kb:
+            RSS_ANON[name] = round(kb["RssAnon"] / 1024.0, 1)
+    except (OSError, KeyError, ValueError, IndexError):
         pass
 
 
@@ -388,14 +393,15 @@ def main():
         lt_full: the device VADMachines start as in a stream past its first
         long_term_speech_avg_sec (every long-term entry pushed; timing hook
         FVAD_DEBUG_VADM_LT_FULL, values not the reference's)"""
+        leg = mode + ("_lt_full" if lt_full else "")
         e = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=mode)
-        rss_stage("engine_%s" % mode)
+        rss_stage("engine_%s" % leg)
         if mode != "fused" and not args.no_vadm:
             e.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
             if lt_full:
                 e.set_debug(fvad.DEBUG_VADM_LT_FULL, 1)
         e.load_synthetic(T, base=base, pushes=P)
-        rss_stage("resident_input_%s" % mode)
+        rss_stage("resident_input_%s" % leg)
         for _ in range(args.warmup):
             e.run_resident(T)
         e.sync()
@@ -456,7 +462,8 @@ def main():
     import resource
     host_mem = {"peak_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1),
                 "pinned_slots_mb": round(DEPTH * (B * Ch * T * 480 * 6 + B * T * 4 * 8) / 2 ** 20, 1)
-                if args.host_rate else 0.0, "stages_rss_mb": dict(RSS_STAGES)}
+                if args.host_rate else 0.0, "stages_rss_mb": dict(RSS_STAGES),
+                "stages_anon_mb": dict(RSS_ANON)}
     host_mem_all = None
     if dist is not None:
         host_mem_all = [None] * world

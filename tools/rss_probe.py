@@ -11,17 +11,22 @@ sys.path.insert(0, os.path.join(ROOT, "formula-vad_amd"))
 import fvad  # noqa: E402
 
 
+KEYS = ("VmRSS", "RssAnon", "RssFile", "RssShmem")
+
+
 def rss():
     with open("/proc/self/status") as f:
-        return next(int(ln.split()[1]) for ln in f if ln.startswith("VmRSS:")) / 1024.0
+        kb = {ln.split(":")[0]: int(ln.split()[1]) for ln in f if ln.startswith(tuple(k + ":" for k in KEYS))}
+    return [kb.get(k, 0) / 1024.0 for k in KEYS]
 
 
 last = [rss()]
+print("%-34s " % "stage" + " ".join("%18s" % k for k in KEYS))
 
 
 def stage(name):
     r = rss()
-    print("%-34s %8.1f MB  (%+8.1f)" % (name, r, r - last[0]), flush=True)
+    print("%-34s " % name + " ".join("%8.1f (%+8.1f)" % (v, v - w) for v, w in zip(r, last[0])), flush=True)
     last[0] = r
 
 
