@@ -74,10 +74,24 @@ def parse():
                     help="also time pushes from host buffers (PCIe-inclusive; reported as host_buffers, never value)")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="no GPU: gloo ranks with a stub engine (tests the launcher, barrier and max-reduce)")
+    ap.add_argument("--rehearse-on-gpu0", action="store_true",
+                    help="multi-rank rehearsal on a 1-GPU box: every rank's engine on device 0, gloo collectives "
+                         "(exercises the N > 1 path end to end; the ranks share one GPU, so the rate is no "
+                         "scaling figure and the line says so)")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="engines per GPU (fvad.EngineGroup): the rank's streams split into this many "
+                         "sub-partitions pushing concurrently, k_prep3 / VADMachines on shared side streams "
+                         "(opt-in: the gain depends on the runtime's hardware-queue placement, DESIGN.md 8 r5)")
+    ap.add_argument("--one-engine-leg", type=int, default=1,
+                    help="with --groups > 1, also time one engine over all the rank's streams "
+                         "(roofline.one_engine: each kernel alone on the GPU)")
     ap.add_argument("--variants", type=int, default=1,
                     help="staged runs: also time the fp16 engine mode (configs[4]'s variant) on the same "
                          "workload and report it under `variants` (never `value`)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.groups < 1 or a.streams_per_gpu % a.groups:
+        ap.error("--groups must divide --streams-per-gpu")
+    return a
 
 
 def maybe_spawn(args):
@@ -277,80 +291,90 @@ def stub_main(args):
 DEPTH = 3  # FVAD_MAX_IN_FLIGHT (include/fvad.h)
 
 
-def host_rate(eng, args, rank, dist, torch, base):
+def host_rate(grp, args, rank, dist, torch, base):
     """Streaming from host memory (fvad_engine_input_slot / submit / collect):
-    FVAD_MAX_IN_FLIGHT = 3 pushes in flight, the input's H2D copy over PCIe
-    overlapping the earlier pushes' kernels, outputs copied back every push.
-    Input: the first two pushes of the resident synthetic audio, alternating.  pinned: the
-    producer writes each push into the engine's pinned slot (the copy cost of
-    the producer itself is not counted); pageable: submit from an ordinary
-    host array (plus a threaded copy into the slot); pinned_i16: the same
-    audio as 16-bit samples through fvad_engine_input_slot_i16 /
-    submit_i16 (half the PCIe bytes, converted on the device)."""
+    FVAD_MAX_IN_FLIGHT = 3 pushes in flight per engine of the group, the
+    input's H2D copy over PCIe overlapping the earlier pushes' kernels,
+    outputs copied back every push.  Input: the first two pushes of the
+    resident synthetic audio, alternating.  pinned: the producer writes each
+    push into the engines' pinned slots (the copy cost of the producer itself
+    is not counted); pageable: submit from ordinary host arrays (plus a
+    threaded copy into the slot); pinned_i16: the same audio as 16-bit samples
+    through fvad_engine_input_slot_i16 / submit_i16 (half the PCIe bytes,
+    converted on the device)."""
     import fvad
     import numpy as np
-    e = eng
-    B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
+    es = grp.engines
+    Ch, T = args.channels, args.ticks
     # host memory stays bounded: the two pushes are generated straight into the
     # pinned slots, the 16-bit slots are converted from them a tick at a time,
-    # and the pageable leg's one host array (push 0's audio, submitted every
-    # step) lives only during that leg
-    slots = []
+    # and the pageable leg's host arrays (push 0's audio, submitted every step)
+    # live only during that leg
+    slots = [[] for _ in es]
     for k in range(DEPTH):  # slot k holds push k & 1
-        sl = e.input_slot()[:T]
-        if k < 2:
-            fvad.synth_ticks(base, B, Ch, args.resident_pushes * T, k * T, T, out=sl)
-        else:
-            sl[...] = slots[0]
-        slots.append(sl)
-        e.submit(sl)
+        for g, e in enumerate(es):
+            sl = e.input_slot()[:T]
+            if k < 2:
+                fvad.synth_ticks(base + grp.first[g], grp.sizes[g], Ch, args.resident_pushes * T, k * T, T, out=sl)
+            else:
+                sl[...] = slots[g][0]
+            slots[g].append(sl)
+            e.submit(sl)
     for _ in range(DEPTH):
-        e.collect(want=False)
-    e.sync()
+        for e in es:
+            e.collect(want=False)
+    grp.sync()
     res = {}
     for kind in ("pinned", "pageable", "pinned_i16"):
         pages = None
         if kind == "pageable":
-            pages = np.array(slots[0])
+            pages = [np.array(sg[0]) for sg in slots]
         elif kind == "pinned_i16":
             for k in range(DEPTH):  # the same audio as 16-bit samples, slot by slot
-                sl16 = e.input_slot_i16()[:T]
-                for t in range(T):
-                    sl16[t] = np.clip(np.round(slots[k][t] * np.float32(32768.0)), -32768, 32767)
-                e.submit_i16(sl16)
+                for g, e in enumerate(es):
+                    sl16 = e.input_slot_i16()[:T]
+                    for t in range(T):
+                        sl16[t] = np.clip(np.round(slots[g][k][t] * np.float32(32768.0)), -32768, 32767)
+                    e.submit_i16(sl16)
             for _ in range(DEPTH):
-                e.collect(want=False)
-        e.sync()
+                for e in es:
+                    e.collect(want=False)
+        grp.sync()
         barrier(dist, torch)
         t0 = time.perf_counter()
         inflight = 0
         for k in range(args.steps):
             if inflight == DEPTH:
-                e.collect(want=True)
+                for e in es:
+                    e.collect(want=True)
                 inflight -= 1
-            if kind == "pinned_i16":
-                e.submit_i16(e.input_slot_i16()[:T])
-            else:
-                e.submit(e.input_slot()[:T] if kind == "pinned" else pages)
+            for g, e in enumerate(es):
+                if kind == "pinned_i16":
+                    e.submit_i16(e.input_slot_i16()[:T])
+                else:
+                    e.submit(e.input_slot()[:T] if kind == "pinned" else pages[g])
             inflight += 1
         while inflight:
-            e.collect(want=True)
+            for e in es:
+                e.collect(want=True)
             inflight -= 1
-        e.sync()
+        grp.sync()
         barrier(dist, torch)
         sec = max_over_ranks(time.perf_counter() - t0, dist, torch)
         rss_stage("host_" + kind)
-        res[kind] = (aggregate_rate(B * Ch * T, 1 if dist is None else dist.get_world_size(), args.steps, sec),
+        res[kind] = (aggregate_rate(grp.B * Ch * T, 1 if dist is None else dist.get_world_size(), args.steps, sec),
                      1000.0 * sec / args.steps)
+    in_bytes = sum(int(sg[0].nbytes) for sg in slots)
     return {"value": round(res["pinned"][0], 1), "unit": "frames/s", "ms_per_step": round(res["pinned"][1], 3),
             "pageable_value": round(res["pageable"][0], 1), "pageable_ms_per_step": round(res["pageable"][1], 3),
             "i16_value": round(res["pinned_i16"][0], 1), "i16_ms_per_step": round(res["pinned_i16"][1], 3),
-            "input_bytes_per_step": int(slots[0].nbytes), "i16_input_bytes_per_step": int(slots[0].nbytes // 2),
-            "note": "streaming submit/collect, 3 pushes in flight, input = the first two pushes of the synthetic "
-                    "streams alternating: from pinned host slots (value) or one pageable host array holding the first push (pageable_value), "
-                    "H2D over PCIe inside the timed region and overlapped with the previous push; per-tick "
-                    "outputs copied back every push; i16_value: the same audio as 16-bit samples from the pinned "
-                    "16-bit slot (fvad_engine_submit_i16, k / 32768 converted on the device)"}
+            "input_bytes_per_step": in_bytes, "i16_input_bytes_per_step": in_bytes // 2,
+            "note": "streaming submit/collect, 3 pushes in flight per engine, input = the first two pushes of the "
+                    "synthetic streams alternating: from pinned host slots (value) or pageable host arrays holding "
+                    "the first push (pageable_value), H2D over PCIe inside the timed region and overlapped with "
+                    "the previous push; per-tick outputs copied back every push; i16_value: the same audio as "
+                    "16-bit samples from the pinned 16-bit slots (fvad_engine_submit_i16, k / 32768 converted on "
+                    "the device)"}
 
 
 def gather_kernel_tables(kt, dist, torch, rank):
@@ -380,7 +404,9 @@ def main():
     maybe_spawn(args)
     if args.cpu_stub:
         return stub_main(args)
-    rank, world, local, dist, torch = dist_setup(args.gpus)
+    rank, world, local, dist, torch = dist_setup(args.gpus, backend="gloo" if args.rehearse_on_gpu0 else "nccl")
+    if args.rehearse_on_gpu0:
+        local = 0
     import fvad
     from fvad import cost
 
@@ -388,18 +414,19 @@ def main():
     model = fvad.Model(seed=1)
     base, _ = stream_partition(rank, B)
 
-    def measure(mode, lt_full=False):
+    def measure(mode, lt_full=False, groups=None):
         """warmup, then exactly args.steps pushes between barriers; max over ranks.
-        lt_full: the device VADMachines start as in a stream past its first
-        long_term_speech_avg_sec (every long-term entry pushed; timing hook
-        FVAD_DEBUG_VADM_LT_FULL, values not the reference's)"""
-        leg = mode + ("_lt_full" if lt_full else "")
-        e = fvad.Engine(model, B, Ch, device=local, max_ticks=T, mode=mode)
+        The rank's streams as `groups` engines pushing concurrently
+        (fvad.EngineGroup).  lt_full: the device VADMachines start as in a
+        stream past its first long_term_speech_avg_sec (every long-term entry
+        pushed; timing hook FVAD_DEBUG_VADM_LT_FULL, values not the reference's)"""
+        groups = args.groups if groups is None else groups
+        leg = mode + ("_lt_full" if lt_full else "") + ("_g%d" % groups if groups != args.groups else "")
+        vadm = mode != "fused" and not args.no_vadm  # VADMachine.run per window on the device
+        e = fvad.EngineGroup(model, B, Ch, groups=groups, vadm=vadm, device=local, max_ticks=T, mode=mode)
         rss_stage("engine_%s" % leg)
-        if mode != "fused" and not args.no_vadm:
-            e.attach_vadm()  # VADMachine.run per window on the device: the full per-frame VAD path
-            if lt_full:
-                e.set_debug(fvad.DEBUG_VADM_LT_FULL, 1)
+        if vadm and lt_full:
+            e.set_debug(fvad.DEBUG_VADM_LT_FULL, 1)
         e.load_synthetic(T, base=base, pushes=P)
         rss_stage("resident_input_%s" % leg)
         for _ in range(args.warmup):
@@ -424,9 +451,18 @@ def main():
 
     host = host_rate(eng, args, rank, dist, torch, base) if args.host_rate else None
     rss_stage("after_host_buffers")
+    del eng  # one engine group's buffers at a time
+    one = None
+    if args.groups > 1 and args.one_engine_leg:
+        # the same workload on one engine per GPU: its kernels run alone, so
+        # their events give the isolated per-launch roofline beside the
+        # co-running one of the line's own run
+        e1, el1, kt1 = measure(args.mode, groups=1)
+        del e1
+        kt1, _ = gather_kernel_tables(kt1, dist, torch, rank)
+        one = (el1, kt1)
     variants = None
     if args.variants and args.mode == "staged":
-        del eng  # one engine's buffers at a time
         e16, el16, kt16 = measure("fp16")
         del e16
         kt16, _ = gather_kernel_tables(kt16, dist, torch, rank)
@@ -478,7 +514,8 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32" if args.mode != "fp16" else "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
-        "data": "synthetic",
+        "data": "synthetic" + ("; REHEARSAL: %d ranks sharing GPU 0 over gloo (--rehearse-on-gpu0), not a "
+                               "scaling figure" % world if args.rehearse_on_gpu0 else ""),
         "config": {"workload": "configs[4] per-GPU partition: %d synthetic 48 kHz streams x %d ch per GPU "
                                "(%d at %d GPU), %d ticks (480 samples/ch) per step, %d distinct resident pushes "
                                "(%.1f s of every stream) cycled, %s"
@@ -487,13 +524,28 @@ def main():
                                   else "fp32 weights, bit-exact path"),
                    "streams_per_gpu": B, "channels": Ch, "ticks_per_step": T, "resident_pushes": P,
                    "fft_size": 2048,
-                   "parallelism": "stream-partition x%d (no collectives)" % world, "mode": args.mode,
+                   "parallelism": "stream-partition x%d (no collectives), %d engines per GPU" % (world, args.groups),
+                   "engines_per_gpu": args.groups, "mode": args.mode,
                    "vad_machine": "device" if (args.mode != "fused" and not args.no_vadm) else "none",
                    },
         "realtime_streams": round(value / (100.0 * Ch), 1),
         "roofline": roofline(args, kt, value, world, ms_per_step, cost, ranks),
+        "engines_per_gpu": args.groups,
         "cpu_baseline": None,
     }
+    if one is not None:
+        el1, kt1 = one
+        v1 = aggregate_rate(B * Ch * T, world, args.steps, el1)
+        r1 = roofline(args, kt1, v1, world, 1000.0 * el1 / args.steps, cost, None, groups=1)
+        line["roofline"]["one_engine"] = {
+            "value": round(v1, 1), "ms_per_step": round(1000.0 * el1 / args.steps, 3),
+            "kernel": r1.get("kernel"), "achieved": r1.get("achieved"), "frac": r1.get("frac"),
+            "frac_attainable": r1.get("frac_attainable"), "kernel_ms_avg": r1.get("kernel_ms_avg"),
+            "traffic": r1.get("traffic"), "kernels_ms": {k: v["ms"] for k, v in r1.get("kernels", {}).items()},
+            "note": "the same workload on ONE engine per GPU (%d streams per launch), measured in its own leg: "
+                    "each kernel alone on the GPU.  The line's value runs %d engines of %d streams whose kernels "
+                    "co-run, so its per-launch times (roofline.kernels) include sharing the GPU with the other "
+                    "engines' kernels" % (B, args.groups, B // args.groups)}
     line["host_memory"] = dict(host_mem, **({"per_rank_peak_rss_mb": [h["peak_rss_mb"] for h in host_mem_all]}
                                             if host_mem_all else {}))
     if variants is not None:
@@ -513,13 +565,17 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(args, kt, value, world, ms_per_step, cost, ranks):
+def roofline(args, kt, value, world, ms_per_step, cost, ranks, groups=None):
     """Roofline of the dominant kernel, per launch, from HIP events recorded
     around each kernel on the stream it runs on (fvad_engine_kernel_times; at
     N > 1 the max over ranks), plus the whole path against SURVEY.md 8(d)'s
     ceilings.  The engine records the events on every 4th timed push
-    (FVAD_EVENT_EVERY): on every push their markers cost it ~1 %."""
-    B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
+    (FVAD_EVENT_EVERY): on every push their markers cost it ~1 %.  With
+    `groups` engines per GPU a launch covers one engine's streams (B / groups)
+    and co-runs with the other engines' kernels."""
+    groups = args.groups if groups is None else groups
+    Ball, Ch, T = args.streams_per_gpu, args.channels, args.ticks
+    B = Ball // groups  # streams per launch (the bench's B is a multiple of groups)
     frames_launch = B * Ch * T
     if args.mode == "fused":
         prep_share = cost.phases(Ch)["prep: s16 scale + HP biquad + rms"]
@@ -566,11 +622,13 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks):
         try:
             with open(args.pmc_json) as f:
                 pm = json.load(f)
-            if (pm.get("streams"), pm.get("ticks"), pm.get("channels"), pm.get("mode")) == (B, T, Ch, args.mode):
+            if (pm.get("streams"), pm.get("ticks"), pm.get("channels"), pm.get("mode"),
+                    pm.get("groups", 1)) == (Ball, T, Ch, args.mode, groups):
                 traffic = pm.get("bytes_per_launch", {}).get(dom)
                 pmc_src = os.path.relpath(args.pmc_json, ROOT)
-                # every kernel of a push (the side-stream ones included)
-                push_bytes = sum(v for n, v in pm.get("bytes_per_launch", {}).items() if n in kt["kernels"])
+                # every kernel of a push (the side-stream ones included), every engine
+                push_bytes = groups * sum(v for n, v in pm.get("bytes_per_launch", {}).items()
+                                          if n in kt["kernels"])
         except Exception:
             traffic = None
     if compute_bound:
@@ -631,7 +689,9 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks):
         # measured time per push: the pipeline's average HBM utilisation
         gbs = push_bytes / (ms_per_step / 1000.0) / 1e9
         out["push_hbm"] = {"bytes": push_bytes, "gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                           "bytes_per_frame": round(push_bytes / frames_launch, 1)}
+                           "bytes_per_frame": round(push_bytes / (groups * frames_launch), 1)}
+    out["engines_per_gpu"] = groups
+    out["streams_per_launch"] = B
     return out
 
 

@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <algorithm>
@@ -81,6 +82,9 @@ struct fvad_engine {
   // alias the buffer of the latest push), buffer b is reused once the push that
   // used it last has finished (ev_buf_free[b])
   hipStream_t pstream = nullptr;
+  // owners of pstream / side: engines of one GPU may share them
+  // (fvad_engine_share_streams), the last one destroys the stream
+  std::shared_ptr<ihipStream_t> pstream_ref, side_ref;
   float *d_xs_b[2] = {}, *d_ratio_b[2] = {}, *d_xlp_b[2] = {};
   int *d_ticks_b[2] = {};
   hipEvent_t ev_prep_done[2] = {}, ev_buf_free[2] = {};
@@ -340,8 +344,10 @@ void free_all(fvad_engine *e) {
     if (ev) (void)hipEventDestroy(ev);
   if (e->d_pcm16) (void)hipFree(e->d_pcm16);
 
-  if (e->side) (void)hipStreamDestroy(e->side);
-  if (e->pstream) (void)hipStreamDestroy(e->pstream);
+  if (e->side && !e->side_ref) (void)hipStreamDestroy(e->side);  // created, not yet owned (a failed attach)
+  if (e->pstream && !e->pstream_ref) (void)hipStreamDestroy(e->pstream);
+  e->side_ref.reset();
+  e->pstream_ref.reset();
   if (e->cstream) (void)hipStreamDestroy(e->cstream);
   for (auto &sl : e->slots) {
     void *hp[] = {sl.in, sl.in16, sl.ticks, sl.vad, sl.ratio, sl.wratio, sl.wvad, sl.band, sl.den, sl.wflag};
@@ -406,6 +412,7 @@ namespace {
 // an engine stream: non-blocking, so the synchronous null-stream copies of the
 // setup calls never wait for queued pushes
 hipError_t make_stream(hipStream_t *s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
+void destroy_stream(ihipStream_t *s) { (void)hipStreamDestroy(s); }
 }  // namespace
 
 extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_model *model, fvad_engine **out) {
@@ -477,6 +484,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
        hipEventCreateWithFlags(&e->ev_buf_free[0], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_buf_free[1], hipEventDisableTiming) != hipSuccess))
     return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
+  if (e->pstream) e->pstream_ref.reset(e->pstream, destroy_stream);
   for (int i = 0; i < e->n_events; i++)
     if (hipEventCreate(&e->evs[0][i]) != hipSuccess || hipEventCreate(&e->evs[1][i]) != hipSuccess)
       return bail(fail(FVAD_EDEVICE, "hipEventCreate failed"));
@@ -585,6 +593,32 @@ extern "C" void fvad_engine_destroy(fvad_engine *e) {
   if (e->side) (void)hipStreamSynchronize(e->side);
   free_all(e);
   delete e;
+}
+
+// e runs its k_prep3 (which & FVAD_SHARE_PREP) and / or its VADMachine
+// kernels (which & FVAD_SHARE_SIDE) on other's streams from now on.  Both
+// engines idle (synchronised here); every dependency stays an event, so
+// sharing only adds order between the engines' side work.
+extern "C" int fvad_engine_share_streams(fvad_engine *e, fvad_engine *other, int which) {
+  if (!e || !other || e == other || (which & ~(FVAD_SHARE_PREP | FVAD_SHARE_SIDE)) || !which)
+    return fail(FVAD_EINVAL, "invalid argument");
+  if (e->cfg.device != other->cfg.device) return fail(FVAD_EINVAL, "engines on different devices");
+  if ((which & FVAD_SHARE_PREP) && (!e->pstream || !other->pstream))
+    return fail(FVAD_EINVAL, "FVAD_SHARE_PREP needs two staged engines");
+  if ((which & FVAD_SHARE_SIDE) && (!e->side || !other->side))
+    return fail(FVAD_EINVAL, "FVAD_SHARE_SIDE needs device VADMachines attached to both engines");
+  int rc;
+  if ((rc = fvad_engine_sync(e)) || (rc = fvad_engine_sync(other))) return rc;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  if (which & FVAD_SHARE_PREP) {
+    e->pstream_ref = other->pstream_ref;
+    e->pstream = other->pstream;
+  }
+  if (which & FVAD_SHARE_SIDE) {
+    e->side_ref = other->side_ref;
+    e->side = other->side;
+  }
+  return FVAD_OK;
 }
 
 namespace {
@@ -1494,6 +1528,7 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
       hipEventCreateWithFlags(&e->ev_vadm_b[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_vadm_b[1], hipEventDisableTiming) != hipSuccess)
     return fail(FVAD_EDEVICE, "side stream / event creation failed");
+  e->side_ref.reset(e->side, destroy_stream);
   e->d_vticks_b[0] = e->d_vticks;
   HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
   HIP_TRY(hipEventRecord(e->ev_vadm_b[0], e->side));

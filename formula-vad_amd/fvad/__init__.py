@@ -96,6 +96,7 @@ class VadmSnapshot(C.Structure):
 
 
 DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR, DEBUG_VADM_LT_FULL = 1, 2, 3
+SHARE_PREP, SHARE_SIDE = 1, 2  # fvad_engine_share_streams
 
 READ_FN = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.c_int, C.POINTER(F32P), C.c_size_t)
 
@@ -178,6 +179,7 @@ SYMBOLS = [
     ("fvad_engine_vadm_snapshot", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("fvad_engine_vadm_rolling", C.c_long, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
     ("fvad_engine_set_debug", C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    ("fvad_engine_share_streams", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     ("fvad_engine_output_log", C.c_int, [C.c_void_p, C.c_int]),
     ("fvad_engine_output_log_read", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int)]),
     ("fvad_engine_clear_times", C.c_int, [C.c_void_p]),
@@ -464,6 +466,12 @@ class Engine:
         lib().fvad_engine_vadm_rolling(self.h, stream, machine, which, out.ctypes.data_as(C.c_void_p), n)
         return out
 
+    def share_streams(self, other, which=SHARE_PREP | SHARE_SIDE):
+        """Run this engine's k_prep3 / VADMachine kernels on other's streams
+        (fvad_engine_share_streams); either engine may be destroyed first:
+        the last one using a stream destroys it."""
+        _check(lib().fvad_engine_share_streams(self.h, other.h, which), "fvad_engine_share_streams")
+
     def set_debug(self, key, value):
         """Test hooks (fvad_engine_set_debug): DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR."""
         _check(lib().fvad_engine_set_debug(self.h, key, value), "fvad_engine_set_debug")
@@ -489,6 +497,72 @@ class Engine:
         except Exception:
             pass
 
+
+
+class EngineGroup:
+    """One GPU's streams as `groups` engines of about n_streams / groups each,
+    pushing concurrently: each engine its own main stream, k_prep3 and the
+    VADMachines of all of them on engine 0's two side streams
+    (fvad_engine_share_streams), so a group of two takes 4 streams where two
+    separate engines would take 6 (the runtime shares its 4 hardware queues
+    round the streams).  Results are each engine's own, bit-identical to one
+    engine over all the streams (tests/test_gpu_groups.py).  Throughput
+    (DESIGN.md section 8, r5): +2-3 % over one engine when it is the first
+    group a process creates, down to -35 % when the runtime's queue placement
+    puts a main stream beside the side work -- so bench.py runs one engine per
+    GPU unless asked (--groups).  Engine g owns streams
+    [first[g], first[g] + sizes[g])."""
+
+    def __init__(self, model, n_streams, n_channels=2, groups=2, vadm=False, **kw):
+        if not 1 <= groups <= n_streams:
+            raise ValueError("groups must be in [1, n_streams]")
+        q, r = divmod(n_streams, groups)
+        self.sizes = [q + (1 if g < r else 0) for g in range(groups)]
+        self.first = [sum(self.sizes[:g]) for g in range(groups)]
+        self.B, self.C = n_streams, n_channels
+        self.engines = []
+        for g, n in enumerate(self.sizes):
+            # engine g's streams exist before engine g + 1's: the runtime hands
+            # out hardware queues in creation order
+            e = Engine(model, n, n_channels, **kw)
+            if vadm:
+                e.attach_vadm()
+            if g and kw.get("mode", "staged") != "fused":  # the fused engine has no side streams
+                e.share_streams(self.engines[0], SHARE_PREP | (SHARE_SIDE if vadm else 0))
+            self.engines.append(e)
+
+    def set_debug(self, key, value):
+        for e in self.engines:
+            e.set_debug(key, value)
+
+    def load_synthetic(self, n_ticks, base=0, pushes=1):
+        for e, f in zip(self.engines, self.first):
+            e.load_synthetic(n_ticks, base=base + f, pushes=pushes)
+
+    def run_resident(self, n_ticks):
+        for e in self.engines:
+            e.run_resident(n_ticks)
+
+    def sync(self):
+        for e in self.engines:
+            e.sync()
+
+    def clear_times(self):
+        for e in self.engines:
+            e.clear_times()
+
+    def kernel_times(self):
+        """Per kernel the mean over the engines of their launch averages (each
+        launch covers one engine's streams, co-running with the others')."""
+        ts = [e.kernel_times() for e in self.engines]
+        names = ts[0]["kernels"].keys()
+        return {"total_ms": sum(t["total_ms"] for t in ts) / len(ts),
+                "kernels": {n: sum(t["kernels"].get(n, 0.0) for t in ts) / len(ts) for n in names},
+                "runs": min(t["runs"] for t in ts)}
+
+    def segments(self, stream, machine=0):
+        g = max(i for i, f in enumerate(self.first) if f <= stream)
+        return self.engines[g].segments(stream - self.first[g], machine)
 
 class Denoiser:
     """src/Denoiser.zig over the rnnoise_* C ABI (GPU, batch of one)."""

@@ -308,6 +308,19 @@ int fvad_engine_vadm_snapshot(fvad_engine *e, int stream, int machine, fvad_vadm
  * error code) */
 long fvad_engine_vadm_rolling(fvad_engine *e, int stream, int machine, int which, double *out, size_t cap);
 
+/* Several engines on one GPU (e.g. a GPU's streams split into sub-partitions
+ * that push concurrently): e runs its k_prep3 (FVAD_SHARE_PREP) and / or its
+ * device VADMachine kernels (FVAD_SHARE_SIDE, both engines with machines
+ * attached) on other's streams from now on, so the engines' side work queues
+ * in order instead of taking a hardware queue each (a process gets
+ * GPU_MAX_HW_QUEUES of them, 4 by default, shared round-robin once they run
+ * out: a main stream sharing one with another engine's k_prep3 waits for it).
+ * Synchronises both engines; results are unchanged (dependencies are events).
+ * The last engine using a stream destroys it. */
+#define FVAD_SHARE_PREP 1
+#define FVAD_SHARE_SIDE 2
+int fvad_engine_share_streams(fvad_engine *e, fvad_engine *other, int which);
+
 /* Test hooks: knobs and a recorder the parity tests use; no product path sets
  * them.  fvad_engine_set_debug keys:
  *   FVAD_DEBUG_VADM_PAR_SERIAL_EVERY  value k > 0: k_vadm_par hands every

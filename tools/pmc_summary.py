@@ -68,8 +68,10 @@ def main():
     write_stats(os.path.join(out, "trace"), os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % tag))
     fetch = counters(os.path.join(out, "fetch"), "FETCH_SIZE")
     write = counters(os.path.join(out, "write"), "WRITE_SIZE")
-    cfg = {"streams": 2048, "ticks": 50, "channels": 2, "mode": "staged"}
-    keys = {"--streams-per-gpu": "streams", "--ticks": "ticks", "--channels": "channels", "--mode": "mode"}
+    # bench.py's defaults; groups = engines per GPU (a launch covers streams / groups)
+    cfg = {"streams": 2048, "ticks": 50, "channels": 2, "mode": "staged", "groups": 1}
+    keys = {"--streams-per-gpu": "streams", "--ticks": "ticks", "--channels": "channels", "--mode": "mode",
+            "--groups": "groups"}
     for i, a in enumerate(args):
         if a in keys and i + 1 < len(args):
             v = args[i + 1]

@@ -11,7 +11,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-BENCH=(bench.py --cpu-baseline 0 --host-rate 0 --variants 0 "$@")
+BENCH=(bench.py --cpu-baseline 0 --host-rate 0 --variants 0 --one-engine-leg 0 "$@")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" --steps 20 --warmup 10 \
   > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run -- python3 "${BENCH[@]}" --steps 2 --warmup 1 \
