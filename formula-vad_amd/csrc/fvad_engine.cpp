@@ -88,6 +88,12 @@ struct fvad_engine {
   float *d_xs_b[2] = {}, *d_ratio_b[2] = {}, *d_xlp_b[2] = {};
   int *d_ticks_b[2] = {};
   hipEvent_t ev_prep_done[2] = {}, ev_buf_free[2] = {};
+  // the last push's k_fftAw done: push k's k_prep3 starts once push k-1's
+  // k_fftAw has finished, so it runs beside k_plpc / k_pcorr instead (measured:
+  // k_fftAw 0.64 -> 0.57, k_plpc 0.48 -> 0.40, k_pcorr 1.18 -> 1.24 ms, push
+  // 5.00 -> 4.90 ms; started after k_plpc it overruns into k_rnn3: 5.93 ms)
+  hipEvent_t ev_fft_a = nullptr;
+  bool fft_a_rec = false;
   bool buf_busy[2] = {false, false};
   int next_buf = 0;
   int n_events = 0;           // timing events per launch
@@ -362,6 +368,7 @@ void free_all(fvad_engine *e) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : e->ev_buf_free)
     if (ev) (void)hipEventDestroy(ev);
+  if (e->ev_fft_a) (void)hipEventDestroy(e->ev_fft_a);
   if (e->stream) (void)hipStreamDestroy(e->stream);
 }
 
@@ -482,7 +489,8 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
        hipEventCreateWithFlags(&e->ev_prep_done[0], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_prep_done[1], hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&e->ev_buf_free[0], hipEventDisableTiming) != hipSuccess ||
-       hipEventCreateWithFlags(&e->ev_buf_free[1], hipEventDisableTiming) != hipSuccess))
+       hipEventCreateWithFlags(&e->ev_buf_free[1], hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_fft_a, hipEventDisableTiming) != hipSuccess))
     return bail(fail(FVAD_EDEVICE, "hipStreamCreate failed"));
   if (e->pstream) e->pstream_ref.reset(e->pstream, destroy_stream);
   for (int i = 0; i < e->n_events; i++)
@@ -723,6 +731,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   // (on pstream) until push k-2 released b, then runs beside push k-1
   const int b = e->next_buf;
   if (e->buf_busy[b]) HIP_TRY(wait_event(e->pstream, e->ev_buf_free[b]));
+  if (e->fft_a_rec) HIP_TRY(wait_event(e->pstream, e->ev_fft_a));
   e->d_xs = e->d_xs_b[b];
   e->d_ratio = e->d_ratio_b[b];
   e->d_ticks = e->d_ticks_b[b];
@@ -801,7 +810,8 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     HIP_TRY(wait_event(e->stream, e->ev_prep_done[b]));
     // window output set b is free once push k-2's k_vadm_hbm has read it
     if (e->vadm.n > 0) HIP_TRY(wait_event(e->stream, e->ev_vadm_b[b]));
-    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr));
+    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr, e->ev_fft_a));
+    e->fft_a_rec = true;
   } else {
     // no denoiser: raw input frames to the ring, windows, FFT B, all on the
     // engine stream after the input copy (queued on the prep stream)

@@ -133,7 +133,10 @@ constexpr int kStagedTime[kStagedKernels][2] = {{0, 1}, {2, 3},   {14, 4},  {4, 
 hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev);
 // Launch the other 10 kernels; when ev != nullptr their timing events are
 // recorded.
-hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev);
+// fft_a_done (optional): recorded on `stream` right after k_fftAw (the next
+// push's k_prep3 waits for it)
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev,
+                         hipEvent_t fft_a_done = nullptr);
 // k_pcorr over `tiles` pitch tiles (fvad_pitch.hip)
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream);
 const char *staged_kernel_name(int i);

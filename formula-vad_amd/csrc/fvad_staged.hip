@@ -2335,7 +2335,7 @@ hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) 
   return hipSuccess;
 }
 
-hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev) {
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev, hipEvent_t fft_a_done) {
   static const int p_plpc = blocks_per_cu(k_plpc, 256);
   const int g_plpc = p_plpc * n_cu;
   const long long frames = (long long)a.n_streams * a.V;
@@ -2352,6 +2352,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   // so they run in order on one stream
   REC(2);
   FVAD_LAUNCH_TRY(launch_wave(kWaveFftA, a, n_cu, stream));
+  if (fft_a_done) FVAD_LAUNCH_TRY(hipEventRecord(fft_a_done, stream));
   REC(3);
   {
     const long long tiles = (long long)((a.n_streams + 63) / 64) * a.n_ticks * a.n_channels;
