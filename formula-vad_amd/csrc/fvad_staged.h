@@ -133,10 +133,15 @@ constexpr int kStagedTime[kStagedKernels][2] = {{0, 1}, {2, 3},   {14, 4},  {4, 
 hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev);
 // Launch the other 10 kernels; when ev != nullptr their timing events are
 // recorded.
-// fft_a_done (optional): recorded on `stream` right after k_fftAw (the next
-// push's k_prep3 waits for it)
+// fft_a_done (optional): recorded right after k_fftAw (the next push's
+// k_prep3 waits for it).  fa_stream (optional, with fft_a_done): k_fftAw runs
+// there instead, after fa_after (the previous push's synth_done: the last
+// reader of X / Ex / Lyf / silence), so it overlaps the previous push's tail
+// on `stream`; `stream` waits for it before k_plpc.  synth_done (optional):
+// recorded on `stream` after k_synthw.
 hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev,
-                         hipEvent_t fft_a_done = nullptr);
+                         hipEvent_t fft_a_done = nullptr, hipStream_t fa_stream = nullptr,
+                         hipEvent_t fa_after = nullptr, hipEvent_t synth_done = nullptr);
 // k_pcorr over `tiles` pitch tiles (fvad_pitch.hip)
 hipError_t launch_pcorr(const StagedArgs &a, long long tiles, int n_cu, hipStream_t stream);
 const char *staged_kernel_name(int i);

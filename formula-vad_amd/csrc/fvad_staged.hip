@@ -2335,7 +2335,8 @@ hipError_t launch_prep(const StagedArgs &a, hipStream_t stream, hipEvent_t *ev) 
   return hipSuccess;
 }
 
-hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev, hipEvent_t fft_a_done) {
+hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipEvent_t *ev, hipEvent_t fft_a_done,
+                         hipStream_t fa_stream, hipEvent_t fa_after, hipEvent_t synth_done) {
   static const int p_plpc = blocks_per_cu(k_plpc, 256);
   const int g_plpc = p_plpc * n_cu;
   const long long frames = (long long)a.n_streams * a.V;
@@ -2346,14 +2347,25 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   static_assert(kWorkSlots * kQueues <= kWorkCounters, "work counters");
 #define REC(k) \
   if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[k], stream))
-  // k_fftAw and the pitch branch (k_plpc -> k_pcorr -> k_select) both only
-  // read xs; run side by side on two streams they stretch each other (both
-  // are persistent grids sized to the GPU: 15.0 vs 14.1 ms per push in r1),
-  // so they run in order on one stream
-  REC(2);
-  FVAD_LAUNCH_TRY(launch_wave(kWaveFftA, a, n_cu, stream));
-  if (fft_a_done) FVAD_LAUNCH_TRY(hipEventRecord(fft_a_done, stream));
-  REC(3);
+  // k_fftAw and the pitch branch (k_plpc -> k_pcorr -> k_select) run in
+  // order (side by side on two streams they stretch each other: 15.0 vs 14.1
+  // ms per push in r1); k_fftAw itself may run on fa_stream beside the
+  // previous push's k_olafb (fvad_staged.h)
+  if (fa_stream && fft_a_done) {
+    // k_fftAw on fa_stream beside the previous push's k_olafb: it writes
+    // nothing that kernel reads, only what the previous push's k_synthw read
+    if (fa_after) FVAD_LAUNCH_TRY(hipStreamWaitEvent(fa_stream, fa_after, 0));
+    if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[2], fa_stream));
+    FVAD_LAUNCH_TRY(launch_wave(kWaveFftA, a, n_cu, fa_stream));
+    if (ev) FVAD_LAUNCH_TRY(hipEventRecord(ev[3], fa_stream));
+    FVAD_LAUNCH_TRY(hipEventRecord(fft_a_done, fa_stream));
+    FVAD_LAUNCH_TRY(hipStreamWaitEvent(stream, fft_a_done, 0));
+  } else {
+    REC(2);
+    FVAD_LAUNCH_TRY(launch_wave(kWaveFftA, a, n_cu, stream));
+    if (fft_a_done) FVAD_LAUNCH_TRY(hipEventRecord(fft_a_done, stream));
+    REC(3);
+  }
   {
     const long long tiles = (long long)((a.n_streams + 63) / 64) * a.n_ticks * a.n_channels;
     REC(14);
@@ -2377,6 +2389,7 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
     FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
   REC(9);
   FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
+  if (synth_done) FVAD_LAUNCH_TRY(hipEventRecord(synth_done, stream));
   REC(10);
   if (olafb_fused(a)) {
     // overlap-add, window bookkeeping and FFT B in one kernel (k_olafb);
