@@ -9,7 +9,9 @@ serial k_vadm_hbm walk; a 10 s long-term buffer (234 windows) wraps around
 several times within the streams (the wrap branch of k_vadm_par), with a
 sync point after every push so each push's machines take k_vadm_par (between
 pushes the engine runs k_vadm_hbm; a sync point flushes the last push as
-k_vadm_par)."""
+k_vadm_par) -- and once more without the syncs, so k_vadm_hbm's lazy folds
+run over a buffer of pushed values that wraps (the production regime of a
+stream past its first long_term_speech_avg_sec)."""
 import numpy as np
 import pytest
 
@@ -31,8 +33,9 @@ def host_segments(fvad_mod, outs, cfg, C, slot, stream):
     return vm.segments()
 
 
-@pytest.mark.parametrize("alt_init,alt_lt_sec", [(True, 180.0), (False, 180.0), (True, 10.0)])
-def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec):
+@pytest.mark.parametrize("alt_init,alt_lt_sec,sync_each",
+                         [(True, 180.0, False), (False, 180.0, False), (True, 10.0, True), (True, 10.0, False)])
+def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each):
     m = fvad_mod.Model(seed=1)
     alt = fvad_mod.VadmConfig.default()
     alt.speech_min_freq, alt.speech_max_freq = 300.0, 3000.0
@@ -57,7 +60,7 @@ def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec):
             if v:
                 pcm[:v, s] = x[:, t0 * 480:(t0 + v) * 480].reshape(C, v, 480).transpose(1, 0, 2)
         outs.append((eng.push(pcm, ticks_valid=valid), valid))
-        if alt_lt_sec < 60:
+        if sync_each:
             eng.sync()  # a sync point per push: every push's machines run as k_vadm_par
     total = 0
     for s in range(B):
