@@ -697,7 +697,11 @@ int enqueue_vadm(fvad_engine *e, const fvad::StagedArgs &v, int b, bool timed, b
     HIP_TRY(hipEventRecord(e->ev_vt[slot][0], e->side));
   }
   bool par = false;
-  HIP_TRY(fvad::launch_vadm(v, e->side, fast || e->dbg_always_par, &par));
+  // a sync point's flush (or the test hook's every push) leaves every machine
+  // exact; between sync points k_vadm_hbm may owe its long-term fold
+  fvad::StagedArgs vf = v;
+  vf.vadm.vfinal = (fast || e->dbg_always_par) ? 1 : 0;
+  HIP_TRY(fvad::launch_vadm(vf, e->side, fast || e->dbg_always_par, &par));
   if (timed) {
     HIP_TRY(hipEventRecord(e->ev_vt[slot][1], e->side));
     e->vadm_pending[slot] = true;

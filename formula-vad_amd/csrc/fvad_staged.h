@@ -42,10 +42,15 @@ struct VadmConst {
 struct VadmState {
   unsigned long long speech_start, speech_end, windows_done;
   double lt_last, st_last, r_last, lt_pre;  // lt_pre: cached prefix (see ra_push_long)
-  unsigned lt_widx, lt_count, st_widx, st_count, r_widx, r_count, lt_nw, pad1;  // lt_nw: entries pushed
+  // lt_nw: entries pushed; lt_defer: long pushes since lt_last was last folded
+  // exactly (k_vadm_hbm's deferred fold: lt_last is then stale, and lt_approx /
+  // lt_amax / lt_fpre carry the walk's estimate, its bound's magnitude and the
+  // exact fold through the last pushed index; every sync point resolves it)
+  unsigned lt_widx, lt_count, st_widx, st_count, r_widx, r_count, lt_nw, lt_defer;
   int lt_has, st_has, r_has, state, lt_pre_ok, pad0;
   float rnn_vad, vol_ratio;
   unsigned rnn_vad_count, vol_ratio_count, n_segs, pad;
+  double lt_approx, lt_amax, lt_fpre;
 };
 struct VadmSeg {
   unsigned long long sample_from, sample_to;
@@ -58,6 +63,7 @@ struct VadmArgs {
   float *buf;     // rolling-average data (f32: each entry is a pushed f32)
   VadmSeg *seg;   // [m][stream][seg_cap]
   int seg_cap;
+  int vfinal;  // this launch is a sync point's: every machine's long-term average folded exactly at the end
   int par_serial_every;  // test hook (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY): k_vadm_par hands stream s to its
                          //   in-kernel serial walk when s % par_serial_every == 0; 0 = never
 };

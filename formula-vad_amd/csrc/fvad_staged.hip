@@ -1816,6 +1816,33 @@ __device__ __forceinline__ void vadm_fsm(VadmState &S, const VadmConst &K, unsig
   }
 }
 
+// Deferred folds.  Between sync points (k_vadm_hbm, final = false) the exact
+// fold a push would end with is owed instead of done: the estimate, its
+// bound's magnitude and the exact prefix ride in the state (lt_defer long
+// pushes since the last exact fold) and the next push's walk continues from
+// them, so a machine folds only for a test the bound does not settle, after
+// kLtDeferMax long pushes, or at a sync point (final: k_vadm_par's drain, or
+// k_vadm_hbm when the push cannot take k_vadm_par), where every machine is
+// resolved -- states and segments read after a sync are the reference's.
+// (One fold per stream and push was ~4 000 f64 adds in the full-buffer
+// regime: k_vadm_hbm 0.44-0.65 ms beside the next push, which stretched the
+// co-running k_prep3 and, through it, k_pspecw.)
+#ifndef FVAD_LT_DEFER_MAX
+#define FVAD_LT_DEFER_MAX 4096
+#endif
+constexpr unsigned kLtDeferMax = FVAD_LT_DEFER_MAX;
+// the fold a deferred machine owes: vadm_stream's fold, the same adds in the
+// same order (the exact prefix through the last pushed index, then the
+// entries after it)
+__device__ __forceinline__ void lt_resolve(VadmState &S, const VadmConst &K, const float *lt, size_t lts) {
+  if (!S.lt_defer) return;
+  const unsigned n = (unsigned)K.n_lt;
+  double acc = S.lt_fpre;
+  if (S.lt_widx != 0) acc = lt_range(acc, lt, lts, S.lt_widx, n, S.lt_nw, K.init, 1.0 / (double)n);
+  S.lt_last = acc;
+  S.lt_defer = 0;
+}
+
 // One machine over all completed windows of the push for one stream; `lt`
 // points at entry 0 of the stream's long-term buffer, `lts` is its stride.
 //
@@ -1838,7 +1865,7 @@ __device__ __forceinline__ void vadm_fsm(VadmState &S, const VadmConst &K, unsig
 // Used when the buffer is full, the terms are nonnegative (band energies,
 // a nonnegative initial average) and the threshold factor is nonnegative;
 // otherwise each pushing window folds at once (ra_push_long).
-__device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t lts) {
+__device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t lts, bool final) {
   const int B = a.n_streams, C = a.n_channels, nb = a.n_bands;
   const int nt = ticks_of(a, s);
   const unsigned long long fft = (unsigned long long)a.plan->nfft_b;
@@ -1849,8 +1876,15 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
   const unsigned n = (unsigned)K.n_lt;
   const double f = (double)K.thr_factor, scalar = 1.0 / (double)n;
   const bool lazy = S.lt_count == n && S.lt_pre_ok && S.lt_has && n > 1 && f >= 0.0 && !(K.has_init && !(K.init >= 0.0));
+  if (!lazy) lt_resolve(S, K, lt, lts);  // (a deferring machine is lazy; kept for safety)
   double approx = S.lt_last, amax = fabs(S.lt_last), fpre = 0.0;
   int pending = 0;  // pushes since lt_last was last folded exactly
+  if (S.lt_defer) {  // owed from earlier pushes (deferred folds)
+    approx = S.lt_approx;
+    amax = S.lt_amax;
+    fpre = S.lt_fpre;
+    pending = (int)S.lt_defer;
+  }
   // the exact average of the current buffer: the fold through the last pushed
   // index (fpre) continued over the entries after it, C order
   auto fold = [&]() {
@@ -1921,7 +1955,11 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
       }
       vadm_fsm(S, K, index, met, vad, vr, seg, a.vadm.seg_cap);
     }
-  if (pending) fold();
+  if (pending && (final || (unsigned)pending >= kLtDeferMax)) fold();
+  S.lt_defer = (unsigned)pending;
+  S.lt_approx = approx;
+  S.lt_amax = amax;
+  S.lt_fpre = fpre;
   a.vadm.st[(size_t)m * B + s] = S;
 }
 
@@ -2004,7 +2042,21 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
       }
       Kw += tot;
     }
-    if (r == 0) Ss[g] = a.vadm.st[(size_t)m * B + (sok ? s : 0)];
+    if (r == 0) {
+      Ss[g] = a.vadm.st[(size_t)m * B + (sok ? s : 0)];
+      // k_vadm_par runs at sync points only: a fold owed from earlier pushes
+      // first (the walk below needs the exact average), also for a stream
+      // with no ticks in this push
+      if (sok) {
+        lt_resolve(Ss[g], K, lt, lts);
+      } else if (s < B) {
+        VadmState S2 = a.vadm.st[(size_t)m * B + s];
+        if (S2.lt_defer) {
+          lt_resolve(S2, K, a.vadm.buf + K.lt_off + (size_t)s * K.lt_pitch, 1);
+          a.vadm.st[(size_t)m * B + s] = S2;
+        }
+      }
+    }
     wave_sync();
     VadmState &S = Ss[g];
     float *st = a.vadm.buf + K.st_off + (sok ? s : 0), *rb = a.vadm.buf + K.r_off + (sok ? s : 0);
@@ -2108,7 +2160,7 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
         // engines whose machines can get here to k_vadm_hbm; the test hook
         // par_serial_every forces it): the serial walk on the leader lane,
         // from the untouched state in HBM
-        vadm_stream(a, m, s, lt, lts);
+        vadm_stream(a, m, s, lt, lts, true);
       } else {
         // the push's long-term values into the buffer (read above as the old entries)
         unsigned w = wbase;
@@ -2419,9 +2471,22 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
 constexpr int kVadmHbmLanes = FVAD_VADM_LANES;  // streams per workgroup (one wave); 16 / 32 / 64 measured within noise, 64 takes fewest wave slots
 __global__ void __launch_bounds__(64) k_vadm_hbm(StagedArgs a) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= a.n_streams || ticks_of(a, s) <= 0) return;
+  if (s >= a.n_streams) return;
+  const bool final = a.vadm.vfinal != 0;
+  if (ticks_of(a, s) <= 0) {  // no windows; at a sync point its owed fold is still due
+    if (final)
+      for (int m = 0; m < a.vadm.n; m++) {
+        VadmState *p = a.vadm.st + (size_t)m * a.n_streams + s;
+        if (p->lt_defer) {
+          VadmState S = *p;
+          lt_resolve(S, a.vadm.c[m], a.vadm.buf + a.vadm.c[m].lt_off + (size_t)s * a.vadm.c[m].lt_pitch, 1);
+          *p = S;
+        }
+      }
+    return;
+  }
   for (int m = 0; m < a.vadm.n; m++)
-    vadm_stream(a, m, s, a.vadm.buf + a.vadm.c[m].lt_off + (size_t)s * a.vadm.c[m].lt_pitch, 1);
+    vadm_stream(a, m, s, a.vadm.buf + a.vadm.c[m].lt_off + (size_t)s * a.vadm.c[m].lt_pitch, 1, final);
 }
 
 hipError_t launch_nodenoise(const StagedArgs &a, int n_cu, hipStream_t stream) {
