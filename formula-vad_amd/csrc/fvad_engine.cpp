@@ -1688,6 +1688,10 @@ extern "C" int fvad_engine_set_debug(fvad_engine *e, int key, int value) {
     case FVAD_DEBUG_VADM_ALWAYS_PAR:
       e->dbg_always_par = value != 0;
       return FVAD_OK;
+    case FVAD_DEBUG_VADM_DEFER_MAX:
+      if (value < 0) return fail(FVAD_EINVAL, "value >= 0 required");
+      e->vadm.defer_max = (unsigned)value;
+      return FVAD_OK;
     case FVAD_DEBUG_VADM_LT_FULL:
       if (e->vadm.n == 0) return fail(FVAD_EINVAL, "no VADMachines attached");
       e->dbg_lt_full = value != 0;

@@ -63,6 +63,7 @@ struct VadmArgs {
   float *buf;     // rolling-average data (f32: each entry is a pushed f32)
   VadmSeg *seg;   // [m][stream][seg_cap]
   int seg_cap;
+  unsigned defer_max;  // test hook (FVAD_DEBUG_VADM_DEFER_MAX): fold once this many long pushes are owed; 0 = kLtDeferMax
   int vfinal;  // this launch is a sync point's: every machine's long-term average folded exactly at the end
   int par_serial_every;  // test hook (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY): k_vadm_par hands stream s to its
                          //   in-kernel serial walk when s % par_serial_every == 0; 0 = never

@@ -1955,7 +1955,7 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
       }
       vadm_fsm(S, K, index, met, vad, vr, seg, a.vadm.seg_cap);
     }
-  if (pending && (final || (unsigned)pending >= kLtDeferMax)) fold();
+  if (pending && (final || (unsigned)pending >= (a.vadm.defer_max ? a.vadm.defer_max : kLtDeferMax))) fold();
   S.lt_defer = (unsigned)pending;
   S.lt_approx = approx;
   S.lt_amax = amax;

@@ -95,7 +95,7 @@ class VadmSnapshot(C.Structure):
                 for n, _ in self._fields_}
 
 
-DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR, DEBUG_VADM_LT_FULL = 1, 2, 3
+DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR, DEBUG_VADM_LT_FULL, DEBUG_VADM_DEFER_MAX = 1, 2, 3, 4
 SHARE_PREP, SHARE_SIDE = 1, 2  # fvad_engine_share_streams
 
 READ_FN = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.c_int, C.POINTER(F32P), C.c_size_t)
@@ -473,7 +473,8 @@ class Engine:
         _check(lib().fvad_engine_share_streams(self.h, other.h, which), "fvad_engine_share_streams")
 
     def set_debug(self, key, value):
-        """Test hooks (fvad_engine_set_debug): DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR."""
+        """Test hooks (fvad_engine_set_debug): DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR,
+        DEBUG_VADM_LT_FULL, DEBUG_VADM_DEFER_MAX."""
         _check(lib().fvad_engine_set_debug(self.h, key, value), "fvad_engine_set_debug")
 
     def output_log(self, n_pushes):

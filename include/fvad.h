@@ -331,10 +331,15 @@ int fvad_engine_share_streams(fvad_engine *e, fvad_engine *other, int which);
  *   FVAD_DEBUG_VADM_LT_FULL  value 1: the machines restart (as by a reset)
  *     with every long-term entry counted as pushed, holding (float)init: the
  *     long-term walk of a stream past its first long_term_speech_avg_sec, for
- *     timing (tools/vadm_steady.py); the values then differ from the reference */
+ *     timing (tools/vadm_steady.py); the values then differ from the reference
+ *   FVAD_DEBUG_VADM_DEFER_MAX  value k > 0: between sync points k_vadm_hbm
+ *     folds a machine's long-term average once k long pushes are owed (1: at
+ *     the end of every push); 0: the default bound (4096).  Results are the
+ *     same for every k: a sync point resolves every owed fold */
 #define FVAD_DEBUG_VADM_PAR_SERIAL_EVERY 1
 #define FVAD_DEBUG_VADM_ALWAYS_PAR 2
 #define FVAD_DEBUG_VADM_LT_FULL 3
+#define FVAD_DEBUG_VADM_DEFER_MAX 4
 int fvad_engine_set_debug(fvad_engine *e, int key, int value);
 /* Output log: the per-tick outputs (fvad_outputs without denoised) of the next
  * n_pushes pushes are copied into device memory on the engine stream as each

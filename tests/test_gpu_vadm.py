@@ -33,9 +33,10 @@ def host_segments(fvad_mod, outs, cfg, C, slot, stream):
     return vm.segments()
 
 
-@pytest.mark.parametrize("alt_init,alt_lt_sec,sync_each",
-                         [(True, 180.0, False), (False, 180.0, False), (True, 10.0, True), (True, 10.0, False)])
-def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each):
+@pytest.mark.parametrize("alt_init,alt_lt_sec,sync_each,defer_max",
+                         [(True, 180.0, False, 0), (False, 180.0, False, 0), (True, 10.0, True, 0),
+                          (True, 10.0, False, 0), (True, 10.0, False, 1), (True, 10.0, False, 7)])
+def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each, defer_max):
     m = fvad_mod.Model(seed=1)
     alt = fvad_mod.VadmConfig.default()
     alt.speech_min_freq, alt.speech_max_freq = 300.0, 3000.0
@@ -47,6 +48,8 @@ def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each):
     streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip(ids, secs)]
     eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=64, bands=((4, 64), (13, 128)))
     eng.attach_vadm([fvad_mod.VadmConfig.default(), alt])
+    if defer_max:  # the long-term fold owed across at most defer_max long pushes (1: every push)
+        eng.set_debug(fvad_mod.DEBUG_VADM_DEFER_MAX, defer_max)
     B, C = len(streams), 2
     lens = [x.shape[1] // 480 for x in streams]
     outs = []
@@ -72,7 +75,7 @@ def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each):
     assert total > 0
 
 
-@pytest.mark.parametrize("flavour", ["default", "always_par", "par_serial_fallback"])
+@pytest.mark.parametrize("flavour", ["default", "always_par", "par_serial_fallback", "defer_max_5"])
 def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
     """The whole device machine state (fvad_engine_vadm_snapshot: speech state
     and indices, RollingAverage last averages / write indices / counts, the
@@ -81,17 +84,21 @@ def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
     between pushes, k_vadm_par for the last one; always_par: every push's
     machine on k_vadm_par (FVAD_DEBUG_VADM_ALWAYS_PAR); par_serial_fallback:
     the same with every second stream forced through k_vadm_par's in-kernel
-    serial walk (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY = 2)."""
+    serial walk (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY = 2); defer_max_5: k_vadm_hbm
+    folds once 5 long pushes are owed (FVAD_DEBUG_VADM_DEFER_MAX), so owed folds
+    are resolved in the middle of pushes as well as by the sync point."""
     m = fvad_mod.Model(seed=1)
     om = oracle_mod.Model(seed=1)
     ids = [0, 3, 19, 39, 7, 12, 59, 8]
     streams, _ = pu.make_streams(fvad_mod, ids, 14.0)
     eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=50)
     eng.attach_vadm()
-    if flavour != "default":
+    if flavour in ("always_par", "par_serial_fallback"):
         eng.set_debug(fvad_mod.DEBUG_VADM_ALWAYS_PAR, 1)
     if flavour == "par_serial_fallback":
         eng.set_debug(fvad_mod.DEBUG_VADM_PAR_SERIAL_EVERY, 2)
+    if flavour == "defer_max_5":
+        eng.set_debug(fvad_mod.DEBUG_VADM_DEFER_MAX, 5)
     pu.engine_run(fvad_mod, eng, streams, 50, denoised=False)
     for s, x in enumerate(streams):
         p = oracle_mod.Pipeline(2, om)
