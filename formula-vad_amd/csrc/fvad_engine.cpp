@@ -99,6 +99,7 @@ struct fvad_engine {
   // push k-1's k_olafb instead of after it (push 4.87 -> 4.78 ms)
   hipEvent_t ev_synth = nullptr;
   bool synth_rec = false;
+  hipEvent_t synth_wait = nullptr;  // the last push's k_synthw-end event: ev_synth, or ev[10] in a timed push
   bool buf_busy[2] = {false, false};
   int next_buf = 0;
   int n_events = 0;           // timing events per launch
@@ -822,7 +823,8 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     // window output set b is free once push k-2's k_vadm_hbm has read it
     if (e->vadm.n > 0) HIP_TRY(wait_event(e->stream, e->ev_vadm_b[b]));
     HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr, e->ev_fft_a, e->pstream,
-                                e->synth_rec ? e->ev_synth : nullptr, e->ev_synth));
+                                e->synth_rec ? e->synth_wait : nullptr, e->ev_synth));
+    e->synth_wait = timed ? e->ev[10] : e->ev_synth;  // (launch_staged records ev[10] in its place when timed)
     e->synth_rec = true;
     e->fft_a_rec = true;
   } else {

@@ -2441,8 +2441,18 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
     FVAD_KERNEL_TRY(k_rnn3, dim3((a.n_streams + kR3S - 1) / kR3S), dim3(kR3NT), 0, stream, a);
   REC(9);
   FVAD_LAUNCH_TRY(launch_wave(kWaveSynth, a, n_cu, stream));
-  if (synth_done) FVAD_LAUNCH_TRY(hipEventRecord(synth_done, stream));
-  REC(10);
+  if (ev && synth_done) {
+    // a timed push: its timing event ev[10] (k_synthw's end, the tail's start)
+    // is also the one the next push's k_fftAw waits for, so every push has
+    // one event record between k_synthw and the tail.  (With a second one in
+    // the timed pushes the tail's dispatch fell behind the next k_fftAw's,
+    // whose persistent grid then took the CUs first: k_plpc ~130 us late in
+    // every timed push.)
+    FVAD_LAUNCH_TRY(hipEventRecord(ev[10], stream));
+  } else {
+    if (synth_done) FVAD_LAUNCH_TRY(hipEventRecord(synth_done, stream));
+    REC(10);
+  }
   if (olafb_fused(a)) {
     // overlap-add, window bookkeeping and FFT B in one kernel (k_olafb);
     // the k_winmeta / k_fftbw events bracket nothing
