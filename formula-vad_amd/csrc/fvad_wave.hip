@@ -856,8 +856,14 @@ int wave_per_cu(K kernel, int nw = kWNW) {
 hipError_t launch_wave(WaveKernel which, const StagedArgs &a, int n_cu, hipStream_t stream) {
   static const int p_fftA = wave_per_cu(k_fftAw), p_pspec = wave_per_cu(k_pspecw, kPNW), p_synth = wave_per_cu(k_synthw, kSNW),
                    p_fftb = wave_per_cu(k_fftbw), p_olafb = wave_per_cu(k_olafb);
+  // k_olafb: at most 2 of its 3 resident workgroups per CU.  Beside the next
+  // push's k_fftAw (which starts ~10 us after it) it then leaves that kernel
+  // a workgroup slot per CU from the start, and its 1 024 items (2 048 stereo
+  // streams) run as two even rounds instead of 1.33: k_olafb 0.44 -> 0.40 ms,
+  // k_fftAw 0.75 -> 0.72, push 4.759 -> 4.745 ms (three interleaved pairs;
+  // measured with the timed pushes' dispatch race gone, §8 r5)
   const int g_fftA = p_fftA * n_cu, g_pspec = p_pspec * n_cu, g_synth = p_synth * n_cu, g_fftb = p_fftb * n_cu,
-            g_olafb = p_olafb * n_cu;
+            g_olafb = std::min(p_olafb, 2) * n_cu;
   if (which == kWaveOlaFb) {
     const int G = kWNW / a.n_channels;
     hipLaunchKernelGGL(k_olafb, dim3((unsigned)std::min<long long>((a.n_streams + G - 1) / G, g_olafb)), dim3(64 * kWNW),
