@@ -75,7 +75,7 @@ def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each, def
     assert total > 0
 
 
-@pytest.mark.parametrize("flavour", ["default", "always_par", "par_serial_fallback", "defer_max_5"])
+@pytest.mark.parametrize("flavour", ["default", "always_par", "par_serial_fallback", "defer_max_5", "ragged"])
 def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
     """The whole device machine state (fvad_engine_vadm_snapshot: speech state
     and indices, RollingAverage last averages / write indices / counts, the
@@ -86,11 +86,17 @@ def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
     the same with every second stream forced through k_vadm_par's in-kernel
     serial walk (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY = 2); defer_max_5: k_vadm_hbm
     folds once 5 long pushes are owed (FVAD_DEBUG_VADM_DEFER_MAX), so owed folds
-    are resolved in the middle of pushes as well as by the sync point."""
+    are resolved in the middle of pushes as well as by the sync point; ragged:
+    three streams end early (3, 6 and 9.5 s of 14), so their machines owe a
+    fold from their last pushes and have no ticks when the sync point's
+    k_vadm_par resolves it."""
     m = fvad_mod.Model(seed=1)
     om = oracle_mod.Model(seed=1)
     ids = [0, 3, 19, 39, 7, 12, 59, 8]
     streams, _ = pu.make_streams(fvad_mod, ids, 14.0)
+    if flavour == "ragged":
+        for s, sec in ((1, 6.0), (4, 9.5), (6, 3.0)):
+            streams[s] = np.ascontiguousarray(streams[s][:, :int(48000 * sec)])
     eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=50)
     eng.attach_vadm()
     if flavour in ("always_par", "par_serial_fallback"):
