@@ -20,7 +20,9 @@ Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
 each rank runs its own stream partition; `--gpus N` without WORLD_SIZE
 re-launches this script under torch.distributed.run with N ranks as a child
 process, before anything touches the GPU.  The only collectives are the
-barrier and the max-reduce of the timing (no data-path collective).
+barrier and the max-reduce of the timing (no data-path collective), on a
+gloo process group with CPU tensors: no RCCL communicator or torch HIP stream
+takes a hardware queue from the engine.
 
 Also reported (never `value`): host_buffers, the streaming rate with the
 input coming from host memory each push (fvad_engine_submit: pinned slots,
@@ -75,9 +77,9 @@ def parse():
     ap.add_argument("--cpu-stub", action="store_true",
                     help="no GPU: gloo ranks with a stub engine (tests the launcher, barrier and max-reduce)")
     ap.add_argument("--rehearse-on-gpu0", action="store_true",
-                    help="multi-rank rehearsal on a 1-GPU box: every rank's engine on device 0, gloo collectives "
-                         "(exercises the N > 1 path end to end; the ranks share one GPU, so the rate is no "
-                         "scaling figure and the line says so)")
+                    help="multi-rank rehearsal on a 1-GPU box: every rank's engine on device 0, otherwise the "
+                         "code the driver runs at N > 1 (gloo collectives on the CPU); the ranks share one GPU, so "
+                         "the rate is no scaling figure and the line says so")
     ap.add_argument("--groups", type=int, default=1,
                     help="engines per GPU (fvad.EngineGroup): the rank's streams split into this many "
                          "sub-partitions pushing concurrently, k_prep3 / VADMachines on shared side streams "
@@ -112,44 +114,38 @@ def maybe_spawn(args):
     sys.exit(subprocess.call(cmd, env=env))
 
 
-def dist_setup(n_gpus, backend="nccl"):
-    """One process per GPU (torch.distributed.run env).  backend "gloo" is
-    used by the CPU tests of this logic (tests/test_dist_cpu.py).  Under
-    torch.distributed.run the world size is the launcher's; it must match
-    --gpus when that was given explicitly."""
+def dist_setup(n_gpus):
+    """One process per GPU (torch.distributed.run env).  The process group is
+    gloo at every N, its tensors on the CPU: the only collectives are the
+    timing barrier, the max-reduce and the kernel-table gather, so no RCCL
+    communicator and no torch HIP stream competes with the engine's streams
+    for the GPU's hardware queues (GPU_MAX_HW_QUEUES = 4).
+    Initialised whenever torch.distributed.run launched this process (world 1
+    included).  Under torch.distributed.run the world size is the launcher's;
+    it must match --gpus when that was given explicitly."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if n_gpus > 1 and world != n_gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (n_gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if "WORLD_SIZE" in os.environ:
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
         return rank, world, local, dist, torch
     return rank, world, local, None, None
-
-
-def _on_gpu(dist):
-    return dist.get_backend() == "nccl"
 
 
 def barrier(dist, torch):
     if dist is not None:
         dist.barrier()
-        if _on_gpu(dist):
-            torch.cuda.synchronize()
 
 
 def max_over_ranks(x, dist, torch):
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda" if _on_gpu(dist) else "cpu")
+    t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -262,7 +258,7 @@ class StubEngine:
 
 
 def stub_main(args):
-    rank, world, local, dist, torch = dist_setup(args.gpus, backend="gloo")
+    rank, world, local, dist, torch = dist_setup(args.gpus)
     B, Ch, T = args.streams_per_gpu, args.channels, args.ticks
     base, _ = stream_partition(rank, B)
     eng = StubEngine(B)
@@ -404,7 +400,7 @@ def main():
     maybe_spawn(args)
     if args.cpu_stub:
         return stub_main(args)
-    rank, world, local, dist, torch = dist_setup(args.gpus, backend="gloo" if args.rehearse_on_gpu0 else "nccl")
+    rank, world, local, dist, torch = dist_setup(args.gpus)
     if args.rehearse_on_gpu0:
         local = 0
     import fvad

@@ -18,6 +18,7 @@
 // identical results.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -119,6 +120,11 @@ struct fvad_engine {
   bool vpend = false, vpend_timed = false;
   int vpend_b = 0;
   fvad::StagedArgs vpend_args{};
+  // a non-final k_vadm_hbm was queued last (its machines may owe their
+  // long-term fold): a sync point with no push pending resolves it with a
+  // resolve-only pass (vowed_args: that launch's argument block)
+  bool vowed = false;
+  fvad::StagedArgs vowed_args{};
   float *d_vwratio = nullptr, *d_vwvad = nullptr, *d_vband = nullptr;
   // VADMachine timing, by kernel: [0] k_vadm_hbm (steady state), [1] k_vadm_par
   // (a push flushed at a sync point); vadm_kind[slot]: the kernel a pending
@@ -343,7 +349,7 @@ void free_all(fvad_engine *e) {
                   e->d_model, e->d_stamps, e->d_X,    e->d_P,     e->d_Ex,    e->d_Ep,
                   e->d_Exp,  e->d_Lyf,     e->d_f34,   e->d_rec,  e->d_ptile, e->d_work, e->d_vadf,  e->d_ys,    e->d_sil,
                   e->d_pitch, e->d_wtick,  e->d_wstart, e->d_gr, e->d_gs, e->d_rnn_img, e->d_gru16, e->d_gru16_bias, e->vadm.st, e->vadm.buf,
-                  e->vadm.seg, e->d_res, e->d_vflag, e->d_vticks, e->d_vticks_b[1], e->d_vwratio, e->d_vwvad, e->d_vband,
+                  e->vadm.seg, e->vadm.count, e->d_res, e->d_vflag, e->d_vticks, e->d_vticks_b[1], e->d_vwratio, e->d_vwvad, e->d_vband,
                   e->d_fbtab, e->d_fbwork, e->d_log};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -391,6 +397,7 @@ extern "C" int fvad_engine_reset(fvad_engine *e) {
   if (e->pstream) HIP_TRY(hipStreamSynchronize(e->pstream));
   if (e->vadm.n > 0) {
     e->vpend = false;  // the pending push's machine state is wiped below: not run
+    e->vowed = false;
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->side));
     const int rc = vadm_reset(e);
@@ -527,17 +534,6 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t frames = T * B * C * fvad::kFrame;
   const size_t TBW = T * B * e->wpt;  // window slots
-  {
-    // a streaming slot pins one push of input and outputs (fvad_engine_submit,
-    // up to FVAD_MAX_IN_FLIGHT of them); the window outputs grow with W =
-    // windows_per_tick (up to 240 at fft_size 2): refuse configurations whose
-    // slot would not be a sane pinned allocation
-    const double slot = 4.0 * ((double)frames * (c.want_denoised ? 2 : 1) + 3.0 * T * B + 2.0 * TBW +
-                               (double)TBW * C * c.n_bands);
-    if (slot > 16.0 * (1ull << 30))
-      return bail(fail(FVAD_ENOMEM, "a push of max_ticks x n_streams needs > 16 GiB of pinned slot memory "
-                                    "(outputs scale with windows_per_tick): lower max_ticks or n_streams"));
-  }
   if ((rc = dalloc(&e->d_state, B * fvad::st::kWords)) || (rc = dalloc(&e->d_ring, B * C * e->ring_len)) ||
       (rc = dalloc(&e->d_pcm_b[0], frames)) || (rc = dalloc(&e->d_pcm_b[1], frames)) ||
       (rc = dalloc(&e->d_ratio_b[0], T * B)) ||
@@ -614,7 +610,9 @@ extern "C" void fvad_engine_destroy(fvad_engine *e) {
 // e runs its k_prep3 (which & FVAD_SHARE_PREP) and / or its VADMachine
 // kernels (which & FVAD_SHARE_SIDE) on other's streams from now on.  Both
 // engines idle (synchronised here); every dependency stays an event, so
-// sharing only adds order between the engines' side work.
+// sharing only adds order between the engines' side work.  An engine whose
+// prep stream is shared runs k_fftAw on its own stream (launch_staged), so
+// the main pipelines stay independent.
 extern "C" int fvad_engine_share_streams(fvad_engine *e, fvad_engine *other, int which) {
   if (!e || !other || e == other || (which & ~(FVAD_SHARE_PREP | FVAD_SHARE_SIDE)) || !which)
     return fail(FVAD_EINVAL, "invalid argument");
@@ -702,7 +700,12 @@ int enqueue_vadm(fvad_engine *e, const fvad::StagedArgs &v, int b, bool timed, b
   // exact; between sync points k_vadm_hbm may owe its long-term fold
   fvad::StagedArgs vf = v;
   vf.vadm.vfinal = (fast || e->dbg_always_par) ? 1 : 0;
+  e->vowed = false;  // (a final pass resolves every machine, those without ticks included)
   HIP_TRY(fvad::launch_vadm(vf, e->side, fast || e->dbg_always_par, &par));
+  if (!vf.vadm.vfinal) {
+    e->vowed = true;
+    e->vowed_args = vf;
+  }
   if (timed) {
     HIP_TRY(hipEventRecord(e->ev_vt[slot][1], e->side));
     e->vadm_pending[slot] = true;
@@ -716,7 +719,22 @@ int enqueue_vadm(fvad_engine *e, const fvad::StagedArgs &v, int b, bool timed, b
 // the last push's VADMachine, enqueued now (after its push's kernels);
 // fast: nothing else is queued behind it (a sync point)
 int vadm_flush(fvad_engine *e, bool fast = true) {
-  if (!e->vpend) return FVAD_OK;
+  if (!e->vpend) {
+    if (fast && e->vowed) {
+      // folds owed with no push pending (a push whose launch failed after
+      // the previous push's non-final pass was queued): k_vadm_hbm with no
+      // ticks and vfinal = 1 only resolves them
+      fvad::StagedArgs r = e->vowed_args;
+      r.n_ticks = 0;
+      r.ticks_valid = nullptr;
+      r.vadm = e->vadm;
+      r.vadm.vfinal = 1;
+      e->vowed = false;
+      HIP_TRY(fvad::launch_vadm(r, e->side, false, nullptr));
+      HIP_TRY(hipEventRecord(e->ev_vadm, e->side));
+    }
+    return FVAD_OK;
+  }
   e->vpend = false;
   // the push's end: ev_buf_free of its parity (recorded after its kernels and
   // ticks copy; re-recorded only by the push after next)
@@ -822,8 +840,13 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
     HIP_TRY(wait_event(e->stream, e->ev_prep_done[b]));
     // window output set b is free once push k-2's k_vadm_hbm has read it
     if (e->vadm.n > 0) HIP_TRY(wait_event(e->stream, e->ev_vadm_b[b]));
-    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr, e->ev_fft_a, e->pstream,
-                                e->synth_rec ? e->synth_wait : nullptr, e->ev_synth));
+    // k_fftAw runs on the prep stream only while this engine owns it: on a
+    // shared one (FVAD_SHARE_PREP) it would queue behind the other engine's
+    // waits and couple the two pipelines, so it stays on the engine stream
+    const bool own_prep = e->pstream_ref.use_count() <= 1;
+    HIP_TRY(fvad::launch_staged(a, e->grid_frames, e->stream, timed ? e->ev : nullptr, e->ev_fft_a,
+                                own_prep ? e->pstream : nullptr, e->synth_rec ? e->synth_wait : nullptr,
+                                e->ev_synth));
     e->synth_wait = timed ? e->ev[10] : e->ev_synth;  // (launch_staged records ev[10] in its place when timed)
     e->synth_rec = true;
     e->fft_a_rec = true;
@@ -1018,6 +1041,18 @@ int ensure_slots(fvad_engine *e, int i) {
   const fvad_engine_config &c = e->cfg;
   const size_t B = c.n_streams, C = c.n_channels, T = c.max_ticks;
   const size_t TB = T * B, TBW = TB * e->wpt, frames = TB * C * fvad::kFrame;
+  {
+    // a streaming slot pins one push of input and outputs (fvad_engine_submit,
+    // up to FVAD_MAX_IN_FLIGHT of them); the window outputs grow with W =
+    // windows_per_tick (up to 240 at fft_size 2): refuse configurations whose
+    // slot would not be a sane pinned allocation (the streaming API only:
+    // resident and push-from-host engines never allocate a slot)
+    const double slot = 4.0 * ((double)frames * (c.want_denoised ? 2 : 1) + 3.0 * TB + 2.0 * TBW +
+                               (double)TBW * C * c.n_bands);
+    if (slot > 16.0 * (1ull << 30))
+      return fail(FVAD_ENOMEM, "a push of max_ticks x n_streams needs > 16 GiB of pinned slot memory "
+                               "(outputs scale with windows_per_tick): lower max_ticks or n_streams");
+  }
   if (!e->slots_ready) {
     // the copy stream at the highest priority: its own hardware queue, so the
     // 16-bit ingest's k_pcm16 does not queue behind a long kernel of a stream
@@ -1488,6 +1523,7 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
   fvad::VadmArgs v{};
   v.n = n;
   v.seg_cap = seg_capacity;
+  v.bound_scale = 1.0;
   long long off = 0;
   std::vector<fvad::VadmState> init((size_t)n * B);
   for (int m = 0; m < n; m++) {
@@ -1694,6 +1730,24 @@ extern "C" int fvad_engine_set_debug(fvad_engine *e, int key, int value) {
       if (value < 0) return fail(FVAD_EINVAL, "value >= 0 required");
       e->vadm.defer_max = (unsigned)value;
       return FVAD_OK;
+    case FVAD_DEBUG_VADM_BOUND_SCALE:
+      if (e->vadm.n == 0) return fail(FVAD_EINVAL, "no VADMachines attached");
+      if (value < -1) return fail(FVAD_EINVAL, "value >= -1 required");
+      if (const int rc = fvad_engine_sync(e)) return rc;  // a queued k_vadm_hbm reads the argument block's copy
+      e->vadm.bound_scale = value == -1 ? HUGE_VAL : (value == 0 ? 1.0 : (double)value);
+      return FVAD_OK;
+    case FVAD_DEBUG_VADM_COUNT:
+      if (e->vadm.n == 0) return fail(FVAD_EINVAL, "no VADMachines attached");
+      if (const int rc = fvad_engine_sync(e)) return rc;
+      if (value && !e->vadm.count) {
+        if (const int rc = dalloc(&e->vadm.count, fvad::kVadmCounts)) return rc;
+      }
+      if (!value && e->vadm.count) {
+        HIP_TRY(hipFree(e->vadm.count));
+        e->vadm.count = nullptr;
+      }
+      if (e->vadm.count) HIP_TRY(hipMemset(e->vadm.count, 0, fvad::kVadmCounts * sizeof(unsigned long long)));
+      return FVAD_OK;
     case FVAD_DEBUG_VADM_LT_FULL:
       if (e->vadm.n == 0) return fail(FVAD_EINVAL, "no VADMachines attached");
       e->dbg_lt_full = value != 0;
@@ -1702,6 +1756,17 @@ extern "C" int fvad_engine_set_debug(fvad_engine *e, int key, int value) {
     default:
       return fail(FVAD_EINVAL, "unknown debug key");
   }
+}
+
+extern "C" int fvad_engine_debug_counts(fvad_engine *e, unsigned long long *out, int n) {
+  if (!e || !out || n < 1) return fail(FVAD_EINVAL, "invalid argument");
+  if (!e->vadm.count) return fail(FVAD_EINVAL, "FVAD_DEBUG_VADM_COUNT is not set");
+  if (const int rc = fvad_engine_sync(e)) return rc;
+  unsigned long long c[fvad::kVadmCounts];
+  HIP_TRY(hipMemcpy(c, e->vadm.count, sizeof(c), hipMemcpyDeviceToHost));
+  const int k = std::min(n, (int)fvad::kVadmCounts);
+  for (int i = 0; i < k; i++) out[i] = c[i];
+  return k;
 }
 
 extern "C" int fvad_engine_output_log(fvad_engine *e, int n_pushes) {

@@ -65,4 +65,40 @@ FVAD_HD inline double add_const_n(double acc, double c, unsigned n) {
   return acc;
 }
 
+// The lazy long-term test of the device VADMachine (fvad_staged.hip
+// vadm_stream).  VADMachine.zig:150-167 tests st_avg > RN(lt_avg * f), lt_avg
+// the long-term RollingAverage's fold of its n terms t_i = RN(e_i / n)
+// (RollingAverage.zig:45-56, C order).  Between exact folds the walk carries
+// an estimate `approx` of that fold, updated per long push as
+// RN(RN(approx + t_new) - t_old) (lt_estimate), and the largest |approx| seen
+// since the last exact fold (amax).  With every entry >= 0:
+//  * a fold of n nonnegative terms is within (n - 1) u of their exact sum
+//    (u = 2^-53), and that sum is <= the fold (1 + (n - 1) u) <= ~amax;
+//  * the estimate starts at an exact fold, and each update adds at most
+//    u |approx + t_new| + u |result| <= 2u (2 amax) to its distance from the
+//    exact sum of the current terms;
+// so |approx - fold| <= (n - 1) u (S_then + S_now) + 4 u pending amax, and
+// lt_bound's E = (2n + 4 pending + 64) u amax * 2 covers it twice over (the
+// +64 and the factor 2 absorb the higher-order terms).  `scale` is the test
+// hook FVAD_DEBUG_VADM_BOUND_SCALE (1 in production; +inf: no test settled).
+FVAD_HD inline double lt_bound(unsigned n, unsigned pending, double amax, double scale) {
+  return (2.0 * n + 4.0 * pending + 64.0) * 0x1p-53 * amax * 2.0 * scale;
+}
+// The test from the estimate: 1 if st_avg > RN(fold * f) for every fold within
+// E of approx, 0 if for none, -1 if the bound leaves it open (the caller then
+// folds exactly).  f >= 0: RN is monotone, and RN(approx +- 2E) lies beyond
+// approx +- E, so hi >= RN(fold * f) >= lo.
+FVAD_HD inline int lt_decide(double st_avg, double approx, double E, double f) {
+  const double lo = (approx - 2.0 * E) * f, hi = (approx + 2.0 * E) * f;
+  if (st_avg > hi) return 1;
+  if (st_avg <= lo) return 0;
+  return -1;
+}
+// One long push into the estimate: t_new = RN(pushed * 1/n) replaces t_old
+// (the overwritten entry's term).
+FVAD_HD inline void lt_estimate(double &approx, double &amax, double t_new, double t_old) {
+  approx = (approx + t_new) - t_old;
+  amax = __builtin_fmax(amax, __builtin_fabs(approx));
+}
+
 }  // namespace fvad

@@ -47,7 +47,11 @@ struct VadmState {
   // lt_amax / lt_fpre carry the walk's estimate, its bound's magnitude and the
   // exact fold through the last pushed index; every sync point resolves it)
   unsigned lt_widx, lt_count, st_widx, st_count, r_widx, r_count, lt_nw, lt_defer;
-  int lt_has, st_has, r_has, state, lt_pre_ok, pad0;
+  // lt_neg: long pushes until every negative (or NaN) entry has left the
+  // long-term buffer; the lazy walk's bound needs nonnegative terms, so the
+  // machine folds at every push until then (band energies are >= 0 and a
+  // window's min is at most 999, so this stays 0 on every pipeline output)
+  int lt_has, st_has, r_has, state, lt_pre_ok, lt_neg;
   float rnn_vad, vol_ratio;
   unsigned rnn_vad_count, vol_ratio_count, n_segs, pad;
   double lt_approx, lt_amax, lt_fpre;
@@ -67,7 +71,14 @@ struct VadmArgs {
   int vfinal;  // this launch is a sync point's: every machine's long-term average folded exactly at the end
   int par_serial_every;  // test hook (FVAD_DEBUG_VADM_PAR_SERIAL_EVERY): k_vadm_par hands stream s to its
                          //   in-kernel serial walk when s % par_serial_every == 0; 0 = never
+  double bound_scale;    // test hook (FVAD_DEBUG_VADM_BOUND_SCALE): the lazy test's bound E times this
+                         //   (1 in production; +inf: every test the estimate would settle folds instead)
+  unsigned long long *count;  // test hook (FVAD_DEBUG_VADM_COUNT): null, or [kVadmCounts] device counters
 };
+// the lazy long-term walk's counters (FVAD_DEBUG_VADM_COUNT): long-term tests
+// decided from an exact average, from the estimate, left open by the bound (an
+// exact fold), and the folds at the end of a push (sync point or defer limit)
+enum { kVcExact = 0, kVcSettled = 1, kVcOpen = 2, kVcEndFold = 3, kVadmCounts = 4 };
 
 struct StagedArgs {
   int n_streams, n_channels, n_ticks;

@@ -1834,6 +1834,11 @@ constexpr unsigned kLtDeferMax = FVAD_LT_DEFER_MAX;
 // the fold a deferred machine owes: vadm_stream's fold, the same adds in the
 // same order (the exact prefix through the last pushed index, then the
 // entries after it)
+// lt_neg's bookkeeping for one long push of v
+__device__ __forceinline__ void lt_neg_push(VadmState &S, unsigned n, float v) {
+  if (S.lt_neg > 0) S.lt_neg--;
+  if (!(v >= 0.0f)) S.lt_neg = (int)n;
+}
 __device__ __forceinline__ void lt_resolve(VadmState &S, const VadmConst &K, const float *lt, size_t lts) {
   if (!S.lt_defer) return;
   const unsigned n = (unsigned)K.n_lt;
@@ -1875,8 +1880,13 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
   VadmSeg *seg = a.vadm.seg + ((size_t)m * B + s) * a.vadm.seg_cap;
   const unsigned n = (unsigned)K.n_lt;
   const double f = (double)K.thr_factor, scalar = 1.0 / (double)n;
-  const bool lazy = S.lt_count == n && S.lt_pre_ok && S.lt_has && n > 1 && f >= 0.0 && !(K.has_init && !(K.init >= 0.0));
+  const bool lazy = S.lt_count == n && S.lt_pre_ok && S.lt_has && n > 1 && f >= 0.0 &&
+                    !(K.has_init && !(K.init >= 0.0)) && S.lt_neg == 0;
   if (!lazy) lt_resolve(S, K, lt, lts);  // (a deferring machine is lazy; kept for safety)
+  unsigned long long *cnt = a.vadm.count;
+  // the bound's scale: the test hook's, +inf once a negative entry is pushed
+  // (no bound holds then: every later test of the push folds)
+  double bscale = a.vadm.bound_scale;
   double approx = S.lt_last, amax = fabs(S.lt_last), fpre = 0.0;
   int pending = 0;  // pushes since lt_last was last folded exactly
   if (S.lt_defer) {  // owed from earlier pushes (deferred folds)
@@ -1913,9 +1923,11 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
       bool met;
       if (!lazy) {
         met = vadm_short(S, K, st, rb, B, min_v, vr);
-        if (!met)
+        if (!met) {
           ra_push_long(lt, lts, K.n_lt, S.lt_widx, S.lt_count, S.lt_nw, K.init, S.lt_last, S.lt_has, S.lt_pre,
                        S.lt_pre_ok, min_v);
+          lt_neg_push(S, n, min_v);
+        }
       } else {
         const double st_avg = ra_push(st, B, K.n_st, S.st_widx, S.st_count, S.st_last, S.st_has, min_v);
         const double r_avg = ra_push(rb, B, K.n_r, S.r_widx, S.r_count, S.r_last, S.r_has, vr);
@@ -1923,19 +1935,18 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
         if (r_avg > (double)K.ratio_thr) {  // else met is false whatever the long-term average
           if (pending == 0) {
             met = st_avg > S.lt_last * f;
+            if (cnt) atomicAdd(cnt + kVcExact, 1ull);
           } else {
-            // |approx - fold| <= E (the fold's (n-1) u, twice, and 2u per
-            // estimate update, on the largest estimate; doubled for the
-            // rounding of approx -+ E itself)
-            const double E = (2.0 * n + 4.0 * pending + 64.0) * 0x1p-53 * amax * 2.0;
-            const double lo = (approx - 2.0 * E) * f, hi = (approx + 2.0 * E) * f;
-            if (st_avg > hi) {
-              met = true;
-            } else if (st_avg <= lo) {
-              met = false;
+            // |approx - fold| <= E (fvad_exact.h lt_bound: the fold's (n-1) u,
+            // twice, and 2u per estimate update, on the largest estimate)
+            const int d = lt_decide(st_avg, approx, lt_bound(n, (unsigned)pending, amax, bscale), f);
+            if (d >= 0) {
+              met = d == 1;
+              if (cnt) atomicAdd(cnt + kVcSettled, 1ull);
             } else {  // not settled by the bound: the exact fold
               fold();
               met = st_avg > S.lt_last * f;
+              if (cnt) atomicAdd(cnt + kVcOpen, 1ull);
             }
           }
         }
@@ -1948,14 +1959,18 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
           S.lt_widx = (wi + 1) % n;
           if (S.lt_nw < n) S.lt_nw++;
           S.lt_pre = S.lt_widx == 0 ? 0.0 : fpre;
-          approx = (approx + t_new) - t_old;
-          amax = fmax(amax, fabs(approx));
+          lt_estimate(approx, amax, t_new, t_old);
           pending++;
+          lt_neg_push(S, n, min_v);
+          if (S.lt_neg) bscale = __builtin_inf();
         }
       }
       vadm_fsm(S, K, index, met, vad, vr, seg, a.vadm.seg_cap);
     }
-  if (pending && (final || (unsigned)pending >= (a.vadm.defer_max ? a.vadm.defer_max : kLtDeferMax))) fold();
+  if (pending && (final || (unsigned)pending >= (a.vadm.defer_max ? a.vadm.defer_max : kLtDeferMax))) {
+    fold();
+    if (cnt) atomicAdd(cnt + kVcEndFold, 1ull);
+  }
   S.lt_defer = (unsigned)pending;
   S.lt_approx = approx;
   S.lt_amax = amax;
@@ -2144,6 +2159,7 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
             S.lt_pre = pre;
             S.lt_last = favg[g][q];
             S.lt_has = 1;
+            lt_neg_push(S, n, wmin[g][jj]);
             npush++;
           }
           S.windows_done++;

@@ -96,6 +96,7 @@ class VadmSnapshot(C.Structure):
 
 
 DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR, DEBUG_VADM_LT_FULL, DEBUG_VADM_DEFER_MAX = 1, 2, 3, 4
+DEBUG_VADM_BOUND_SCALE, DEBUG_VADM_COUNT = 5, 6
 SHARE_PREP, SHARE_SIDE = 1, 2  # fvad_engine_share_streams
 
 READ_FN = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.c_int, C.POINTER(F32P), C.c_size_t)
@@ -179,6 +180,7 @@ SYMBOLS = [
     ("fvad_engine_vadm_snapshot", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("fvad_engine_vadm_rolling", C.c_long, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t]),
     ("fvad_engine_set_debug", C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    ("fvad_engine_debug_counts", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     ("fvad_engine_share_streams", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     ("fvad_engine_output_log", C.c_int, [C.c_void_p, C.c_int]),
     ("fvad_engine_output_log_read", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int)]),
@@ -474,8 +476,17 @@ class Engine:
 
     def set_debug(self, key, value):
         """Test hooks (fvad_engine_set_debug): DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR,
-        DEBUG_VADM_LT_FULL, DEBUG_VADM_DEFER_MAX."""
+        DEBUG_VADM_LT_FULL, DEBUG_VADM_DEFER_MAX, DEBUG_VADM_BOUND_SCALE, DEBUG_VADM_COUNT."""
         _check(lib().fvad_engine_set_debug(self.h, key, value), "fvad_engine_set_debug")
+
+    def debug_counts(self):
+        """DEBUG_VADM_COUNT's counters (fvad_engine_debug_counts): long-term tests
+        decided exactly / settled by the bound / left open by it (folded), and
+        end-of-push folds."""
+        out = np.zeros(4, np.uint64)
+        n = lib().fvad_engine_debug_counts(self.h, out.ctypes.data_as(C.c_void_p), 4)
+        _check(n if n < 0 else 0, "fvad_engine_debug_counts")
+        return dict(zip(("exact", "settled", "open", "end_fold"), (int(v) for v in out[:n])))
 
     def output_log(self, n_pushes):
         """Record the per-tick outputs of the next n_pushes pushes on the device (no host sync)."""

@@ -116,6 +116,8 @@ typedef struct {
   int use_denoiser;     /* VAD.Config.use_denoiser (default 1).  0: fft_size frames of raw input go
                          * straight to FFT B (VAD.zig:206-212,239-249); per-tick vad / ratio are -1,
                          * the window ratio is preAnalyzeSegment's over the frame, window vad -1 */
+  /* ABI note (r5): the trailing `unsigned cu_mask[8]` of earlier builds was removed; a binding
+   * compiled against them must drop it (fvad_engine_config_default fills every field) */
 } fvad_engine_config;
 
 /* staged: time-parallel frame kernels + a thin per-stream recurrence kernel;
@@ -316,7 +318,10 @@ long fvad_engine_vadm_rolling(fvad_engine *e, int stream, int machine, int which
  * GPU_MAX_HW_QUEUES of them, 4 by default, shared round-robin once they run
  * out: a main stream sharing one with another engine's k_prep3 waits for it).
  * Synchronises both engines; results are unchanged (dependencies are events).
- * The last engine using a stream destroys it. */
+ * Only k_prep3 moves: an engine alone on its prep stream also runs k_fftAw
+ * there (beside its previous push's tail), one whose prep stream is shared
+ * runs k_fftAw on its own engine stream, so the main pipelines stay
+ * uncoupled.  The last engine using a stream destroys it. */
 #define FVAD_SHARE_PREP 1
 #define FVAD_SHARE_SIDE 2
 int fvad_engine_share_streams(fvad_engine *e, fvad_engine *other, int which);
@@ -335,12 +340,25 @@ int fvad_engine_share_streams(fvad_engine *e, fvad_engine *other, int which);
  *   FVAD_DEBUG_VADM_DEFER_MAX  value k > 0: between sync points k_vadm_hbm
  *     folds a machine's long-term average once k long pushes are owed (1: at
  *     the end of every push); 0: the default bound (4096).  Results are the
- *     same for every k: a sync point resolves every owed fold */
+ *     same for every k: a sync point resolves every owed fold
+ *   FVAD_DEBUG_VADM_BOUND_SCALE  value k > 0: the lazy long-term walk's error
+ *     bound E (fvad_exact.h lt_bound) times k; -1: infinite, so every test the
+ *     estimate would decide takes the exact fold instead; 0: back to 1.
+ *     Results are the same for every k >= 1
+ *   FVAD_DEBUG_VADM_COUNT  value 1: count the long-term tests by how they were
+ *     decided (fvad_engine_debug_counts), from zero; 0: stop counting */
 #define FVAD_DEBUG_VADM_PAR_SERIAL_EVERY 1
 #define FVAD_DEBUG_VADM_ALWAYS_PAR 2
 #define FVAD_DEBUG_VADM_LT_FULL 3
 #define FVAD_DEBUG_VADM_DEFER_MAX 4
+#define FVAD_DEBUG_VADM_BOUND_SCALE 5
+#define FVAD_DEBUG_VADM_COUNT 6
 int fvad_engine_set_debug(fvad_engine *e, int key, int value);
+/* FVAD_DEBUG_VADM_COUNT's counters, out[0..min(n, 4)): long-term tests decided
+ * from an exact average, tests the bound settled from the estimate, tests it
+ * left open (an exact fold), folds at the end of a push.  Returns the count
+ * written (synchronises the engine). */
+int fvad_engine_debug_counts(fvad_engine *e, unsigned long long *out, int n);
 /* Output log: the per-tick outputs (fvad_outputs without denoised) of the next
  * n_pushes pushes are copied into device memory on the engine stream as each
  * push's kernels end -- no host synchronisation, so a run of asynchronous

@@ -1,7 +1,8 @@
 """world_size-2 gloo run of bench.py's multi-GPU logic on CPU: rendezvous on
 127.0.0.1, disjoint stream partitions per rank, barrier, max-over-ranks timing
 and the whole-job rate (the N>1 path the driver launches with
-torch.distributed.run, minus the GPU)."""
+torch.distributed.run, minus the GPU).  bench.py's process group is gloo at
+every N (CPU tensors, no RCCL), so this is the production collective path."""
 import os
 import socket
 import sys
@@ -25,11 +26,13 @@ def _worker(rank, world, port, q):
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     sys.path.insert(0, ROOT)
     import bench
-    r, w, local, dist, torch = bench.dist_setup(world, backend="gloo")
+    r, w, local, dist, torch = bench.dist_setup(world)
+    assert dist.get_backend() == "gloo"  # the production path: no RCCL at any N
     base, n = bench.stream_partition(r, 2048)
     bench.barrier(dist, torch)
     elapsed = 1.0 + r  # rank 1 is the slow one
     mx = bench.max_over_ranks(elapsed, dist, torch)
+    assert not torch.cuda.is_initialized()  # barrier / max-reduce touch no HIP stream
     ids = torch.tensor([base, base + n], dtype=torch.int64)
     gathered = [torch.zeros(2, dtype=torch.int64) for _ in range(w)]
     dist.all_gather(gathered, ids)
@@ -77,3 +80,28 @@ def test_bench_self_launch_two_ranks():
     assert ro["kernels"] == {"k_a": 2.0, "k_b": 2.0}
     assert ro["ranks"]["max_rank"] == {"k_a": 1, "k_b": 0}
     assert set(ro["ranks"]["per_rank"]) == {"0", "1"}
+
+
+def test_bench_has_no_rccl_path():
+    """The bench's collectives are gloo only: no RCCL
+    communicator or torch HIP stream beside the engine's streams."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "nccl" not in src and "torch.cuda" not in src
+
+
+def test_bench_world_one_under_launcher():
+    """--gpus 1 under torch.distributed.run (world 1): the gloo group is
+    initialised like at N > 1 and the line carries the per-rank table."""
+    import json
+    import subprocess
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                          os.path.join(ROOT, "bench.py"), "--gpus", "1", "--cpu-stub", "--steps", "3", "--warmup", "1"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and set(d["roofline"]["ranks"]["per_rank"]) == {"0"}

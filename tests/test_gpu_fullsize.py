@@ -17,7 +17,9 @@ re-block, FFT B; VADMachine.zig:126-230 segments):
   every stream's segments, the whole VADMachine state (fvad_engine_vadm_snapshot)
   and its RollingAverage buffers against the oracle fed the same 25 pushes;
   also with every machine on k_vadm_par and a third of them forced through its
-  in-kernel serial fallback;
+  in-kernel serial fallback, and with the lazy long-term bound made infinite
+  (every test the estimate would settle folds exactly); the fp16 variant under
+  the same schedule at its tolerance;
 * configs[3]'s per-GPU shard: 4096 streams over 8 GPUs = 512 streams, here
   rank 3's ids 1536..2047, 12 pushes (6 s, the silence included), staged and
   fp16.
@@ -286,9 +288,14 @@ def test_bench_schedule_staged_every_stream(fvad_mod, oracle_mod, model):
     eng.load_synthetic(T, base=base, pushes=P)
     ref = oracle_workload(*BENCH)
     for schedule in ("bench", "nosync"):
+        eng.set_debug(fvad_mod.DEBUG_VADM_COUNT, 1)
         got, segs, state = run_schedule(eng, schedule, False, B)
+        cnt = eng.debug_counts()
+        eng.set_debug(fvad_mod.DEBUG_VADM_COUNT, 0)
         check_exact(last_push(ref, T), got, segs)
         check_state(ref, state)
+        # how the lazy long-term walk decided its tests
+        print("bench schedule %s: long-term tests %s" % (schedule, cnt))
         got, segs, state = run_schedule(eng, schedule, True, B)
         assert got["vad"].shape == (len(ref[0][0]), B)
         n_seg = check_exact(ref, got, segs)
@@ -300,3 +307,37 @@ def test_bench_schedule_staged_every_stream(fvad_mod, oracle_mod, model):
     check_exact(ref, got, segs)
     check_state(ref, state)
     print("k_vadm_par on every push, every third stream on its serial fallback: bit-exact")
+    # the lazy walk with its bound made infinite: every test the estimate
+    # would settle takes vadm_stream's open branch (the exact fold)
+    eng.set_debug(fvad_mod.DEBUG_VADM_ALWAYS_PAR, 0)
+    eng.set_debug(fvad_mod.DEBUG_VADM_PAR_SERIAL_EVERY, 0)
+    eng.set_debug(fvad_mod.DEBUG_VADM_BOUND_SCALE, -1)
+    eng.set_debug(fvad_mod.DEBUG_VADM_COUNT, 1)
+    got, segs, state = run_schedule(eng, "nosync", True, B)
+    cnt = eng.debug_counts()
+    check_exact(ref, got, segs)
+    check_state(ref, state)
+    assert cnt["open"] > 0 and cnt["settled"] == 0, cnt
+    print("bound made infinite: bit-exact, long-term tests %s" % cnt)
+
+
+@pytest.mark.timeout(900)
+def test_bench_schedule_fp16_every_stream(fvad_mod, oracle_mod, model):
+    """The fp16 variant (configs[4]; bench.py's `variants.fp16` line) under the
+    bench's own schedule: 2048 streams, the 25 pushes through
+    run_resident with no synchronisation inside a leg -- k_prep3 of push k+1
+    and k_vadm_hbm of push k beside push k+1's kernels -- every push's outputs
+    from the device output log and every stream's segments, within
+    check_tolerance's bounds and MAX_MOVED, for the bench's (5, sync, 20, sync)
+    schedule and 25 back to back."""
+    base, B, P, R = BENCH
+    eng = fvad_mod.Engine(model, B, 2, max_ticks=T, mode="fp16")
+    eng.attach_vadm()
+    eng.load_synthetic(T, base=base, pushes=P)
+    ref = oracle_workload(*BENCH)
+    for schedule in ("bench", "nosync"):
+        got, segs, _ = run_schedule(eng, schedule, True, B)
+        assert got["vad"].shape == (len(ref[0][0]), B)
+        wv, wb, n_seg, diffs = check_tolerance(ref, got, segs)
+        print("fp16 bench schedule %s: max |dvad| %.3g, band rel %.3g, %d segments, moved bounds %s" % (
+            schedule, wv, wb, n_seg, diffs))

@@ -33,10 +33,15 @@ def host_segments(fvad_mod, outs, cfg, C, slot, stream):
     return vm.segments()
 
 
-@pytest.mark.parametrize("alt_init,alt_lt_sec,sync_each,defer_max",
-                         [(True, 180.0, False, 0), (False, 180.0, False, 0), (True, 10.0, True, 0),
-                          (True, 10.0, False, 0), (True, 10.0, False, 1), (True, 10.0, False, 7)])
-def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each, defer_max):
+@pytest.mark.parametrize("alt_init,alt_lt_sec,sync_each,defer_max,bound",
+                         [(True, 180.0, False, 0, 0), (False, 180.0, False, 0, 0), (True, 10.0, True, 0, 0),
+                          (True, 10.0, False, 0, 0), (True, 10.0, False, 1, 0), (True, 10.0, False, 7, 0),
+                          (True, 10.0, False, 0, -1), (True, 180.0, False, 0, -1)])
+def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each, defer_max, bound):
+    """bound -1: FVAD_DEBUG_VADM_BOUND_SCALE infinite -- every long-term test
+    the lazy walk's estimate would settle takes the exact fold instead (the
+    branch the bound leaves open, fvad_staged.hip vadm_stream), counted with
+    FVAD_DEBUG_VADM_COUNT."""
     m = fvad_mod.Model(seed=1)
     alt = fvad_mod.VadmConfig.default()
     alt.speech_min_freq, alt.speech_max_freq = 300.0, 3000.0
@@ -50,6 +55,9 @@ def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each, def
     eng.attach_vadm([fvad_mod.VadmConfig.default(), alt])
     if defer_max:  # the long-term fold owed across at most defer_max long pushes (1: every push)
         eng.set_debug(fvad_mod.DEBUG_VADM_DEFER_MAX, defer_max)
+    if bound:
+        eng.set_debug(fvad_mod.DEBUG_VADM_BOUND_SCALE, bound)
+        eng.set_debug(fvad_mod.DEBUG_VADM_COUNT, 1)
     B, C = len(streams), 2
     lens = [x.shape[1] // 480 for x in streams]
     outs = []
@@ -73,9 +81,13 @@ def test_device_vadm_matches_host(fvad_mod, alt_init, alt_lt_sec, sync_each, def
             assert got == ref, (s, mi, got[:3], ref[:3])
             total += len(ref)
     assert total > 0
+    if bound:  # the open branch ran, and nothing was settled from the estimate
+        cnt = eng.debug_counts()
+        assert cnt["open"] > 0 and cnt["settled"] == 0, cnt
 
 
-@pytest.mark.parametrize("flavour", ["default", "always_par", "par_serial_fallback", "defer_max_5", "ragged"])
+@pytest.mark.parametrize("flavour", ["default", "always_par", "par_serial_fallback", "defer_max_5", "ragged",
+                                     "bound_open", "bound_open_defer_max_5"])
 def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
     """The whole device machine state (fvad_engine_vadm_snapshot: speech state
     and indices, RollingAverage last averages / write indices / counts, the
@@ -89,7 +101,11 @@ def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
     are resolved in the middle of pushes as well as by the sync point; ragged:
     three streams end early (3, 6 and 9.5 s of 14), so their machines owe a
     fold from their last pushes and have no ticks when the sync point's
-    k_vadm_par resolves it."""
+    k_vadm_par resolves it; bound_open (also with defer_max_5): the lazy
+    walk's bound made infinite (FVAD_DEBUG_VADM_BOUND_SCALE = -1), so every
+    long-term test it would settle from the estimate runs the exact fold
+    (vadm_stream's open branch), counted (FVAD_DEBUG_VADM_COUNT); default
+    counts how its tests were decided and needs some settled by the bound."""
     m = fvad_mod.Model(seed=1)
     om = oracle_mod.Model(seed=1)
     ids = [0, 3, 19, 39, 7, 12, 59, 8]
@@ -103,9 +119,18 @@ def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
         eng.set_debug(fvad_mod.DEBUG_VADM_ALWAYS_PAR, 1)
     if flavour == "par_serial_fallback":
         eng.set_debug(fvad_mod.DEBUG_VADM_PAR_SERIAL_EVERY, 2)
-    if flavour == "defer_max_5":
+    if flavour.endswith("defer_max_5"):
         eng.set_debug(fvad_mod.DEBUG_VADM_DEFER_MAX, 5)
+    if flavour.startswith("bound_open"):
+        eng.set_debug(fvad_mod.DEBUG_VADM_BOUND_SCALE, -1)
+    eng.set_debug(fvad_mod.DEBUG_VADM_COUNT, 1)
     pu.engine_run(fvad_mod, eng, streams, 50, denoised=False)
+    cnt = eng.debug_counts()
+    print(flavour, cnt)
+    if flavour.startswith("bound_open"):
+        assert cnt["open"] > 0 and cnt["settled"] == 0, cnt
+    elif flavour == "default":
+        assert cnt["settled"] > 0, cnt
     for s, x in enumerate(streams):
         p = oracle_mod.Pipeline(2, om)
         for k in range(0, x.shape[1], 24000):

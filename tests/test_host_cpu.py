@@ -205,3 +205,31 @@ def test_add_const_n_exact(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 / 200000 mismatches" in out.stdout
+
+
+def test_lazy_longterm_bound(tmp_path):
+    """The device VADMachine's lazy long-term test (fvad_staged.hip vadm_stream
+    via fvad_exact.h lt_bound / lt_decide / lt_estimate, the code the kernel
+    compiles) decides exactly as the reference's st_avg > RN(avg * f)
+    (VADMachine.zig:150-167, RollingAverage.zig:45-56) on 2 * 10^6 adversarial
+    decisions: st_avg at the exact threshold and +-1, +-2 ulps of it, at the
+    bound's window edges +-1, +-2 ulps, over value streams spanning 70 binades
+    and owed runs up to 4096 pushes.  Every settled decision matches, and the
+    estimate stays within a quarter of E.  With E scaled by 10^-3 the same
+    harness finds mismatches: it is sharp enough to catch a bound that is too
+    tight."""
+    import re
+    import subprocess
+    exe = tmp_path / "ltb"
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-std=c++20", "-I",
+                           os.path.join(PKG, "csrc"), os.path.join(ROOT, "tests", "lt_bound_harness.cpp"), "-o",
+                           str(exe)])
+    out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    m = re.search(r"decisions (\d+) settled (\d+) open (\d+) mismatches (\d+) .* max \|approx-fold\|/E (\S+)", out.stdout)
+    assert m, out.stdout
+    dec, settled, opened, bad, worst = int(m[1]), int(m[2]), int(m[3]), int(m[4]), float(m[5])
+    assert dec >= 2000000 and bad == 0 and settled > 0.3 * dec and opened > 0.3 * dec, out.stdout
+    assert worst < 0.5, out.stdout
+    sharp = subprocess.run([str(exe), "200000", "1e-3"], capture_output=True, text=True, timeout=120)
+    assert sharp.returncode == 1 and "MISMATCH" in sharp.stdout, sharp.stdout
