@@ -198,6 +198,9 @@ struct fvad_engine {
   bool slots_ready = false;
   int sub_next = 0, col_next = 0;
   int16_t *d_pcm16 = nullptr;  // device staging of a 16-bit submit (converted into d_pcm by k_pcm16)
+  // this push's input is 16-bit samples in d_pcm's buffer, read by k_prep3
+  // itself (staged engines with the denoiser: no d_pcm16, no k_pcm16)
+  bool pcm16_push = false;
 
 };
 
@@ -772,6 +775,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   a.ticks_valid = use_ticks ? e->d_ticks : nullptr;
   a.tail = use_tail ? e->d_ticks + c.n_streams : nullptr;  // [B..2B) of the ticks buffer
   a.pcm = e->d_pcm;
+  a.pcm16 = e->pcm16_push ? reinterpret_cast<const int16_t *>(e->d_pcm) : nullptr;
   a.xs = e->d_xs;
   a.xlp = e->d_xlp_b[b];
   a.LX = e->LX;
@@ -1212,11 +1216,19 @@ int submit_any(fvad_engine *e, const Sample *pcm, int n_ticks, const int32_t *ti
   const bool staged = c.mode != FVAD_MODE_FUSED;
   hipStream_t cs = staged ? e->cstream : e->stream;
   if ((rc = input_buffer(e, cs))) return rc;
+  // staged with the denoiser: k_prep3 reads the 16-bit samples straight from
+  // the input buffer (half its input bytes; the copy stream carries only the
+  // H2D copy, and no conversion kernel takes a slot beside the pushes)
+  const bool direct16 = k16 && staged && c.use_denoiser && !e->raw_s16;
   if constexpr (k16) {
-    // d_pcm16 is overwritten by the next 16-bit submit only after this
-    // conversion read it (both on cs, in order)
-    HIP_TRY(hipMemcpyAsync(e->d_pcm16, sl.in16, n_samples * sizeof(int16_t), hipMemcpyHostToDevice, cs));
-    HIP_TRY(fvad::launch_pcm16(e->d_pcm16, e->d_pcm, n_samples, cs));
+    if (direct16) {
+      HIP_TRY(hipMemcpyAsync(e->d_pcm, sl.in16, n_samples * sizeof(int16_t), hipMemcpyHostToDevice, cs));
+    } else {
+      // d_pcm16 is overwritten by the next 16-bit submit only after this
+      // conversion read it (both on cs, in order)
+      HIP_TRY(hipMemcpyAsync(e->d_pcm16, sl.in16, n_samples * sizeof(int16_t), hipMemcpyHostToDevice, cs));
+      HIP_TRY(fvad::launch_pcm16(e->d_pcm16, e->d_pcm, n_samples, cs));
+    }
   } else {
     HIP_TRY(hipMemcpyAsync(e->d_pcm, sl.in, bytes, hipMemcpyHostToDevice, cs));
   }
@@ -1232,7 +1244,10 @@ int submit_any(fvad_engine *e, const Sample *pcm, int n_ticks, const int32_t *ti
   HIP_TRY(hipEventRecord(sl.h2d, cs));
   sl.h2d_busy = true;
   if (staged) HIP_TRY(hipStreamWaitEvent(e->pstream, sl.h2d, 0));
-  if ((rc = launch(e, n_ticks, use_ticks, false, !tt.empty()))) return rc;
+  e->pcm16_push = direct16;
+  rc = launch(e, n_ticks, use_ticks, false, !tt.empty());
+  e->pcm16_push = false;
+  if (rc) return rc;
   if ((rc = release_input(e))) return rc;
   // outputs into the slot's pinned buffers, after the kernels on the engine
   // stream (the next push's kernels queue behind these copies)

@@ -87,6 +87,7 @@ struct StagedArgs {
   const int *ticks_valid;  // nullable
   const int *tail;         // nullable: real samples (1..480) in each stream's last valid tick (use_denoiser = 0)
   const float *pcm;        // [t][s][c][480] normalised input
+  const int16_t *pcm16;    // nullable: the same as 16-bit samples k (k / 32768), read by k_prep3 instead of pcm
   float *xs;               // [s][L] high-passed s16-scale samples, 1248 history first
   float *xlp;              // [s][LX] pitch_downsample's x_lp over xs (x_lp[m] from xs[2m-1..2m+1]),
   int LX;                  //   624 history first (= 624 + V * 240); m = 0 unused

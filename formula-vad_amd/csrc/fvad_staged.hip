@@ -91,18 +91,29 @@ static_assert((kFrame / 4) % kPrepRing == 0, "prep ring must divide a frame");
 // floats apart, and a tick holds a whole number of blocks, so a block is one
 // base pointer and kPrepRing immediate offsets.  The next block's chunks load
 // while this block's are filtered (the last block reloads itself).
-template <bool Scaled>
-__device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, float &mem0, float &mem1) {
-  constexpr int kChunksCh = kFrame / 4;  // float4 chunks of one channel's frame
+// A chunk is 4 samples: a float4 of the float input, or a uint2 of 16-bit
+// samples k (fvad_engine_submit_i16), read as k / 32768.0f -- k_pcm16's
+// conversion, exact in f32, done here so the 16-bit push needs no float copy
+// of its input (half k_prep3's input bytes, and no conversion kernel).
+__device__ __forceinline__ float4 chunk4(float4 v) { return v; }
+__device__ __forceinline__ float4 chunk4(uint2 v) {
+  constexpr float k = 1.0f / 32768.0f;
+  return make_float4((float)(short)(v.x & 0xffffu) * k, (float)(short)(v.x >> 16) * k,
+                     (float)(short)(v.y & 0xffffu) * k, (float)(short)(v.y >> 16) * k);
+}
+template <bool Scaled, typename In>
+__device__ __forceinline__ void prep_chain(const StagedArgs &a, const void *src, int s, int nt, float &mem0,
+                                           float &mem1) {
+  constexpr int kChunksCh = kFrame / 4;  // chunks of one channel's frame
   static_assert(kChunksCh % kPrepRing == 0, "ring blocks end at channel boundaries");
   const int C = a.n_channels;
   const int per_tick = C * kChunksCh;
   const int bpt = per_tick / kPrepRing;  // blocks per tick
   const int nb = nt * bpt;
-  const size_t tick_stride = (size_t)a.n_streams * C * kFrame;
-  const float4 *tick_row = reinterpret_cast<const float4 *>(a.pcm + (size_t)s * C * kFrame);
+  const size_t tick_stride = (size_t)a.n_streams * per_tick;  // in chunks
+  const In *tick_row = reinterpret_cast<const In *>(src) + (size_t)s * per_tick;
   float4 *dst = reinterpret_cast<float4 *>(a.xs + (size_t)s * a.L + kHist);
-  float4 ring[kPrepRing];
+  In ring[kPrepRing];
 #pragma unroll
   for (int u = 0; u < kPrepRing; u++) ring[u] = tick_row[u];
   int rn = 1;  // block within the tick of the next block
@@ -127,13 +138,13 @@ __device__ __forceinline__ void prep_chain(const StagedArgs &a, int s, int nt, f
   for (int b = 0; b < nb; b++) {
     if (rn == bpt && b + 1 < nb) {
       rn = 0;
-      tick_row = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(tick_row) + tick_stride);
+      tick_row += tick_stride;
     }
-    const float4 *q = tick_row + (b + 1 < nb ? rn : rn - 1) * kPrepRing;
+    const In *q = tick_row + (b + 1 < nb ? rn : rn - 1) * kPrepRing;
     rn++;
 #pragma unroll
     for (int u = 0; u < kPrepRing; u++) {
-      const float4 x = ring[u];
+      const float4 x = chunk4(ring[u]);
       ring[u] = q[u];
       float4 y;
       y.x = step(x.x);
@@ -213,9 +224,11 @@ __global__ void __launch_bounds__(64) k_prep3(StagedArgs a) {
         float *hp = a.state + (size_t)s * st::kWords + st::kHp;
         float mem0 = hp[0], mem1 = hp[1];
         if (a.raw_s16)
-          prep_chain<false>(a, s, nt, mem0, mem1);
+          prep_chain<false, float4>(a, a.pcm, s, nt, mem0, mem1);
+        else if (a.pcm16)
+          prep_chain<true, uint2>(a, a.pcm16, s, nt, mem0, mem1);
         else
-          prep_chain<true>(a, s, nt, mem0, mem1);
+          prep_chain<true, float4>(a, a.pcm, s, nt, mem0, mem1);
         hp[0] = mem0;
         hp[1] = mem1;
       }
