@@ -357,20 +357,51 @@ def host_rate(grp, args, rank, dist, torch, base):
         grp.sync()
         barrier(dist, torch)
         sec = max_over_ranks(time.perf_counter() - t0, dist, torch)
+        # the same stream in steady state: W + K pushes back to back, timed from
+        # the completion (collect) of push W - 1 to that of push W + K - 1 --
+        # K push periods with the pipeline full, no fill or drain (a continuous
+        # ingest's rate; the line above starts and ends with nothing in flight)
+        W = DEPTH + 2
+        done = []
+        inflight = 0
+        for k in range(W + args.steps):
+            if inflight == DEPTH:
+                for e in es:
+                    e.collect(want=True)
+                done.append(time.perf_counter())
+                inflight -= 1
+            for g, e in enumerate(es):
+                if kind == "pinned_i16":
+                    e.submit_i16(e.input_slot_i16()[:T])
+                else:
+                    e.submit(e.input_slot()[:T] if kind == "pinned" else pages[g])
+            inflight += 1
+        while inflight:
+            for e in es:
+                e.collect(want=True)
+            done.append(time.perf_counter())
+            inflight -= 1
+        grp.sync()
+        barrier(dist, torch)
+        steady = max_over_ranks(done[W + args.steps - 1] - done[W - 1], dist, torch)
         rss_stage("host_" + kind)
         res[kind] = (aggregate_rate(grp.B * Ch * T, 1 if dist is None else dist.get_world_size(), args.steps, sec),
-                     1000.0 * sec / args.steps)
+                     1000.0 * sec / args.steps, 1000.0 * steady / args.steps)
     in_bytes = sum(int(sg[0].nbytes) for sg in slots)
     return {"value": round(res["pinned"][0], 1), "unit": "frames/s", "ms_per_step": round(res["pinned"][1], 3),
             "pageable_value": round(res["pageable"][0], 1), "pageable_ms_per_step": round(res["pageable"][1], 3),
             "i16_value": round(res["pinned_i16"][0], 1), "i16_ms_per_step": round(res["pinned_i16"][1], 3),
+            "steady_ms_per_step": {k: round(v[2], 3) for k, v in res.items()},
             "input_bytes_per_step": in_bytes, "i16_input_bytes_per_step": in_bytes // 2,
             "note": "streaming submit/collect, 3 pushes in flight per engine, input = the first two pushes of the "
                     "synthetic streams alternating: from pinned host slots (value) or pageable host arrays holding "
                     "the first push (pageable_value), H2D over PCIe inside the timed region and overlapped with "
                     "the previous push; per-tick outputs copied back every push; i16_value: the same audio as "
                     "16-bit samples from the pinned 16-bit slots (fvad_engine_submit_i16, k / 32768 converted on "
-                    "the device)"}
+                    "the device).  steady_ms_per_step: the same streams with the pipeline kept full -- push "
+                    "periods from one collect to the one %d pushes later, after %d pushes of warm-up (the "
+                    "*_ms_per_step figures start and end with nothing in flight, so they include the first "
+                    "push's H2D copy and k_prep3 and the last push's drain)" % (args.steps, DEPTH + 2)}
 
 
 def gather_kernel_tables(kt, dist, torch, rank):
