@@ -657,7 +657,7 @@ __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftbw(StagedArgs a) {
 // k_winmeta (completion, share-weighted volume ratio, window vad) runs on
 // every wave of the stream identically; channel 0 writes it.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64 * kWNW, 4) k_olafb(StagedArgs a) {
+__global__ void __launch_bounds__(64 * kWNW, kWOcc) k_olafb(StagedArgs a) {
   __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][kFbSlots];  // window samples, then the FFT exchanges
   __shared__ float mg[kWNW][kFbMag];
   __shared__ float ovg[kWNW][kFrame];  // a completing tick's samples past the window
