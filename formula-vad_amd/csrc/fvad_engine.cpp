@@ -1539,6 +1539,7 @@ extern "C" int fvad_engine_attach_vadm(fvad_engine *e, const fvad_vadm_config *c
   v.n = n;
   v.seg_cap = seg_capacity;
   v.bound_scale = 1.0;
+  v.negate_at = -1;
   long long off = 0;
   std::vector<fvad::VadmState> init((size_t)n * B);
   for (int m = 0; m < n; m++) {
@@ -1750,6 +1751,12 @@ extern "C" int fvad_engine_set_debug(fvad_engine *e, int key, int value) {
       if (value < -1) return fail(FVAD_EINVAL, "value >= -1 required");
       if (const int rc = fvad_engine_sync(e)) return rc;  // a queued k_vadm_hbm reads the argument block's copy
       e->vadm.bound_scale = value == -1 ? HUGE_VAL : (value == 0 ? 1.0 : (double)value);
+      return FVAD_OK;
+    case FVAD_DEBUG_VADM_NEGATE_AT:
+      if (e->vadm.n == 0) return fail(FVAD_EINVAL, "no VADMachines attached");
+      if (value < -1) return fail(FVAD_EINVAL, "value >= -1 required");
+      if (const int rc = fvad_engine_sync(e)) return rc;
+      e->vadm.negate_at = value;
       return FVAD_OK;
     case FVAD_DEBUG_VADM_COUNT:
       if (e->vadm.n == 0) return fail(FVAD_EINVAL, "no VADMachines attached");

@@ -74,6 +74,8 @@ struct VadmArgs {
   double bound_scale;    // test hook (FVAD_DEBUG_VADM_BOUND_SCALE): the lazy test's bound E times this
                          //   (1 in production; +inf: every test the estimate would settle folds instead)
   unsigned long long *count;  // test hook (FVAD_DEBUG_VADM_COUNT): null, or [kVadmCounts] device counters
+  long long negate_at;   // test hook (FVAD_DEBUG_VADM_NEGATE_AT): window number whose band minimum enters
+                         //   the machine negated (lt_neg's path); -1 = none
 };
 // the lazy long-term walk's counters (FVAD_DEBUG_VADM_COUNT): long-term tests
 // decided from an exact average, from the estimate, left open by the bound (an

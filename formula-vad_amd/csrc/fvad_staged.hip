@@ -1924,13 +1924,14 @@ __device__ void vadm_stream(const StagedArgs &a, int m, int s, float *lt, size_t
     for (int w = 0, nw = a.out_win_flag[(size_t)t * B + s]; w < nw; w++) {
       const size_t o = ((size_t)t * B + s) * a.wpt + w;
       const unsigned long long index = S.windows_done * fft;
-      S.windows_done++;
       float min_v = 999, max_v = 0;
       for (int c = 0; c < C; c++) {
         const float v = a.out_band[(o * C + c) * nb + K.slot];
         if (v < min_v) min_v = v;
         if (v > max_v) max_v = v;
       }
+      if ((long long)S.windows_done == a.vadm.negate_at) min_v = -min_v;  // test hook
+      S.windows_done++;
       // fft_input.vad orelse 0 (VADMachine.zig:240-246): no vad without the denoiser
       const float vad = a.use_denoiser ? a.out_win_vad[o] : 0.0f, vr = a.out_win_ratio[o];
       bool met;
@@ -2086,6 +2087,11 @@ __global__ void __launch_bounds__(64) k_vadm_par(StagedArgs a) {
       }
     }
     wave_sync();
+    if (r == 0 && sok && a.vadm.negate_at >= 0) {  // test hook FVAD_DEBUG_VADM_NEGATE_AT
+      const long long k = a.vadm.negate_at - (long long)Ss[g].windows_done;
+      if (k >= 0 && k < Kw && k < kVpMaxW) wmin[g][k] = -wmin[g][k];
+      wave_sync();
+    }
     VadmState &S = Ss[g];
     float *st = a.vadm.buf + K.st_off + (sok ? s : 0), *rb = a.vadm.buf + K.r_off + (sok ? s : 0);
     VadmSeg *seg = a.vadm.seg + ((size_t)m * B + (sok ? s : 0)) * a.vadm.seg_cap;

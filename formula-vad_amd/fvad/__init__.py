@@ -96,7 +96,7 @@ class VadmSnapshot(C.Structure):
 
 
 DEBUG_VADM_PAR_SERIAL_EVERY, DEBUG_VADM_ALWAYS_PAR, DEBUG_VADM_LT_FULL, DEBUG_VADM_DEFER_MAX = 1, 2, 3, 4
-DEBUG_VADM_BOUND_SCALE, DEBUG_VADM_COUNT = 5, 6
+DEBUG_VADM_BOUND_SCALE, DEBUG_VADM_COUNT, DEBUG_VADM_NEGATE_AT = 5, 6, 7
 SHARE_PREP, SHARE_SIDE = 1, 2  # fvad_engine_share_streams
 
 READ_FN = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.c_int, C.POINTER(F32P), C.c_size_t)

@@ -346,13 +346,18 @@ int fvad_engine_share_streams(fvad_engine *e, fvad_engine *other, int which);
  *     estimate would decide takes the exact fold instead; 0: back to 1.
  *     Results are the same for every k >= 1
  *   FVAD_DEBUG_VADM_COUNT  value 1: count the long-term tests by how they were
- *     decided (fvad_engine_debug_counts), from zero; 0: stop counting */
+ *     decided (fvad_engine_debug_counts), from zero; 0: stop counting
+ *   FVAD_DEBUG_VADM_NEGATE_AT  value k >= 0: window k of every stream enters
+ *     every machine with its band minimum negated (a value the pipeline never
+ *     produces: the path that folds exactly until that entry has left the
+ *     long-term buffer); -1: off (default) */
 #define FVAD_DEBUG_VADM_PAR_SERIAL_EVERY 1
 #define FVAD_DEBUG_VADM_ALWAYS_PAR 2
 #define FVAD_DEBUG_VADM_LT_FULL 3
 #define FVAD_DEBUG_VADM_DEFER_MAX 4
 #define FVAD_DEBUG_VADM_BOUND_SCALE 5
 #define FVAD_DEBUG_VADM_COUNT 6
+#define FVAD_DEBUG_VADM_NEGATE_AT 7
 int fvad_engine_set_debug(fvad_engine *e, int key, int value);
 /* FVAD_DEBUG_VADM_COUNT's counters, out[0..min(n, 4)): long-term tests decided
  * from an exact average, tests the bound settled from the estimate, tests it

@@ -139,3 +139,58 @@ def test_device_vadm_state_matches_oracle(fvad_mod, oracle_mod, flavour):
         for which in range(3):
             assert np.array_equal(eng.vadm_rolling(s, which), p.vadm_rolling(which)), (s, which)
         assert eng.segments(s) == p.segments(), s
+
+
+@pytest.mark.parametrize("negate_at", [60, 700])
+def test_device_vadm_negative_entry_matches_host(fvad_mod, negate_at):
+    """A band minimum the pipeline never produces -- window `negate_at` of every
+    stream enters the machines negated (FVAD_DEBUG_VADM_NEGATE_AT) -- voids the
+    lazy walk's bound (it holds for nonnegative terms), so the device machine
+    folds exactly until that entry has left the long-term buffer (lt_neg) and
+    then goes back to the lazy walk: the 10 s alternative machine (234
+    entries) does both within these 40-70 s streams, the default 180 s one
+    stays on the exact path.  Segments and their debug averages equal the
+    host VADMachine's fed the same values (VADMachine.zig:126-230)."""
+    m = fvad_mod.Model(seed=1)
+    alt = fvad_mod.VadmConfig.default()
+    alt.speech_min_freq, alt.speech_max_freq = 300.0, 3000.0
+    alt.min_vad_duration_sec = 0.3
+    alt.long_term_speech_avg_sec = 10.0
+    ids, secs = [0, 4, 19, 42], [70.0, 55.5, 40.0, 66.0]
+    streams = [fvad_mod.synth_stream(i, int(48000 * s), 2)[0] for i, s in zip(ids, secs)]
+    eng = fvad_mod.Engine(m, len(streams), 2, max_ticks=64, bands=((4, 64), (13, 128)))
+    eng.attach_vadm([fvad_mod.VadmConfig.default(), alt])
+    eng.set_debug(fvad_mod.DEBUG_VADM_NEGATE_AT, negate_at)
+    B, C = len(streams), 2
+    lens = [x.shape[1] // 480 for x in streams]
+    outs = []
+    for t0 in range(0, max(lens), 64):
+        nt = min(64, max(lens) - t0)
+        pcm = np.zeros((nt, B, C, 480), np.float32)
+        valid = np.zeros(B, np.int32)
+        for s, x in enumerate(streams):
+            v = max(0, min(nt, lens[s] - t0))
+            valid[s] = v
+            if v:
+                pcm[:v, s] = x[:, t0 * 480:(t0 + v) * 480].reshape(C, v, 480).transpose(1, 0, 2)
+        outs.append((eng.push(pcm, ticks_valid=valid), valid))
+    total = 0
+    for s in range(B):
+        for mi, (cfg, slot) in enumerate(((fvad_mod.VadmConfig.default(), 0), (alt, 1))):
+            vm = fvad_mod.VADMachine(cfg, n_channels=C)
+            wd = 0
+            for o, valid in outs:
+                for t in range(valid[s]):
+                    if not o["win_flag"][t, s]:
+                        continue
+                    band = np.array(o["band"][t, s, :, slot], np.float32)
+                    if wd == negate_at:  # the machine sees -min over the channels
+                        band = np.full(C, -band.min(), np.float32)
+                    vm.run(wd * 2048, band, float(o["win_vad"][t, s]), float(o["win_ratio"][t, s]))
+                    wd += 1
+            assert wd > negate_at + 234, (s, wd)
+            ref = vm.segments()
+            got = eng.segments(s, mi)
+            assert got == ref, (s, mi, got[:3], ref[:3])
+            total += len(ref)
+    assert total > 0
