@@ -17,22 +17,13 @@ NAMES = ["load state", "pitch shift", "analysis window+scatter", "FFT A (X) + co
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 MODE = sys.argv[3] if len(sys.argv) > 3 else "fused"
-FFTA = []
-if MODE == "staged" and os.environ.get("FVAD_RNN", "3") == "3":
+if MODE == "staged":  # k_rnn3 (the only staged recurrence kernel since r2)
     NAMES = ["P1 z|r gates + spectral variability(t) + gains(t-5)",
              "P2 candidates, dense(t), outputs, features(t+1)",
              "  P1 role: denoise z|r", "  P1 role: noise z|r", "  P1 role: vad z|r", "  P1 role: spectral var",
              "  P1 role: gains", "", "  P2 role: denoise h", "  P2 role: noise h", "  P2 role: vad h",
              "  P2 role: dense", "  P2 role: denoise_output", "  P2 role: vad_output", "  P2 role: features"]
     ROLES = True
-elif MODE == "staged" and os.environ.get("FVAD_RNN") == "2":
-    NAMES = ["P1 z|r gates + features(t+1) + gains(t-3)", "P2 candidates + spectral variability",
-             "P3 outputs, dense(t+1), vad_out"] + [""] * 9
-elif MODE == "staged":
-    NAMES = ["features+deltas+dist row", "spectral variability", "dense", "vad z|r", "vad h", "noise z|r + vad_out",
-             "noise h", "denoise z|r", "denoise h", "denoise_output", "gains + outputs + prefetch", "next act"]
-    FFTA = ["group setup", "window scatter (global loads)", "FFT 960 x F", "X store + band sums + log10",
-            "Ly chain + silence", "DCT(Ly)"]
 if MODE == "fp16":  # k_gru16 supersteps (fvad_gru16.hip), stamps[48..49]
     GRU = ["A  z|r gates vad(u-1) noise(u-2) denoise(u-3), dense(u), outputs, features(u+1)",
            "B  candidates vad(u-1) noise(u-2) denoise(u-3), gains(u-4), spectral var(u+1)"]
@@ -70,13 +61,6 @@ for i, n in enumerate(NAMES[:24]):
     print("%2d %-28s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[i] / tot, buf[i] / frames))
 if MODE == "fused":
     print("   %-28s %6.2f%%" % ("store state", 100.0 * buf[23] / tot if len(buf) > 23 else 0))
-
-if MODE == "staged":
-    groups = B * 2 * T / 4.0
-    ft = sum(buf[16:22])
-    print("k_fftA: stamped cycles per 4-frame group per WG: %.0f" % (ft / groups * 0 + ft / max(1, groups)))
-    for i, n in enumerate(FFTA):
-        print("%2d %-32s %6.2f%%  %8.0f cyc/group" % (i, n, 100.0 * buf[16 + i] / max(1, ft), buf[16 + i] / groups))
 
 if MODE == "staged":
     PIT = ["Q0 xf + coarse Syy -> LDS", "Q1 coarse xcorr", "Q2 coarse scan (survivors)", "Q3 fine xcorr",
