@@ -199,9 +199,10 @@ int fvad_engine_collect(fvad_engine *e, fvad_outputs *out, int *n_ticks);
  * float normalisation, as the reference's sf_read_float gives
  * AudioPipeline.pushSamples, src/AudioPipeline.zig:86-120; exact in f32), so
  * the outputs are bit-identical to a float submit of those samples.  Half the
- * host-to-device bytes; the conversion runs on the device, on the copy
- * stream.  The slot and the submit/collect rules are fvad_engine_input_slot's
- * and fvad_engine_submit's. */
+ * host-to-device bytes; the conversion runs on the device: staged engines
+ * with the denoiser read the 16-bit samples in k_prep3 itself, the others
+ * convert on the copy stream (k_pcm16).  The slot and the submit/collect
+ * rules are fvad_engine_input_slot's and fvad_engine_submit's. */
 int16_t *fvad_engine_input_slot_i16(fvad_engine *e);
 int fvad_engine_submit_i16(fvad_engine *e, const int16_t *pcm, int n_ticks, const int32_t *ticks_valid,
                            const int32_t *last_tick_samples);
