@@ -341,3 +341,46 @@ def test_bench_schedule_fp16_every_stream(fvad_mod, oracle_mod, model):
         wv, wb, n_seg, diffs = check_tolerance(ref, got, segs)
         print("fp16 bench schedule %s: max |dvad| %.3g, band rel %.3g, %d segments, moved bounds %s" % (
             schedule, wv, wb, n_seg, diffs))
+
+
+@pytest.mark.timeout(600)
+def test_bench_size_i16_equals_float(fvad_mod, model):
+    """The 16-bit ingest at the bench's size (2048 stereo streams, 50-tick
+    pushes, the host legs' engine with device VADMachines): k_prep3 reads the
+    16-bit samples itself (no float copy), and every output and segment equals
+    a float submit of k / 32768.0f, push for push, with three pushes in flight
+    on both engines; ragged ticks on the last push."""
+    B, P = 2048, 6
+    src = fvad_mod.synth_ticks(0, B, 2, P * T, 0, P * T)
+    q = np.clip(np.round(src * np.float32(32768.0)), -32768, 32767).astype(np.int16)
+    qf = q.astype(np.float32) / np.float32(32768.0)
+    valid = np.full(B, T, np.int32)
+    valid[::7] = 13
+    outs = []
+    for kind in ("float", "i16"):
+        eng = fvad_mod.Engine(model, B, 2, max_ticks=T, mode="staged")
+        eng.attach_vadm()
+        got, inflight = [], 0
+        for k in range(P):
+            if inflight == 3:
+                got.append(eng.collect())
+                inflight -= 1
+            tv = valid if k == P - 1 else None
+            if kind == "float":
+                eng.submit(qf[k * T:(k + 1) * T], ticks_valid=tv)
+            else:
+                eng.submit_i16(q[k * T:(k + 1) * T], ticks_valid=tv)
+            inflight += 1
+        while inflight:
+            got.append(eng.collect())
+            inflight -= 1
+        eng.sync()
+        outs.append((got, [eng.segments(s) for s in range(B)]))
+        del eng
+    (fa, fs), (ia, is_) = outs
+    for a, b in zip(fa, ia):
+        for key in ("vad", "ratio", "win_flag", "win_ratio", "win_vad"):
+            assert np.array_equal(a[key], b[key]), key
+        wf = a["win_flag"].astype(bool)
+        assert np.array_equal(a["band"][wf], b["band"][wf])
+    assert fs == is_
