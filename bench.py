@@ -60,8 +60,9 @@ def parse():
     ap.add_argument("--streams-per-gpu", type=int, default=2048)
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--ticks", type=int, default=50)
-    ap.add_argument("--mode", choices=("staged", "fused", "fp16"), default="staged",
-                    help="staged (bit-exact, default), fused (bit-exact), fp16 (configs[4]: GRU on MFMA, tolerance)")
+    ap.add_argument("--mode", choices=("staged", "fused", "fp16", "fp16_fused"), default="staged",
+                    help="staged (bit-exact, default), fused (bit-exact), fp16 (configs[4]: GRU on MFMA, tolerance), "
+                         "fp16_fused (configs[4]'s fused FFT -> feature -> GRU kernel, k_fused16; equal to fp16)")
     ap.add_argument("--no-vadm", action="store_true", help="staged: do not run the device VADMachine (k_vadm)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on this host (rank 0)")
     ap.add_argument("--cpu-streams", type=int, default=48,
@@ -504,6 +505,20 @@ def main():
                       "moved by one FFT-B window; tests/test_gpu_fullsize.py, test_gpu_fp16.py)",
             "note": "BASELINE configs[4]'s fp16-GRU variant on the same workload and clock (bench.py --mode fp16 "
                     "gives its full line)"}}
+        ef, elf, ktf = measure("fp16_fused")
+        del ef
+        ktf, _ = gather_kernel_tables(ktf, dist, torch, rank)
+        variants["fp16_fused"] = {
+            "value": round(aggregate_rate(B * Ch * T, world, args.steps, elf), 1), "unit": "frames/s",
+            "ms_per_step": round(1000.0 * elf / args.steps, 3),
+            "dtype": "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
+            "k_fused16_ms": round(ktf["kernels"].get("k_fused16", 0.0), 4),
+            "kernels_ms": {k: round(v, 4) for k, v in ktf["kernels"].items() if k != "k_pspecw"},
+            "parity": "every output identical to the fp16 variant's (tests/test_gpu_fused16.py), so the fp16 "
+                      "variant's tolerance parity holds",
+            "note": "BASELINE configs[4]'s fused FFT -> feature -> GRU kernel: the pitch-spectrum FFT, its "
+                    "features and the GRU stack in one kernel (k_fused16 in place of k_pspecw + k_gru16), same "
+                    "workload and clock (bench.py --mode fp16_fused gives its full line)"}
         if not args.no_vadm:
             # the same workload with the VADMachines in their long-running
             # regime: a stream past its first 180 s re-folds a long-term
@@ -541,14 +556,14 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32" if args.mode != "fp16" else "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
+        "vs_baseline": None, "dtype": "f32" if args.mode not in ("fp16", "fp16_fused") else "f32+f16 (GRU gates: f16 MFMA, f32 accumulate)",
         "data": "synthetic" + ("; REHEARSAL: %d ranks sharing GPU 0 over gloo (--rehearse-on-gpu0), not a "
                                "scaling figure" % world if args.rehearse_on_gpu0 else ""),
         "config": {"workload": "configs[4] per-GPU partition: %d synthetic 48 kHz streams x %d ch per GPU "
                                "(%d at %d GPU), %d ticks (480 samples/ch) per step, %d distinct resident pushes "
                                "(%.1f s of every stream) cycled, %s"
                                % (B, Ch, B * world, world, T, P, P * T * 0.01,
-                                  "fp16 GRU weights on MFMA (configs[4] variant, tolerance parity)" if args.mode == "fp16"
+                                  "fp16 GRU weights on MFMA (configs[4] variant, tolerance parity)" if args.mode in ("fp16", "fp16_fused")
                                   else "fp32 weights, bit-exact path"),
                    "streams_per_gpu": B, "channels": Ch, "ticks_per_step": T, "resident_pushes": P,
                    "fft_size": 2048,
@@ -671,7 +686,7 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks, groups=None):
     # v_mfma_f32_16x16x32_f16), the rest on the VALU
     f_alg = cost.flops_per_channel_frame(Ch)
     b_alg = cost.path_bytes_per_channel_frame(Ch)
-    f_gru = cost.phases(Ch)["GRU stack"] if args.mode == "fp16" else 0.0
+    f_gru = cost.phases(Ch)["GRU stack"] if args.mode in ("fp16", "fp16_fused") else 0.0
     fps_gpu = value / world
     ceil_hbm = HBM_PEAK_GBS * 1e9 / b_alg
     ceil_valu = 1.0 / ((f_alg - f_gru) / (FP32_PEAK_TFLOPS * 1e12) + f_gru / (F16_MFMA_PEAK_TFLOPS * 1e12))
@@ -687,7 +702,7 @@ def roofline(args, kt, value, world, ms_per_step, cost, ranks, groups=None):
                                     f_gru, F16_MFMA_PEAK_TFLOPS, f_alg - f_gru))
     if compute_bound:
         roof = ("FP32 VALU (157.3 TFLOP/s, FMA-counted; %s)" %
-                ("the GRU stack is on f16 MFMA, this kernel is not" if args.mode == "fp16" and dom != "k_gru16"
+                ("the GRU stack is on f16 MFMA, this kernel is not" if args.mode in ("fp16", "fp16_fused") and dom not in ("k_gru16", "k_fused16")
                  else "no MFMA instruction runs in this kernel"))
     else:
         roof = "HBM3E 8 TB/s"

@@ -42,6 +42,8 @@ int fail(int code, const std::string &msg) {
   g_err = msg;
   return code;
 }
+// the GRU stack on the matrix cores (configs[4]): split (k_pspecw + k_gru16) or fused (k_fused16)
+bool fp16_mode(int mode) { return mode == FVAD_MODE_FP16 || mode == FVAD_MODE_FP16_FUSED; }
 }  // namespace
 
 extern "C" const char *fvad_last_error(void) { return g_err.c_str(); }
@@ -323,7 +325,7 @@ int upload_model(fvad_engine *e, const fvad::HostModel &hm) {
     rc = dalloc(&e->d_rnn_img, img.size());
     if (rc) return rc;
     HIP_TRY(hipMemcpy(e->d_rnn_img, img.data(), img.size(), hipMemcpyHostToDevice));
-    if (e->cfg.mode == FVAD_MODE_FP16) {  // MFMA fragments of the same image (fvad_gru16.hip)
+    if (fp16_mode(e->cfg.mode)) {  // MFMA fragments of the same image (fvad_gru16.hip)
       std::vector<uint16_t> frags((size_t)fvad::gru16_frag_count() * 64 * 8);
       std::vector<float> bias(fvad::gru16_bias_rows());
       fvad::gru16_build(img.data(), frags.data(), bias.data());
@@ -470,7 +472,7 @@ extern "C" int fvad_engine_create(const fvad_engine_config *cfg, const fvad_mode
   }
   if (hi - lo + 1 > 256 && (c.mode == FVAD_MODE_FUSED || c.fft_size == 2048))
     return fail(FVAD_EINVAL, "reported bins must span <= 256");
-  if (c.mode != FVAD_MODE_STAGED && c.mode != FVAD_MODE_FUSED && c.mode != FVAD_MODE_FP16)
+  if (c.mode != FVAD_MODE_STAGED && c.mode != FVAD_MODE_FUSED && !fp16_mode(c.mode))
     return fail(FVAD_EINVAL, "unknown engine mode");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FVAD_EDEVICE, "no HIP device available");
@@ -799,6 +801,7 @@ int launch_staged(fvad_engine *e, int n_ticks, bool use_ticks, bool use_tail, bo
   a.rnn_img = e->d_rnn_img;
   a.gru16_frags = e->d_gru16;
   a.gru16_bias = e->d_gru16_bias;
+  a.fuse16 = e->cfg.mode == FVAD_MODE_FP16_FUSED;
   for (int m = 0; m < fvad::rnnimg::kMats; m++) a.rnn_act[m] = e->rnn_act[m];
   a.ys = e->d_ys;
   a.ring = e->d_ring;
@@ -1483,7 +1486,7 @@ extern "C" const char *fvad_engine_kernel_name(const fvad_engine *e, int i) {
   if (e && i == e->n_kernels + 1 && e->vadm.n > 0) return "k_vadm_par";
   if (!e || i < 0 || i >= e->n_kernels) return nullptr;
   if (e->cfg.mode == FVAD_MODE_FUSED) return i == 0 ? "k_prep" : "k_frame";
-  if (e->cfg.mode == FVAD_MODE_FP16 && i == 6) return "k_gru16";
+  if (fp16_mode(e->cfg.mode) && i == 6) return e->cfg.mode == FVAD_MODE_FP16_FUSED ? "k_fused16" : "k_gru16";
   if (e->olafb && i == 8) return "k_olafb";
   return fvad::staged_kernel_name(i);
 }

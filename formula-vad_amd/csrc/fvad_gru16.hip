@@ -32,10 +32,13 @@
 #pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fvad_device.h"
 #include "fvad_internal.h"
 #include "fvad_staged.h"
 #include "fvad_staged_dev.h"
+#include "fvad_wavedev.h"
 
 namespace fvad {
 namespace g16 {
@@ -166,8 +169,7 @@ constexpr int kFeatItems = kGS * (kBands + 7 + kCeps);
 constexpr int kDzrFrags = 12 * 7;  // denoise z|r: the largest matrix lives in LDS (84 KB)
 constexpr int kFr = 20;            // register fragment slots (see the wave plan)
 
-struct Lds {
-  alignas(16) half8 dzr[kDzrFrags][64];
+struct LdsCore {
   alignas(16) _Float16 op[kGS][kRowHalf];
   alignas(16) float sv[kGS][28], sn[kGS][52], sd[kGS][100];  // f32 GRU states (row pitch: distinct bank groups)
   alignas(16) float zv[kGS][28], zn[kGS][52], zd[kGS][100];  // update gates z of the frame
@@ -177,10 +179,21 @@ struct Lds {
   float ceps[kGS][kCeps * kBands];
   float dist[kGS][kCeps * kCeps];
   float lastg[kGS][kBands];
-  float pf[kGS][kPfW];
+  float pf[2][kGS][kPfW];  // raw features of frame f in pf[f & 1]
   int act[8][kGS];
   int memid[kGS], nfs[kGS];
   long long fbase[kGS];
+};
+// k_gru16: the denoise z|r fragments in LDS
+struct LdsSplit : LdsCore {
+  alignas(16) half8 dzr[kDzrFrags][64];
+};
+// k_fused16: the pitch-spectrum FFT's exchange regions (one per wave) and
+// tables take that LDS; the denoise z|r fragments are read from L2 instead
+constexpr int kFW = kGNT / 64;
+struct LdsFused : LdsCore {
+  alignas(16) float2 Rg[kFW][wfft::kSlots];
+  WaveTabs tb;
 };
 
 // A fragments of tile `tile` of matrix M into fr[F0 .. F0 + nkb(M))
@@ -196,8 +209,8 @@ __device__ __forceinline__ void load_frags(half8 (&fr)[kFr], const half8 *__rest
 // this lane's B chunk of K block kb of matrix M (frame versions in V): a
 // select over the four lane groups of compile-time chunks, plus the version
 // offset of the segment the chunk belongs to
-template <int M>
-__device__ __forceinline__ half8 b_operand(const Lds &L, int lane, int kb, const Ver &V) {
+template <int M, class LT>
+__device__ __forceinline__ half8 b_operand(const LT &L, int lane, int kb, const Ver &V) {
   const int s = lane & 15, g = lane >> 4;
   const char *row = reinterpret_cast<const char *>(L.op[s]);
   const int c0 = op_chunk(M, 4 * kb), c1 = op_chunk(M, 4 * kb + 1), c2 = op_chunk(M, 4 * kb + 2),
@@ -207,9 +220,12 @@ __device__ __forceinline__ half8 b_operand(const Lds &L, int lane, int kb, const
 }
 
 // acc = bias + sum over matrix M's K blocks of A . B for frame f (one MFMA
-// chain); A from registers fr[F0 + kb] (F0 >= 0) or from LDS (denoise z|r, F0 < 0)
-template <int F0, int M>
-__device__ __forceinline__ f4 mma_job(const half8 (&fr)[kFr], int tile, const Lds &L, int lane, int f) {
+// chain).  k_gru16: A from registers fr[F0 + kb] (F0 >= 0) or, for the
+// denoise z|r matrix (F0 < 0), from its LDS copy dz.  k_fused16 (LdsFused):
+// every A fragment from the global image dz (L2), the registers are the FFT's.
+template <int F0, int M, class LT>
+__device__ __forceinline__ f4 mma_job(const half8 (&fr)[kFr], int tile, const LT &L, const half8 *__restrict__ dz,
+                                      int lane, int f) {
   constexpr int NK = nkb(M);
   const Ver V = versions<M>(f);
   f4 acc = *reinterpret_cast<const f4 *>(&L.bias[bias_base(M) + tile * 16 + 4 * (lane >> 4)]);
@@ -217,10 +233,12 @@ __device__ __forceinline__ f4 mma_job(const half8 (&fr)[kFr], int tile, const Ld
   for (int kb = 0; kb < NK; kb++) {
     const half8 b = b_operand<M>(L, lane, kb, V);
     half8 w;
-    if constexpr (F0 >= 0)
+    if constexpr (std::is_same_v<LT, LdsFused>)
+      w = dz[(frag_base(M) + tile * NK + kb) * 64 + lane];
+    else if constexpr (F0 >= 0)
       w = fr[F0 + kb];
     else
-      w = L.dzr[tile * NK + kb][lane];
+      w = dz[(tile * NK + kb) * 64 + lane];
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(w, b, acc, 0, 0, 0);
   }
   return acc;
@@ -236,8 +254,8 @@ __device__ __forceinline__ void put_h4(_Float16 *dst, float a, float b, float c,
 }
 
 // z|r tile epilogue of a GRU with N neurons: z -> Z, r * state -> operand segment rs
-template <int N, int PZ, int PS>
-__device__ __forceinline__ void epi_zr(Lds &L, const f4 &acc, int tile, int lane, float (*Z)[PZ], float (*S)[PS],
+template <int N, int PZ, int PS, class LT>
+__device__ __forceinline__ void epi_zr(LT &L, const f4 &acc, int tile, int lane, float (*Z)[PZ], float (*S)[PS],
                                        int rs_seg) {
   const int s = lane & 15, r0 = tile * 16 + 4 * (lane >> 4);
   float v[4];
@@ -255,8 +273,8 @@ __device__ __forceinline__ void epi_zr(Lds &L, const f4 &acc, int tile, int lane
 // candidate tile epilogue: s' = z s + (1 - z) act(sum) for active streams, the
 // new state into operand half offset `dst` (the frame's version); an inactive
 // stream keeps its state and still fills the frame's version with it
-template <int N, int PZ, int PS>
-__device__ __forceinline__ void epi_h(Lds &L, const f4 &acc, int tile, int lane, int act, float (*Z)[PZ],
+template <int N, int PZ, int PS, class LT>
+__device__ __forceinline__ void epi_h(LT &L, const f4 &acc, int tile, int lane, int act, float (*Z)[PZ],
                                       float (*S)[PS], int dst, bool on) {
   const int s = lane & 15, r0 = tile * 16 + 4 * (lane >> 4);
   if (r0 >= N) return;
@@ -300,49 +318,74 @@ __device__ __forceinline__ void epi_h(Lds &L, const f4 &acc, int tile, int lane,
 // inactive).  8 puts 256 workgroups on the 256 CUs at 2048 streams instead of
 // 128: k_gru16 0.554 -> 0.530 ms (latency-bound supersteps, the same per
 // workgroup).
-template <int kSpw>
-__global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
+//
+// kFuse (k_fused16, BASELINE configs[4]'s "fused FFT -> feature -> GRU
+// kernel"): the pitch-spectrum FFT and its features 34..40 (k_pspecw's
+// per-frame work, pspec_frame) run inside the recurrence, wave W on stream W:
+// at superstep u it transforms frame u + 2 (at the end of phase B) and hands
+// the features to the GRU in LDS (pf) instead of through HBM; P, Ep and Exp
+// still go to HBM for k_synthw.  The FFT takes the registers the resident A
+// fragments had and its exchange regions the LDS of the denoise z|r copy, so
+// every fragment is read from L2 (192 KB per workgroup and frame step, the
+// same 192 KB for every workgroup of an XCD).
+template <int kSpw, bool kFuse>
+__device__ __forceinline__ void gru16_body(const StagedArgs &a) {
   static_assert(kSpw > 0 && kSpw <= kGS, "streams per k_gru16 workgroup");
+  static_assert(!kFuse || kSpw == kFW, "k_fused16: one stream per wave");
   constexpr int S = kGS;
-  __shared__ Lds L;
-  const int tid = threadIdx.x, lane = tid & 63, W = tid >> 6;
+  using LT = std::conditional_t<kFuse, LdsFused, LdsSplit>;
+  __shared__ LT L;
+  // (tid / lane / col: renewed opaquely every k_fused16 step, see the loop)
+  int tid = threadIdx.x, lane = tid & 63;
+  const int W = tid >> 6;
   const int sb = blockIdx.x * kSpw;
   auto sok = [&](int s) { return s < kSpw && sb + s < a.n_streams; };
   const int *ra = a.rnn_act;
   half8 fr[kFr];
   {
     const half8 *img = reinterpret_cast<const half8 *>(a.gru16_frags);
-    if (W < 2) {
-      load_frags<0, 0>(fr, img, W, lane);
-      load_frags<2, 6>(fr, img, W, lane);
-    } else if (W < 4) {
-      load_frags<0, 1>(fr, img, W - 2, lane);
-      load_frags<2, 6>(fr, img, W, lane);
-    } else if (W == 4) {
-      load_frags<0, 1>(fr, img, 2, lane);
-      load_frags<2, 3>(fr, img, 0, lane);
-      load_frags<7, 8>(fr, img, 0, lane);
-      load_frags<8, 6>(fr, img, 4, lane);
-      load_frags<15, 4>(fr, img, 1, lane);
-    } else if (W == 5) {
-      load_frags<0, 3>(fr, img, 1, lane);
-      load_frags<5, 3>(fr, img, 2, lane);
-      load_frags<10, 6>(fr, img, 5, lane);
-      load_frags<17, 7>(fr, img, 1, lane);
-    } else if (W == 6) {
-      load_frags<0, 3>(fr, img, 3, lane);
-      load_frags<5, 3>(fr, img, 4, lane);
-      load_frags<10, 4>(fr, img, 0, lane);
-      load_frags<15, 2>(fr, img, 1, lane);
-    } else {
-      load_frags<0, 3>(fr, img, 5, lane);
-      load_frags<5, 7>(fr, img, 0, lane);
-      load_frags<11, 4>(fr, img, 2, lane);
-      load_frags<16, 2>(fr, img, 0, lane);
+    if constexpr (!kFuse) {  // (k_fused16 reads every fragment from L2)
+      if (W < 2) {
+        load_frags<0, 0>(fr, img, W, lane);
+        load_frags<2, 6>(fr, img, W, lane);
+      } else if (W < 4) {
+        load_frags<0, 1>(fr, img, W - 2, lane);
+        load_frags<2, 6>(fr, img, W, lane);
+      } else if (W == 4) {
+        load_frags<0, 1>(fr, img, 2, lane);
+        load_frags<2, 3>(fr, img, 0, lane);
+        load_frags<7, 8>(fr, img, 0, lane);
+        load_frags<8, 6>(fr, img, 4, lane);
+        load_frags<15, 4>(fr, img, 1, lane);
+      } else if (W == 5) {
+        load_frags<0, 3>(fr, img, 1, lane);
+        load_frags<5, 3>(fr, img, 2, lane);
+        load_frags<10, 6>(fr, img, 5, lane);
+        load_frags<17, 7>(fr, img, 1, lane);
+      } else if (W == 6) {
+        load_frags<0, 3>(fr, img, 3, lane);
+        load_frags<5, 3>(fr, img, 4, lane);
+        load_frags<10, 4>(fr, img, 0, lane);
+        load_frags<15, 2>(fr, img, 1, lane);
+      } else {
+        load_frags<0, 3>(fr, img, 5, lane);
+        load_frags<5, 7>(fr, img, 0, lane);
+        load_frags<11, 4>(fr, img, 2, lane);
+        load_frags<16, 2>(fr, img, 0, lane);
+      }
     }
-    const half8 *dz = img + (size_t)frag_base(5) * 64;
-    for (int i = tid; i < kDzrFrags * 64; i += kGNT) (&L.dzr[0][0])[i] = dz[i];
+    if constexpr (!kFuse) {
+      const half8 *dzg = img + (size_t)frag_base(5) * 64;
+      for (int i = tid; i < kDzrFrags * 64; i += kGNT) (&L.dzr[0][0])[i] = dzg[i];
+    } else {
+      wave_tabs_load(L.tb, a.plan, tid, kGNT);
+    }
   }
+  const half8 *__restrict__ dz;
+  if constexpr (!kFuse)
+    dz = &L.dzr[0][0];
+  else
+    dz = reinterpret_cast<const half8 *>(a.gru16_frags);
   // ---- LDS: operand rows, states, tables
   for (int i = tid; i < S * kRowHalf; i += kGNT) (&L.op[0][0])[i] = (_Float16)0;
   for (int i = tid; i < kBiasRows; i += kGNT) L.bias[i] = a.gru16_bias[i];
@@ -389,8 +432,9 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
   for (int s = 0; s < S; s++) maxnf = max(maxnf, L.nfs[s]);
   // raw feature lane (s, i): i < 22 Lyf, 22..28 f34, 29 silence (the flag's
   // bits, nonzero = silent: no wait for the load where it is issued)
+  // (k_fused16: the f34 words come from pspec below, not from HBM)
   const int pfs = tid / kPfW, pfi = tid - pfs * kPfW;
-  const bool pf_lane = tid < S * kPfW;
+  const bool pf_lane = tid < S * kPfW && !(kFuse && pfi >= kBands && pfi < kBands + 7);
   auto fetch = [&](int v) -> float {
     if (!pf_lane || v >= L.nfs[pfs]) return 1.0f;  // past the end: treated as silent (inactive)
     const long long f = L.fbase[pfs] + v;
@@ -403,7 +447,7 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
   auto feat_c = [&](int f, int idx) {
     const int s = idx / (kBands + 7 + kCeps), i = idx - s * (kBands + 7 + kCeps);
     const bool valid = f < L.nfs[s];
-    const bool on = valid && __float_as_int(L.pf[s][kPfW - 1]) == 0;
+    const bool on = valid && __float_as_int(L.pf[f & 1][s][kPfW - 1]) == 0;
     if (i == 0) {
       L.act[f & 7][s] = on;
       if (valid && !on) a.vadf[L.fbase[s] + f] = 0;  // silent: X passes through, state untouched
@@ -411,7 +455,7 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     if (!on) return;
     _Float16 *feat = &L.op[s][seg_half(g16::kFeat, f % 5)];
     const int mi = L.memid[s];
-    const float *c0 = L.pf[s];
+    const float *c0 = L.pf[f & 1][s];
     if (i < kBands) {
       L.ceps[s][mi * kBands + i] = c0[i];
       if (i < 6) {
@@ -461,17 +505,31 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     if (mid == kCeps) mid = 0;
     L.memid[s] = mid;
   };
+  // k_fused16: wave W's pitch spectrum of stream W's frame v, features 34..40
+  // into pf[v & 1] (the caller's barrier publishes them)
+  auto pspec = [&](int v) {
+    if constexpr (kFuse) {
+      if (!sok(W) || v >= L.nfs[W]) return;
+      const int f = (int)(L.fbase[W] + v);
+      wfft::Tw tw;
+      wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
+      const float v34 = pspec_frame(a, f, a.pitch[f], L.tb, tw, L.Rg[W], lane);
+      if (lane < 7) L.pf[v & 1][W][kBands + lane] = v34;
+    }
+  };
   // prologue: features of frame 0, raw features of frame 1 staged
-  if (pf_lane) L.pf[pfs][pfi] = fetch(0);
+  if (pf_lane) L.pf[0][pfs][pfi] = fetch(0);
+  pspec(0);
+  pspec(1);
   __syncthreads();
   for (int idx = tid; idx < kFeatItems; idx += kGNT) feat_c(0, idx);
   __syncthreads();
   if (tid < S * kCeps && 0 < maxnf) feat_d(0);
   const float pf1 = fetch(1);
   __syncthreads();
-  if (pf_lane) L.pf[pfs][pfi] = pf1;
+  if (pf_lane) L.pf[1][pfs][pfi] = pf1;
   __syncthreads();
-  const int col = lane & 15;
+  int col = lane & 15;
   auto live = [&](int f) { return f >= 0 && f < maxnf; };
   auto den_out = [&](const f4 &acc, int tile) {  // denoise_output tile -> the frame's gains
     const int r0 = tile * 16 + 4 * (lane >> 4);
@@ -496,17 +554,27 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
 #endif
   for (int u = 0; u < maxnf + 4; u++) {
     const int fV = u - 1, fN = u - 2, fD = u - 3, fO = u - 4;
+    // k_fused16: the fragment loads stay in the step (hoisted out of the loop
+    // they would be the resident fragments again, in more registers than exist)
+    const half8 *__restrict__ dzs = kFuse ? dz + opaque0() : dz;
+    // ... and so do the lane-derived LDS and HBM addresses: as loop invariants
+    // they would all be held (or spilled) through the step's FFT
+    if constexpr (kFuse) {
+      asm volatile("" : "+v"(tid));
+      asm volatile("" : "+v"(lane));
+      asm volatile("" : "+v"(col));
+    }
     const float pf_next = fetch(u + 2);  // raw features of u + 2, staged at the end of phase B
     // ---- phase A: z|r gates of vad(u-1), noise(u-2), denoise(u-3); dense(u),
     // vad_out(u-2), den_out(u-4); features(u+1)
     WSTAMP_BEGIN();
     if (live(fD)) {
-      epi_zr<96>(L, mma_job<-1, 5>(fr, W, L, lane, fD), W, lane, L.zd, L.sd, kRsd);
-      if (W < 4) epi_zr<96>(L, mma_job<-1, 5>(fr, W + 8, L, lane, fD), W + 8, lane, L.zd, L.sd, kRsd);
+      epi_zr<96>(L, mma_job<-1, 5>(fr, W, L, dzs, lane, fD), W, lane, L.zd, L.sd, kRsd);
+      if (W < 4) epi_zr<96>(L, mma_job<-1, 5>(fr, W + 8, L, dzs, lane, fD), W + 8, lane, L.zd, L.sd, kRsd);
     }
     if (W < 2) {
       if (u < maxnf) {
-        const f4 acc = mma_job<0, 0>(fr, W, L, lane, u);
+        const f4 acc = mma_job<0, 0>(fr, W, L, dzs, lane, u);
         const int r0 = W * 16 + 4 * (lane >> 4);
         if (r0 < 24) {
           float v[4];
@@ -516,23 +584,23 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
         }
       }
     } else if (W < 4) {
-      if (live(fV)) epi_zr<24>(L, mma_job<0, 1>(fr, W - 2, L, lane, fV), W - 2, lane, L.zv, L.sv, kRsv);
+      if (live(fV)) epi_zr<24>(L, mma_job<0, 1>(fr, W - 2, L, dzs, lane, fV), W - 2, lane, L.zv, L.sv, kRsv);
     } else if (W == 4) {
-      if (live(fV)) epi_zr<24>(L, mma_job<0, 1>(fr, 2, L, lane, fV), 2, lane, L.zv, L.sv, kRsv);
+      if (live(fV)) epi_zr<24>(L, mma_job<0, 1>(fr, 2, L, dzs, lane, fV), 2, lane, L.zv, L.sv, kRsv);
       if (live(fN)) {
-        epi_zr<48>(L, mma_job<2, 3>(fr, 0, L, lane, fN), 0, lane, L.zn, L.sn, kRsn);
-        const f4 acc = mma_job<7, 8>(fr, 0, L, lane, fN);
+        epi_zr<48>(L, mma_job<2, 3>(fr, 0, L, dzs, lane, fN), 0, lane, L.zn, L.sn, kRsn);
+        const f4 acc = mma_job<7, 8>(fr, 0, L, dzs, lane, fN);
         if (lane < 16 && on_of(fN)) a.vadf[L.fbase[col] + fN] = activate(L.tt, ra[8], kWs * acc[0]);
       }
     } else if (W < 7) {
       if (live(fN)) {
-        epi_zr<48>(L, mma_job<0, 3>(fr, 2 * W - 9, L, lane, fN), 2 * W - 9, lane, L.zn, L.sn, kRsn);
-        epi_zr<48>(L, mma_job<5, 3>(fr, 2 * W - 8, L, lane, fN), 2 * W - 8, lane, L.zn, L.sn, kRsn);
+        epi_zr<48>(L, mma_job<0, 3>(fr, 2 * W - 9, L, dzs, lane, fN), 2 * W - 9, lane, L.zn, L.sn, kRsn);
+        epi_zr<48>(L, mma_job<5, 3>(fr, 2 * W - 8, L, dzs, lane, fN), 2 * W - 8, lane, L.zn, L.sn, kRsn);
       }
-      if (W == 5 && live(fO)) den_out(mma_job<17, 7>(fr, 1, L, lane, fO), 1);
+      if (W == 5 && live(fO)) den_out(mma_job<17, 7>(fr, 1, L, dzs, lane, fO), 1);
     } else {
-      if (live(fN)) epi_zr<48>(L, mma_job<0, 3>(fr, 5, L, lane, fN), 5, lane, L.zn, L.sn, kRsn);
-      if (live(fO)) den_out(mma_job<5, 7>(fr, 0, L, lane, fO), 0);
+      if (live(fN)) epi_zr<48>(L, mma_job<0, 3>(fr, 5, L, dzs, lane, fN), 5, lane, L.zn, L.sn, kRsn);
+      if (live(fO)) den_out(mma_job<5, 7>(fr, 0, L, dzs, lane, fO), 0);
     }
     if (u + 1 < maxnf) {
       // distance rows (the 22-term sums) one per lane on w0, w1; the rest on w2, w3, w6, w7
@@ -554,14 +622,14 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
         const int dst = seg_half(kSd, 0);
         const bool on = on_of(fD);
         if (W < 4)
-          epi_h<96>(L, mma_job<2, 6>(fr, W, L, lane, fD), W, lane, ra[6], L.zd, L.sd, dst, on);
+          epi_h<96>(L, mma_job<2, 6>(fr, W, L, dzs, lane, fD), W, lane, ra[6], L.zd, L.sd, dst, on);
         else if (W == 4)
-          epi_h<96>(L, mma_job<8, 6>(fr, 4, L, lane, fD), 4, lane, ra[6], L.zd, L.sd, dst, on);
+          epi_h<96>(L, mma_job<8, 6>(fr, 4, L, dzs, lane, fD), 4, lane, ra[6], L.zd, L.sd, dst, on);
         else
-          epi_h<96>(L, mma_job<10, 6>(fr, 5, L, lane, fD), 5, lane, ra[6], L.zd, L.sd, dst, on);
+          epi_h<96>(L, mma_job<10, 6>(fr, 5, L, dzs, lane, fD), 5, lane, ra[6], L.zd, L.sd, dst, on);
       }
       if (W == 4 && live(fN))
-        epi_h<48>(L, mma_job<15, 4>(fr, 1, L, lane, fN), 1, lane, ra[4], L.zn, L.sn, seg_half(kSn, fN & 1), on_of(fN));
+        epi_h<48>(L, mma_job<15, 4>(fr, 1, L, dzs, lane, fN), 1, lane, ra[4], L.zn, L.sn, seg_half(kSn, fN & 1), on_of(fN));
       if (W < 2 && u + 1 < maxnf) feat_d(u + 1);
       // gain smoothing g = max(g, .6*lastg) (denoise.c), frame u-4, on w2, w3, w5
       if ((W == 2 || W == 3 || W == 5) && live(fO)) {
@@ -581,16 +649,17 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     } else {
       if (live(fN)) {
         const int t = W == 6 ? 0 : 2;
-        const f4 acc = W == 6 ? mma_job<10, 4>(fr, 0, L, lane, fN) : mma_job<11, 4>(fr, 2, L, lane, fN);
+        const f4 acc = W == 6 ? mma_job<10, 4>(fr, 0, L, dzs, lane, fN) : mma_job<11, 4>(fr, 2, L, dzs, lane, fN);
         epi_h<48>(L, acc, t, lane, ra[4], L.zn, L.sn, seg_half(kSn, fN & 1), on_of(fN));
       }
       if (live(fV)) {
         const int t = W == 6 ? 1 : 0;
-        const f4 acc = W == 6 ? mma_job<15, 2>(fr, 1, L, lane, fV) : mma_job<16, 2>(fr, 0, L, lane, fV);
+        const f4 acc = W == 6 ? mma_job<15, 2>(fr, 1, L, dzs, lane, fV) : mma_job<16, 2>(fr, 0, L, dzs, lane, fV);
         epi_h<24>(L, acc, t, lane, ra[2], L.zv, L.sv, seg_half(kSv, fV % 3), on_of(fV));
       }
     }
-    if (pf_lane) L.pf[pfs][pfi] = pf_next;  // read by the next phase A only
+    pspec(u + 2);
+    if (pf_lane) L.pf[u & 1][pfs][pfi] = pf_next;  // frame u + 2: read from the next phase A on
     WSTAMP_END(1);
     lds_sync();
     RSTAMP(1);
@@ -629,8 +698,14 @@ __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) {
     reinterpret_cast<int *>(a.state)[(size_t)(sb + tid) * st::kWords + st::kMemId] = L.memid[tid];
 }
 
+__global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) { gru16_body<8, false>(a); }
+__global__ void __launch_bounds__(kGNT) k_fused16(StagedArgs a) { gru16_body<8, true>(a); }
+
 hipError_t launch_gru16(const StagedArgs &a, hipStream_t stream) {
-  hipLaunchKernelGGL(k_gru16<8>, dim3((a.n_streams + 7) / 8), dim3(kGNT), 0, stream, a);
+  if (a.fuse16)
+    hipLaunchKernelGGL(k_fused16, dim3((a.n_streams + 7) / 8), dim3(kGNT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(k_gru16, dim3((a.n_streams + 7) / 8), dim3(kGNT), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -109,6 +109,7 @@ struct StagedArgs {
   const int8_t *rnn_img;   // rnnimg image (fvad_internal.h), device
   const void *gru16_frags;   // FVAD_MODE_FP16: MFMA A fragments (fvad_gru16.hip), null otherwise
   const float *gru16_bias;   //   and the gate biases per tile row
+  int fuse16;                // FVAD_MODE_FP16_FUSED: the pitch spectrum runs inside the GRU kernel (k_fused16)
   int rnn_act[rnnimg::kMats];  // activation of each image matrix
   float *ys;               // [f][960] windowed synthesis output
   float *ring;             // [s][c][ring_len]
@@ -186,7 +187,8 @@ long long fftb_work_stride(int nfft_b, int bin_lo_all, int bin_hi_all, int gener
 bool fftb_generic(int nc);  // kf_factor(nc) has a radix > 5
 // 16-bit ingest: dst[i] = src[i] / 32768.0f (exact), n a multiple of 8
 hipError_t launch_pcm16(const int16_t *src, float *dst, size_t n, hipStream_t stream);
-// fp16 / MFMA recurrence (fvad_gru16.hip), run in k_rnn3's place when a.gru16_frags is set
+// fp16 / MFMA recurrence (fvad_gru16.hip), run in k_rnn3's place when a.gru16_frags is set;
+// with a.fuse16 it is k_fused16, which also does k_pspecw's work
 hipError_t launch_gru16(const StagedArgs &a, hipStream_t stream);
 int gru16_frag_count();   // A fragments of 64 lanes x 8 f16
 int gru16_bias_rows();

@@ -2468,7 +2468,8 @@ hipError_t launch_staged(const StagedArgs &a, int n_cu, hipStream_t stream, hipE
   FVAD_KERNEL_TRY(k_select, dim3((a.n_streams + kSelStreams - 1) / kSelStreams), dim3(64), 0, stream, a);
   REC(6);
   REC(7);
-  FVAD_LAUNCH_TRY(launch_wave(kWavePspec, a, n_cu, stream));
+  if (!(a.gru16_frags && a.fuse16))  // FVAD_MODE_FP16_FUSED: k_fused16 computes the pitch spectra
+    FVAD_LAUNCH_TRY(launch_wave(kWavePspec, a, n_cu, stream));
   REC(8);
   if (a.gru16_frags)  // FVAD_MODE_FP16: the GRU stack on the matrix cores (configs[4])
     FVAD_LAUNCH_TRY(launch_gru16(a, stream));

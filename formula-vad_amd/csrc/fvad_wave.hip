@@ -13,6 +13,7 @@
 #include "fvad_internal.h"
 #include "fvad_staged.h"
 #include "fvad_staged_dev.h"
+#include "fvad_wavedev.h"
 #include "fvad_wfft.h"
 
 namespace fvad {
@@ -59,57 +60,13 @@ __device__ __forceinline__ int lane_val(int v, int l) { return __builtin_amdgcn_
 // the frames before)
 __device__ __forceinline__ void settle(int v) { asm volatile("" ::"v"(v)); }
 
-// A per-iteration zero the compiler cannot see through: table reads indexed
-// with it stay inside the frame loop instead of being hoisted into registers
-// for the whole kernel (which would cost occupancy).
-__device__ __forceinline__ int opaque0() {
-  int z = 0;
-  asm volatile("" : "+s"(z));
-  return z;
-}
-
-struct WaveTabs {
-  BandTab T;
-  wfft::TwTab tw;
-  float hw[kFrame];
-};
-__device__ __forceinline__ void wave_tabs_load(WaveTabs &w, const Plan *__restrict__ P, int tid) {
-  bandtab_load(w.T, P, tid, 64 * kWNW);
-  wfft::load_twtab(w.tw, reinterpret_cast<const float2 *>(P->tw960), tid, 64 * kWNW);
-  for (int i = tid; i < kFrame; i += 64 * kWNW) w.hw[i] = P->half_window[i];
-}
-
-// A frame's raw window samples.  (Loading them one frame ahead saved k_pspecw
-// 0.07 ms at 3 waves per SIMD; its 16 registers kept it there.  Without the
-// prefetch it fits 128 VGPRs and runs 4 waves per SIMD, which hide that
-// latency better: 0.531 -> 0.497 ms.)
-struct WinRaw {
-  float x[16];
-};
-__device__ __forceinline__ void win_load(WinRaw &w, const float *__restrict__ pb, int lane) {
-#pragma unroll
-  for (int k = 0; k < 16; k++) w.x[k] = lane < 60 ? pb[wfft::in_index(lane, k)] : 0.0f;
-}
-// layout-A input of a 960-sample analysis window from its prefetched samples
-// (x * w / 960, imag 0)
-__device__ __forceinline__ void win_apply(const WinRaw &w, const float *hw, int lane, float2 (&v)[16]) {
-  hw += opaque0();
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int i = wfft::in_index(lane, k);
-    float val = w.x[k];
-    val *= lane < 60 ? win960(hw, i) : 0.0f;
-    v[k] = make_float2(kScale960 * val, kScale960 * 0.0f);
-  }
-}
-
 __global__ void __launch_bounds__(64 * kWNW, kWOcc) k_fftAw(StagedArgs a) {
   __shared__ __attribute__((aligned(16))) float2 Rg[kWNW][wfft::kSlots];
   __shared__ WaveTabs tb;
   __shared__ float exb[kWNW][kWB][kBands + 2], lyb[kWNW][kWB][kBands + 2];
   __shared__ int silb[kWNW][kWB];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  wave_tabs_load(tb, a.plan, tid);
+  wave_tabs_load(tb, a.plan, tid, 64 * kWNW);
   wfft::Tw tw;
   wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
   __syncthreads();
@@ -215,15 +172,11 @@ __global__ void __launch_bounds__(64 * kPNW, 4) k_pspecw(StagedArgs a) {
   __shared__ __attribute__((aligned(16))) float2 Rg[kPNW][wfft::kSlots];
   __shared__ WaveTabs tb;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  bandtab_load(tb.T, a.plan, tid, 64 * kPNW);
-  wfft::load_twtab(tb.tw, reinterpret_cast<const float2 *>(a.plan->tw960), tid, 64 * kPNW);
-  for (int i = tid; i < kFrame; i += 64 * kPNW) tb.hw[i] = a.plan->half_window[i];
+  wave_tabs_load(tb, a.plan, tid, 64 * kPNW);
   wfft::Tw tw;
   wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
   __syncthreads();
-  const BandTab &T = tb.T;
   float2 *R = Rg[wv];
-  float *tr = reinterpret_cast<float *>(R);
   const long long nb = ((long long)a.n_streams * a.V + kWB - 1) / kWB;
   for (long long g = wave_first<kPNW>(a, kWavePspec, kWorkPspec, lane); g < nb;
        g = wave_next<kPNW>(a, kWavePspec, kWorkPspec, lane, g)) {
@@ -231,67 +184,13 @@ __global__ void __launch_bounds__(64 * kPNW, 4) k_pspecw(StagedArgs a) {
     const int fl = batch_frames(a, g, lane);
     const int pl = fl >= 0 ? a.pitch[fl] : 0;
     settle(pl);
-    auto pwin = [&](int f, int fr) { return frame_pb(a, f) + (kPitchBuf - kWin - lane_val(pl, fr)); };
-    auto frame = [&](int fr) __attribute__((always_inline)) {
-      const int f = lane_val(fl, fr);
-      if (f < 0) return;
-      WinRaw cur;
-      win_load(cur, pwin(f, fr), lane);
-      const int pit = lane_val(pl, fr);
-      // X of bins < 400 (Exp terms) and the band's Ex, issued before the
-      // transform (Ex loaded after the P stores waited for them)
-      float2 xr[7];
-      const float2 *X = a.X + (size_t)f * kFreq;
-#pragma unroll
-      // (unconditional loads, lanes past the bins read bin 480 and are never
-      // used: a masked load's block would take its consumers, and their wait,
-      // right after it)
-      for (int r = 0; r < 7; r++) xr[r] = X[min(64 * r + lane, kFreq - 1)];
-      const float exl = a.Ex[(size_t)f * kBands + min(lane, kBands - 1)];
-      float2 v[16];
-      win_apply(cur, tb.hw, lane, v);
-      wfft::run(v, tw, tb.tw, R, lane);
-      float2 *P = a.P + (size_t)f * kFreq;
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-        if (64 * r + lane < kFreq) P[64 * r + lane] = v[r];
-#pragma unroll
-      for (int r = 0; r < 7; r++) {
-        const int n = 64 * r + lane;
-        if (n < 400) {
-          band_terms(v[r], v[r], T, n, tr[n], tr[400 + n]);
-          band_terms(xr[r], v[r], T, n, tr[800 + n], tr[1200 + n]);
-        }
-      }
-      wfft::wsync();
-      // Ep chains on lanes 0..21, Exp chains on lanes 32..53
-      const int h = lane >> 5, b = lane & 31;
-      float cv = 0;
-      if (b < kBands) cv = band_chain(tr + 800 * h, tr + 800 * h + 400, T, b);
-      const float expv = __shfl(cv, lane + 32);
-      float e = 0;
-      if (lane < kBands) {
-        const size_t o = (size_t)f * kBands + lane;
-        e = (float)((double)expv / sqrt(.001 + (double)(exl * cv)));
-        a.Ep[o] = cv;
-        a.Exp[o] = e;
-      }
-      float sum = 0;
-#pragma unroll
-      for (int j = 0; j < kBands; j++)
-        sum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), j)) * T.dct[j * kBands + (lane < 6 ? lane : 0)];
-      if (lane < 6) {
-        float val = (float)(sum * sqrt(2. / 22));
-        if (lane == 0) val = (float)(val - 1.3);
-        if (lane == 1) val = (float)(val - 0.9);
-        a.f34[(size_t)f * 8 + lane] = val;
-      } else if (lane == 6) {
-        a.f34[(size_t)f * 8 + 6] = (float)(.01 * (pit - 300));
-      }
-      wfft::wsync();
-    };
 #pragma unroll 1
-    for (int fr = 0; fr < kWB; fr++) frame(fr);
+    for (int fr = 0; fr < kWB; fr++) {
+      const int f = lane_val(fl, fr);
+      if (f < 0) continue;
+      const float v34 = pspec_frame(a, f, lane_val(pl, fr), tb, tw, R, lane);
+      if (lane < 7) a.f34[(size_t)f * 8 + lane] = v34;
+    }
   }
 }
 

@@ -38,7 +38,7 @@ class EngineConfig(C.Structure):
                 ("mode", C.c_int), ("use_denoiser", C.c_int)]
 
 
-MODE_STAGED, MODE_FUSED, MODE_FP16 = 0, 1, 2
+MODE_STAGED, MODE_FUSED, MODE_FP16, MODE_FP16_FUSED = 0, 1, 2, 3
 MAX_TIMES = 16
 
 
@@ -314,7 +314,7 @@ class Engine:
             cfg.band_lo[i] = lo
             cfg.band_hi[i] = hi
         cfg.want_denoised = int(want_denoised)
-        cfg.mode = {"staged": MODE_STAGED, "fused": MODE_FUSED, "fp16": MODE_FP16}[mode]
+        cfg.mode = {"staged": MODE_STAGED, "fused": MODE_FUSED, "fp16": MODE_FP16, "fp16_fused": MODE_FP16_FUSED}[mode]
         cfg.use_denoiser = int(use_denoiser)
         self.cfg = cfg
         self.model = model

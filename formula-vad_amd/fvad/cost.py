@@ -178,6 +178,9 @@ def staged_kernels(n_channels=2, fft_size=2048):
     k["k_olafb"] = (960 + p["re-block + FFT B share"], 960 * 4 + 4 * 4.0 / C + 2 * 8192.0 / 50)
     k["k_vadm_par"] = k["k_vadm_hbm"]  # the same machine, window-parallel (the push flushed at a sync point)
     k["k_gru16"] = k["k_rnn3"]  # FVAD_MODE_FP16: the same recurrence, gate sums on MFMA
+    # FVAD_MODE_FP16_FUSED: k_pspecw's work and k_gru16's in one kernel; features
+    # 34..40 pass in LDS, so the f34 row (8 floats) is neither written nor read
+    k["k_fused16"] = (k["k_pspecw"][0] + k["k_rnn3"][0], k["k_pspecw"][1] + k["k_rnn3"][1] - 2 * 8 * 4)
     return {n: {"flops": f, "bytes": b} for n, (f, b) in k.items()}
 
 

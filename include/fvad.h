@@ -112,7 +112,7 @@ typedef struct {
   int band_lo[FVAD_MAX_BANDS]; /* inclusive FFT-B bin ranges (FFT.freqToBin) */
   int band_hi[FVAD_MAX_BANDS];
   int want_denoised;    /* keep denoised PCM (VAD.zig temp_denoiser_segment) */
-  int mode;             /* FVAD_MODE_STAGED (default), FVAD_MODE_FUSED or FVAD_MODE_FP16 */
+  int mode;             /* FVAD_MODE_STAGED (default), FVAD_MODE_FUSED, FVAD_MODE_FP16 or FVAD_MODE_FP16_FUSED */
   int use_denoiser;     /* VAD.Config.use_denoiser (default 1).  0: fft_size frames of raw input go
                          * straight to FFT B (VAD.zig:206-212,239-249); per-tick vad / ratio are -1,
                          * the window ratio is preAnalyzeSegment's over the frame, window vad -1 */
@@ -125,10 +125,14 @@ typedef struct {
  * and fused give identical results (bit-exact with the CPU reference).
  * fp16: BASELINE configs[4] -- the staged pipeline with the GRU stack on the
  * matrix cores (int8 weights as f16, f16 inputs, f32 accumulation): within
- * the stated tolerance (vad |d| <= 2e-2), not bit-exact. */
+ * the stated tolerance (vad |d| <= 2e-2), not bit-exact.
+ * fp16_fused: configs[4]'s fused FFT -> feature -> GRU kernel -- fp16 with
+ * the pitch-spectrum FFT and its features computed inside the GRU kernel
+ * (k_fused16 replaces k_pspecw + k_gru16); results identical to fp16's. */
 #define FVAD_MODE_STAGED 0
 #define FVAD_MODE_FUSED 1
 #define FVAD_MODE_FP16 2
+#define FVAD_MODE_FP16_FUSED 3
 #define FVAD_MAX_TIMES 16
 
 void fvad_engine_config_default(fvad_engine_config *cfg, int n_streams, int n_channels);

@@ -24,9 +24,10 @@ if MODE == "staged":  # k_rnn3 (the only staged recurrence kernel since r2)
              "  P1 role: gains", "", "  P2 role: denoise h", "  P2 role: noise h", "  P2 role: vad h",
              "  P2 role: dense", "  P2 role: denoise_output", "  P2 role: vad_output", "  P2 role: features"]
     ROLES = True
-if MODE == "fp16":  # k_gru16 supersteps (fvad_gru16.hip), stamps[48..49]
+if MODE in ("fp16", "fp16_fused"):  # k_gru16 / k_fused16 supersteps (fvad_gru16.hip), stamps[48..49]
     GRU = ["A  z|r gates vad(u-1) noise(u-2) denoise(u-3), dense(u), outputs, features(u+1)",
-           "B  candidates vad(u-1) noise(u-2) denoise(u-3), gains(u-4), spectral var(u+1)"]
+           "B  candidates vad(u-1) noise(u-2) denoise(u-3), gains(u-4), spectral var(u+1)"
+           + (", pitch spectrum(u+2)" if MODE == "fp16_fused" else "")]
 L = fvad.lib()
 L.fvad_engine_stamps.restype = C.c_int
 L.fvad_engine_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
@@ -40,10 +41,11 @@ e.run_resident(T)
 e.sync()
 buf = (C.c_ulonglong * 64)()
 assert L.fvad_engine_stamps(e.h, buf, 64) == 0
-if MODE == "fp16":
-    frames = (B // 16) * 2 * T
+if MODE in ("fp16", "fp16_fused"):
+    frames = (B // 8) * 2 * T  # one workgroup per 8 streams (kSpw), stamps from thread 0
     gt = sum(buf[48:48 + len(GRU)])
-    print("k_gru16: stamped cycles per frame step per WG: %.0f" % (gt / frames))
+    print("k_gru16" if MODE == "fp16" else "k_fused16", end="")
+    print(": stamped cycles per frame step per WG: %.0f" % (gt / frames))
     for i, n in enumerate(GRU):
         print("%2d %-44s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[48 + i] / max(1, gt), buf[48 + i] / frames))
     print("per-wave busy cycles per frame step (phase A | phase B):")
