@@ -190,7 +190,8 @@ struct LdsSplit : LdsCore {
 };
 // k_fused16: the pitch-spectrum FFT's exchange regions (one per wave) and
 // tables take that LDS; the denoise z|r fragments are read from L2 instead
-constexpr int kFW = kGNT / 64;
+constexpr int kFW = 8;             // k_fused16: pitch-spectrum waves (one per stream), after the 8 GRU waves
+constexpr int kFNT = kGNT + 64 * kFW;
 struct LdsFused : LdsCore {
   alignas(16) float2 Rg[kFW][wfft::kSlots];
   WaveTabs tb;
@@ -321,23 +322,27 @@ __device__ __forceinline__ void epi_h(LT &L, const f4 &acc, int tile, int lane, 
 //
 // kFuse (k_fused16, BASELINE configs[4]'s "fused FFT -> feature -> GRU
 // kernel"): the pitch-spectrum FFT and its features 34..40 (k_pspecw's
-// per-frame work, pspec_frame) run inside the recurrence, wave W on stream W:
-// at superstep u it transforms frame u + 2 (at the end of phase B) and hands
-// the features to the GRU in LDS (pf) instead of through HBM; P, Ep and Exp
-// still go to HBM for k_synthw.  The FFT takes the registers the resident A
-// fragments had and its exchange regions the LDS of the denoise z|r copy, so
-// every fragment is read from L2 (192 KB per workgroup and frame step, the
-// same 192 KB for every workgroup of an XCD).
+// per-frame work, fvad_wavedev.h) run inside the recurrence on 8 more waves,
+// wave 8 + j on stream j: at superstep u it transforms frame u + 2 in phase A
+// (pspec_transform) and finishes its features in phase B (pspec_features),
+// handing them to the GRU waves in LDS (pf) instead of through HBM; P, Ep and
+// Exp still go to HBM for k_synthw.  16 waves = 4 per SIMD leave 128 VGPRs a
+// wave, so the GRU waves hold no A fragments (every fragment is read from L2
+// each frame step: 192 KB per workgroup, the same 192 KB for every workgroup
+// of an XCD), and the exchange regions take the LDS of the denoise z|r copy.
 template <int kSpw, bool kFuse>
 __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
   static_assert(kSpw > 0 && kSpw <= kGS, "streams per k_gru16 workgroup");
-  static_assert(!kFuse || kSpw == kFW, "k_fused16: one stream per wave");
+  static_assert(!kFuse || kSpw == kFW, "k_fused16: one pitch-spectrum wave per stream");
   constexpr int S = kGS;
+  constexpr int NT = kFuse ? kFNT : kGNT;  // threads of the workgroup
   using LT = std::conditional_t<kFuse, LdsFused, LdsSplit>;
   __shared__ LT L;
   // (tid / lane / col: renewed opaquely every k_fused16 step, see the loop)
   int tid = threadIdx.x, lane = tid & 63;
-  const int W = tid >> 6;
+  // k_fused16: the wave index as a scalar, so the wave plan's tile offsets
+  // derived from it stay out of the (128) VGPRs
+  const int W = kFuse ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const int sb = blockIdx.x * kSpw;
   auto sok = [&](int s) { return s < kSpw && sb + s < a.n_streams; };
   const int *ra = a.rnn_act;
@@ -378,7 +383,7 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
       const half8 *dzg = img + (size_t)frag_base(5) * 64;
       for (int i = tid; i < kDzrFrags * 64; i += kGNT) (&L.dzr[0][0])[i] = dzg[i];
     } else {
-      wave_tabs_load(L.tb, a.plan, tid, kGNT);
+      wave_tabs_load(L.tb, a.plan, tid, NT);
     }
   }
   const half8 *__restrict__ dz;
@@ -387,18 +392,18 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
   else
     dz = reinterpret_cast<const half8 *>(a.gru16_frags);
   // ---- LDS: operand rows, states, tables
-  for (int i = tid; i < S * kRowHalf; i += kGNT) (&L.op[0][0])[i] = (_Float16)0;
-  for (int i = tid; i < kBiasRows; i += kGNT) L.bias[i] = a.gru16_bias[i];
-  for (int i = tid; i < 201; i += kGNT) L.tt[i] = a.plan->tansig[i];
-  for (int idx = tid; idx < S * kCeps * kBands; idx += kGNT) {
+  for (int i = tid; i < S * kRowHalf; i += NT) (&L.op[0][0])[i] = (_Float16)0;
+  for (int i = tid; i < kBiasRows; i += NT) L.bias[i] = a.gru16_bias[i];
+  for (int i = tid; i < 201; i += NT) L.tt[i] = a.plan->tansig[i];
+  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
     const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
     L.ceps[s][i] = sok(s) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] : 0.0f;
   }
-  for (int idx = tid; idx < S * kCeps * kCeps; idx += kGNT) {
+  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
     const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
     L.dist[s][i] = sok(s) ? a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] : 0.0f;
   }
-  for (int idx = tid; idx < S * kBands; idx += kGNT) {
+  for (int idx = tid; idx < S * kBands; idx += NT) {
     const int s = idx / kBands, i = idx - s * kBands;
     L.lastg[s][i] = sok(s) ? a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] : 0.0f;
   }
@@ -412,7 +417,7 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
   }
   __syncthreads();
   // states before frame 0 = the versions of frame -1 (vad 2, noise 1)
-  for (int idx = tid; idx < S * 96; idx += kGNT) {
+  for (int idx = tid; idx < S * 96; idx += NT) {
     const int s = idx / 96, i = idx - s * 96;
     const bool ok = sok(s);
     const float *stp = a.state + (size_t)(sb + s) * st::kWords;
@@ -505,24 +510,29 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
     if (mid == kCeps) mid = 0;
     L.memid[s] = mid;
   };
-  // k_fused16: wave W's pitch spectrum of stream W's frame v, features 34..40
-  // into pf[v & 1] (the caller's barrier publishes them)
-  auto pspec = [&](int v) {
-    if constexpr (kFuse) {
-      if (!sok(W) || v >= L.nfs[W]) return;
-      const int f = (int)(L.fbase[W] + v);
-      wfft::Tw tw;
-      wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
-      const float v34 = pspec_frame(a, f, a.pitch[f], L.tb, tw, L.Rg[W], lane);
-      if (lane < 7) L.pf[v & 1][W][kBands + lane] = v34;
-    }
-  };
+  // k_fused16: waves kGNT / 64 + j are stream j's pitch-spectrum waves (their
+  // loop is below the GRU's); pframe(v): stream j's frame v, or -1
+  const bool fft_wave = kFuse && W >= kGNT / 64;
+  const int fj = W - kGNT / 64;
+  auto pframe = [&](int v) { return (kFuse && sok(fj) && v < L.nfs[fj]) ? (int)(L.fbase[fj] + v) : -1; };
   // prologue: features of frame 0, raw features of frame 1 staged
   if (pf_lane) L.pf[0][pfs][pfi] = fetch(0);
-  pspec(0);
-  pspec(1);
+  if constexpr (kFuse) {
+#ifndef FVAD_DIAG_NO_PSPEC  // (diagnostic build: k_fused16's GRU alone, wrong features)
+    if (fft_wave) {
+      wfft::Tw tw;
+      wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960), lane);
+      for (int v = 0; v < 2; v++) {
+        const int f = pframe(v);
+        if (f < 0) continue;
+        const float v34 = pspec_frame(a, f, a.pitch[f], L.tb, tw, L.Rg[fj], lane);
+        if (lane < 7) L.pf[v & 1][fj][kBands + lane] = v34;
+      }
+    }
+#endif
+  }
   __syncthreads();
-  for (int idx = tid; idx < kFeatItems; idx += kGNT) feat_c(0, idx);
+  for (int idx = tid; idx < kFeatItems; idx += NT) feat_c(0, idx);
   __syncthreads();
   if (tid < S * kCeps && 0 < maxnf) feat_d(0);
   const float pf1 = fetch(1);
@@ -552,13 +562,57 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
   do {                \
   } while (0)
 #endif
+  if (fft_wave) {
+    // k_fused16's pitch-spectrum waves, in step with the GRU waves' barriers
+    // (two per superstep): at superstep u the transform of frame u + 2 in
+    // phase A, its features in phase B; a frame's pitch loads one superstep
+    // ahead.  (Its window, X and Ex loaded a phase ahead as well measured
+    // slower: 1.65 vs 1.39 ms.)
+    if constexpr (kFuse) {
+      int f2 = pframe(2), f3 = pframe(3);
+      int pit2 = f2 >= 0 ? a.pitch[f2] : 0, pit3 = f3 >= 0 ? a.pitch[f3] : 0;
+#ifdef FVAD_DIAG_NO_PSPEC
+      f2 = f3 = -1;
+#endif
+      for (int u = 0; u < maxnf + 4; u++) {
+        const int f = f2, pit = pit2;  // frame u + 2
+        asm volatile("" : "+v"(lane));  // lane-derived table addresses: per step, not held (as the GRU loop)
+        WSTAMP_BEGIN();
+        float exl = 0.0f;
+        if (f >= 0) {
+          PspecIn in;
+          pspec_load(in, a, f, pit, lane);
+          wfft::Tw tw;
+          wfft::load_tw(tw, reinterpret_cast<const float2 *>(a.plan->tw960 + opaque0()), lane);
+          pspec_transform(a, f, in, L.tb, tw, L.Rg[fj], lane);
+          exl = in.exl;
+        }
+        f2 = f3;
+        pit2 = pit3;
+        f3 = pframe(u + 4);
+#ifdef FVAD_DIAG_NO_PSPEC
+        f3 = -1;
+#endif
+        pit3 = f3 >= 0 ? a.pitch[f3] : 0;
+        WSTAMP_END(0);
+        lds_sync();
+        WSTAMP_BEGIN();
+        if (f >= 0) {
+          const float v34 = pspec_features(a, f, pit, L.tb, L.Rg[fj], lane, exl);
+          if (lane < 7) L.pf[u & 1][fj][kBands + lane] = v34;
+        }
+        WSTAMP_END(1);
+        lds_sync();
+      }
+    }
+  } else {
   for (int u = 0; u < maxnf + 4; u++) {
     const int fV = u - 1, fN = u - 2, fD = u - 3, fO = u - 4;
     // k_fused16: the fragment loads stay in the step (hoisted out of the loop
     // they would be the resident fragments again, in more registers than exist)
     const half8 *__restrict__ dzs = kFuse ? dz + opaque0() : dz;
     // ... and so do the lane-derived LDS and HBM addresses: as loop invariants
-    // they would all be held (or spilled) through the step's FFT
+    // they would all be held (or spilled) in the 128 VGPRs
     if constexpr (kFuse) {
       asm volatile("" : "+v"(tid));
       asm volatile("" : "+v"(lane));
@@ -658,35 +712,35 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
         epi_h<24>(L, acc, t, lane, ra[2], L.zv, L.sv, seg_half(kSv, fV % 3), on_of(fV));
       }
     }
-    pspec(u + 2);
     if (pf_lane) L.pf[u & 1][pfs][pfi] = pf_next;  // frame u + 2: read from the next phase A on
     WSTAMP_END(1);
     lds_sync();
     RSTAMP(1);
   }
+  }  // GRU waves
 #ifdef FVAD_STAMPS
-  if (lane == 0 && a.stamps) {
-    atomicAdd(&a.stamps[W], wacc[0]);
-    atomicAdd(&a.stamps[8 + W], wacc[1]);
+  if (lane == 0 && a.stamps) {  // k_fused16's pitch-spectrum waves: [16..23] A, [24..31] B
+    atomicAdd(&a.stamps[W < 8 ? W : W + 8], wacc[0]);
+    atomicAdd(&a.stamps[W < 8 ? 8 + W : W + 16], wacc[1]);
   }
 #endif
 #undef WSTAMP_BEGIN
 #undef WSTAMP_END
   STAMP_FLUSH(48, 2);
   // ---- state write-back (streams that ran at least one frame)
-  for (int idx = tid; idx < S * kCeps * kBands; idx += kGNT) {
+  for (int idx = tid; idx < S * kCeps * kBands; idx += NT) {
     const int s = idx / (kCeps * kBands), i = idx - s * (kCeps * kBands);
     if (sok(s) && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsMem + i] = L.ceps[s][i];
   }
-  for (int idx = tid; idx < S * kCeps * kCeps; idx += kGNT) {
+  for (int idx = tid; idx < S * kCeps * kCeps; idx += NT) {
     const int s = idx / (kCeps * kCeps), i = idx - s * (kCeps * kCeps);
     if (sok(s) && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kCepsDist + i] = L.dist[s][i];
   }
-  for (int idx = tid; idx < S * kBands; idx += kGNT) {
+  for (int idx = tid; idx < S * kBands; idx += NT) {
     const int s = idx / kBands, i = idx - s * kBands;
     if (sok(s) && L.nfs[s] > 0) a.state[(size_t)(sb + s) * st::kWords + st::kLastG + i] = L.lastg[s][i];
   }
-  for (int idx = tid; idx < S * 96; idx += kGNT) {
+  for (int idx = tid; idx < S * 96; idx += NT) {
     const int s = idx / 96, i = idx - s * 96;
     if (!sok(s) || L.nfs[s] <= 0) continue;
     float *stp = a.state + (size_t)(sb + s) * st::kWords;
@@ -699,11 +753,11 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
 }
 
 __global__ void __launch_bounds__(kGNT) k_gru16(StagedArgs a) { gru16_body<8, false>(a); }
-__global__ void __launch_bounds__(kGNT) k_fused16(StagedArgs a) { gru16_body<8, true>(a); }
+__global__ void __launch_bounds__(kFNT) k_fused16(StagedArgs a) { gru16_body<8, true>(a); }
 
 hipError_t launch_gru16(const StagedArgs &a, hipStream_t stream) {
   if (a.fuse16)
-    hipLaunchKernelGGL(k_fused16, dim3((a.n_streams + 7) / 8), dim3(kGNT), 0, stream, a);
+    hipLaunchKernelGGL(k_fused16, dim3((a.n_streams + 7) / 8), dim3(kFNT), 0, stream, a);
   else
     hipLaunchKernelGGL(k_gru16, dim3((a.n_streams + 7) / 8), dim3(kGNT), 0, stream, a);
   return hipGetLastError();

@@ -61,28 +61,38 @@ __device__ __forceinline__ void win_apply(const WinRaw &w, const float *hw, int 
 
 // One frame's pitch spectrum, one wave (rnnoise compute_frame_features after
 // pitch_search / remove_doubling, called from rnnoise_process_frame at
-// Denoiser.zig:60): the pitch window at lag pit -> FFT -> P (HBM), the band
-// energies Ep and the normalised correlations Exp (HBM, k_synthw reads them),
-// DCT(Exp).  Returns, on lanes 0..6, the frame's features 34..40 (lane 6:
-// .01 (pit - 300)); the caller stores them.  R: the wave's exchange region.
-__device__ __forceinline__ float pspec_frame(const StagedArgs &a, int f, int pit, const WaveTabs &tb,
-                                             const wfft::Tw &tw, float2 *R, int lane) {
-  const BandTab &T = tb.T;
-  float *tr = reinterpret_cast<float *>(R);
-  WinRaw cur;
-  win_load(cur, frame_pb(a, f) + (kPitchBuf - kWin - pit), lane);
-  // X of bins < 400 (Exp terms) and the band's Ex, issued before the
-  // transform (Ex loaded after the P stores waited for them)
+// Denoiser.zig:60), in two halves.  pspec_transform: the pitch window at lag
+// pit -> FFT -> P (HBM), the Ep and Exp band terms into the wave's exchange
+// region R (its inputs from pspec_load; the frame's Ex of band `lane` goes on
+// to the second half).  pspec_features: the band energies Ep and the normalised
+// correlations Exp (HBM, k_synthw reads them), DCT(Exp); returns, on lanes
+// 0..6, the frame's features 34..40 (lane 6: .01 (pit - 300)), which the
+// caller stores.  k_pspecw runs the halves back to back (pspec_frame),
+// k_fused16 one per phase.
+// A frame's inputs to pspec_transform: the raw pitch window, X of bins < 400
+// (Exp terms) and the band's Ex (k_fused16 loads them a phase ahead)
+struct PspecIn {
+  WinRaw w;
   float2 xr[7];
+  float exl;
+};
+__device__ __forceinline__ void pspec_load(PspecIn &in, const StagedArgs &a, int f, int pit, int lane) {
+  win_load(in.w, frame_pb(a, f) + (kPitchBuf - kWin - pit), lane);
   const float2 *X = a.X + (size_t)f * kFreq;
 #pragma unroll
   // (unconditional loads, lanes past the bins read bin 480 and are never
   // used: a masked load's block would take its consumers, and their wait,
   // right after it)
-  for (int r = 0; r < 7; r++) xr[r] = X[min(64 * r + lane, kFreq - 1)];
-  const float exl = a.Ex[(size_t)f * kBands + min(lane, kBands - 1)];
+  for (int r = 0; r < 7; r++) in.xr[r] = X[min(64 * r + lane, kFreq - 1)];
+  in.exl = a.Ex[(size_t)f * kBands + min(lane, kBands - 1)];
+}
+__device__ __forceinline__ void pspec_transform(const StagedArgs &a, int f, const PspecIn &in, const WaveTabs &tb,
+                                                const wfft::Tw &tw, float2 *R, int lane) {
+  const BandTab &T = tb.T;
+  float *tr = reinterpret_cast<float *>(R);
+  const float2 *xr = in.xr;
   float2 v[16];
-  win_apply(cur, tb.hw, lane, v);
+  win_apply(in.w, tb.hw, lane, v);
   wfft::run(v, tw, tb.tw, R, lane);
   float2 *P = a.P + (size_t)f * kFreq;
 #pragma unroll
@@ -97,6 +107,11 @@ __device__ __forceinline__ float pspec_frame(const StagedArgs &a, int f, int pit
     }
   }
   wfft::wsync();
+}
+__device__ __forceinline__ float pspec_features(const StagedArgs &a, int f, int pit, const WaveTabs &tb,
+                                                const float2 *R, int lane, float exl) {
+  const BandTab &T = tb.T;
+  const float *tr = reinterpret_cast<const float *>(R);
   // Ep chains on lanes 0..21, Exp chains on lanes 32..53
   const int h = lane >> 5, b = lane & 31;
   float cv = 0;
@@ -119,6 +134,14 @@ __device__ __forceinline__ float pspec_frame(const StagedArgs &a, int f, int pit
   if (lane == 6) val = (float)(.01 * (pit - 300));
   wfft::wsync();
   return val;
+}
+__device__ __forceinline__ float pspec_frame(const StagedArgs &a, int f, int pit, const WaveTabs &tb,
+                                             const wfft::Tw &tw, float2 *R, int lane) {
+  // (inputs loaded before the transform: Ex loaded after the P stores waited for them)
+  PspecIn in;
+  pspec_load(in, a, f, pit, lane);
+  pspec_transform(a, f, in, tb, tw, R, lane);
+  return pspec_features(a, f, pit, tb, R, lane, in.exl);
 }
 
 }  // namespace fvad

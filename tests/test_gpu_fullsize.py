@@ -343,6 +343,26 @@ def test_bench_schedule_fp16_every_stream(fvad_mod, oracle_mod, model):
             schedule, wv, wb, n_seg, diffs))
 
 
+@pytest.mark.timeout(900)
+def test_bench_schedule_fused16_equals_fp16(fvad_mod, model):
+    """configs[4]'s fused FFT -> feature -> GRU kernel (mode fp16_fused,
+    k_fused16) at the bench's size and unsynchronised schedule: every push's
+    outputs and every stream's segments IDENTICAL to the fp16 mode's (the same
+    pitch-spectrum and GRU expressions, so not a tolerance check)."""
+    base, B, P, R = BENCH
+    res = {}
+    for mode in ("fp16", "fp16_fused"):
+        eng = fvad_mod.Engine(model, B, 2, max_ticks=T, mode=mode)
+        eng.attach_vadm()
+        eng.load_synthetic(T, base=base, pushes=P)
+        res[mode] = run_schedule(eng, "nosync", True, B)[:2]
+        del eng
+    (ga, sa), (gb, sb) = res["fp16"], res["fp16_fused"]
+    for key in ga:
+        assert np.array_equal(ga[key], gb[key]), key
+    assert sa == sb
+
+
 @pytest.mark.timeout(600)
 def test_bench_size_i16_equals_float(fvad_mod, model):
     """The 16-bit ingest at the bench's size (2048 stereo streams, 50-tick

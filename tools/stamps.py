@@ -51,6 +51,10 @@ if MODE in ("fp16", "fp16_fused"):
     print("per-wave busy cycles per frame step (phase A | phase B):")
     for w in range(8):
         print("  w%d %8.0f | %8.0f" % (w, buf[w] / frames, buf[8 + w] / frames))
+    if MODE == "fp16_fused":
+        print("pitch-spectrum waves (phase A: transform of u+2 | phase B: its features):")
+        for w in range(8):
+            print("  w%d %8.0f | %8.0f" % (8 + w, buf[16 + w] / frames, buf[24 + w] / frames))
     sys.exit(0)
 tot = sum(buf[:24]) if MODE == "fused" else (sum(buf[:2]) if len(NAMES) > 12 else sum(buf[:12]))
 frames = B * 2 * T
