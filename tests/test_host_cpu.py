@@ -26,6 +26,18 @@ def test_abi_exports_every_declared_symbol(fvad_mod):
     assert names <= bound, sorted(names - bound)
 
 
+def test_header_constants_match_binding(fvad_mod):
+    """The engine modes and debug keys the binding passes are the header's
+    values (FVAD_MODE_FP16_FUSED, r6, included)."""
+    hdr = open(os.path.join(ROOT, "include", "fvad.h")).read()
+    defs = dict((k, int(v)) for k, v in re.findall(r"#define\s+(FVAD_[A-Z0-9_]+)\s+(-?\d+)\b", hdr))
+    for name in ("MODE_STAGED", "MODE_FUSED", "MODE_FP16", "MODE_FP16_FUSED"):
+        assert getattr(fvad_mod, name) == defs["FVAD_" + name], name
+    for name in ("DEBUG_VADM_PAR_SERIAL_EVERY", "DEBUG_VADM_ALWAYS_PAR", "DEBUG_VADM_LT_FULL", "DEBUG_VADM_DEFER_MAX",
+                 "DEBUG_VADM_BOUND_SCALE", "DEBUG_VADM_COUNT", "DEBUG_VADM_NEGATE_AT"):
+        assert getattr(fvad_mod, name) == defs["FVAD_" + name], name
+
+
 @pytest.mark.parametrize("seed", [0, 1, 1234, 2 ** 40 + 7])
 def test_synthetic_model_identical_to_oracle(fvad_mod, oracle_mod, seed):
     assert np.array_equal(fvad_mod.Model(seed=seed).blob(), oracle_mod.Model(seed=seed).blob())
