@@ -29,6 +29,10 @@
 // gain smoothing of u - 4 fill the waves a phase leaves idle.  Operand
 // segments read by layers of different frames in one phase are versioned by
 // frame (OpSeg).
+//
+// k_fused16 (engine mode FVAD_MODE_FP16_FUSED, configs[4]'s "fused FFT ->
+// feature -> GRU kernel") is the same body with k_pspecw's per-frame work on
+// 8 more waves; see above gru16_body.  Its outputs equal k_gru16's bit for bit.
 #pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
 
@@ -188,8 +192,8 @@ struct LdsCore {
 struct LdsSplit : LdsCore {
   alignas(16) half8 dzr[kDzrFrags][64];
 };
-// k_fused16: the pitch-spectrum FFT's exchange regions (one per wave) and
-// tables take that LDS; the denoise z|r fragments are read from L2 instead
+// k_fused16: the pitch-spectrum waves' exchange regions (one per wave) and
+// FFT tables take that LDS; every A fragment is read from L2 instead
 constexpr int kFW = 8;             // k_fused16: pitch-spectrum waves (one per stream), after the 8 GRU waves
 constexpr int kFNT = kGNT + 64 * kFW;
 struct LdsFused : LdsCore {
