@@ -627,6 +627,10 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
     // ---- phase A: z|r gates of vad(u-1), noise(u-2), denoise(u-3); dense(u),
     // vad_out(u-2), den_out(u-4); features(u+1)
     WSTAMP_BEGIN();
+    // waves 5..7 carry the longest phase-A chains (stamps): they issue first
+    // (k_gru16 0.512 -> 0.505 ms interleaved; w5 and w7 only 0.512, phase B's
+    // longest waves raised as well 0.514-0.523)
+    if (W >= 5) __builtin_amdgcn_s_setprio(2);
     if (live(fD)) {
       epi_zr<96>(L, mma_job<-1, 5>(fr, W, L, dzs, lane, fD), W, lane, L.zd, L.sd, kRsd);
       if (W < 4) epi_zr<96>(L, mma_job<-1, 5>(fr, W + 8, L, dzs, lane, fD), W + 8, lane, L.zd, L.sd, kRsd);
@@ -670,6 +674,7 @@ __device__ __forceinline__ void gru16_body(const StagedArgs &a) {
         for (int k = lane + 64 * ((W & 1) + (W >> 2) * 2); k < S * kLight; k += 4 * 64)
           feat_c(u + 1, (k / kLight) * kIt + k % kLight);
     }
+    if (W >= 5) __builtin_amdgcn_s_setprio(0);
     WSTAMP_END(0);
     lds_sync();
     RSTAMP(0);
