@@ -34,10 +34,11 @@ def _same(a, b, tag):
             assert np.array_equal(x[k], y[k]), (tag, s, k)
 
 
-@pytest.mark.parametrize("n_channels", [1, 2, 3])
+@pytest.mark.parametrize("n_channels", [1, 2, 3, 8])
 def test_fused16_equals_fp16_ragged(fvad_mod, model, n_channels):
     """Ragged streams (digital silence in stream 19), ragged pushes, 13
-    streams: one full 8-stream workgroup and a partial one."""
+    streams: one full 8-stream workgroup and a partial one; up to the 8
+    channels an engine takes (8 interleaved frames per tick and stream)."""
     ids = [0, 1, 19, 42, 5, 6, 7, 8, 9, 10, 11, 12, 13]
     secs = [7.0, 5.99, 6.5, 2.5] + [3.0 + 0.11 * i for i in range(9)]
     streams = [fvad_mod.synth_stream(i, int(48000 * s), n_channels)[0] for i, s in zip(ids, secs)]
