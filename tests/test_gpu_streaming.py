@@ -41,7 +41,7 @@ def _chunks(streams, nt_push):
     return out
 
 
-@pytest.mark.parametrize("mode,depth", [("staged", 2), ("fused", 2), ("staged", 3), ("fp16", 3)])
+@pytest.mark.parametrize("mode,depth", [("staged", 2), ("fused", 2), ("staged", 3), ("fp16", 3), ("fp16_fused", 3)])
 def test_submit_collect_equals_push(fvad_mod, models, mode, depth):
     """depth (2 or FVAD_MAX_IN_FLIGHT = 3) pushes in flight, alternating caller
     buffers and the zero-copy input slot, ragged ticks: every output equals
@@ -76,7 +76,7 @@ def test_submit_collect_equals_push(fvad_mod, models, mode, depth):
         assert np.array_equal(a["band"][wf], b["band"][wf])
 
 
-@pytest.mark.parametrize("mode,depth", [("staged", 3), ("fused", 2), ("fp16", 3)])
+@pytest.mark.parametrize("mode,depth", [("staged", 3), ("fused", 2), ("fp16", 3), ("fp16_fused", 3)])
 def test_submit_i16_equals_float_push(fvad_mod, models, mode, depth):
     """16-bit ingest (fvad_engine_submit_i16, k_pcm16): samples k give the
     outputs of a float push of k / 32768.0f (libsndfile's short -> float),
