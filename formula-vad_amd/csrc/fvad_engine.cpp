@@ -210,12 +210,12 @@ struct fvad_engine {
 extern "C" int fvad_engine_stamps(fvad_engine *e, unsigned long long *out, int n) {
   if (!e) return FVAD_EINVAL;
   if (!e->d_stamps) {
-    HIP_TRY(hipMalloc(&e->d_stamps, 64 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(e->d_stamps, 0, 64 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&e->d_stamps, 128 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(e->d_stamps, 0, 128 * sizeof(unsigned long long)));
     return FVAD_OK;
   }
   HIP_TRY(hipStreamSynchronize(e->stream));
-  if (out) HIP_TRY(hipMemcpy(out, e->d_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (out) HIP_TRY(hipMemcpy(out, e->d_stamps, std::min(n, 128) * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return FVAD_OK;
 }
 

@@ -1335,6 +1335,11 @@ __global__ void __launch_bounds__(kR3NT) k_rnn3(StagedArgs a) {
     for (int i = 0; i < 7; i++)
       if (tid == p2[i]) atomicAdd(&a.stamps[8 + i], racc2[1]);
   }
+  // every wave's busy cycles per phase (lane 0): stamps[64 + w] P1, [80 + w] P2
+  if (a.stamps && (tid & 63) == 0) {
+    atomicAdd(&a.stamps[64 + (tid >> 6)], racc2[0]);
+    atomicAdd(&a.stamps[80 + (tid >> 6)], racc2[1]);
+  }
   (void)racc;
   (void)rslot;
 #endif

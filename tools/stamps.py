@@ -39,8 +39,8 @@ e.sync()
 assert L.fvad_engine_stamps(e.h, None, 0) == 0  # allocate + zero
 e.run_resident(T)
 e.sync()
-buf = (C.c_ulonglong * 64)()
-assert L.fvad_engine_stamps(e.h, buf, 64) == 0
+buf = (C.c_ulonglong * 128)()
+assert L.fvad_engine_stamps(e.h, buf, 128) == 0
 if MODE in ("fp16", "fp16_fused"):
     frames = (B // 8) * 2 * T  # one workgroup per 8 streams (kSpw), stamps from thread 0
     gt = sum(buf[48:48 + len(GRU)])
@@ -67,6 +67,10 @@ for i, n in enumerate(NAMES[:24]):
     print("%2d %-28s %6.2f%%  %8.0f cyc/frame" % (i, n, 100.0 * buf[i] / tot, buf[i] / frames))
 if MODE == "fused":
     print("   %-28s %6.2f%%" % ("store state", 100.0 * buf[23] / tot if len(buf) > 23 else 0))
+if MODE == "staged":
+    print("k_rnn3 per-wave busy cycles per frame step (P1 | P2):")
+    for w in range(16):
+        print("  w%-2d %8.0f | %8.0f" % (w, buf[64 + w] / frames, buf[80 + w] / frames))
 
 if MODE == "staged":
     PIT = ["Q0 xf + coarse Syy -> LDS", "Q1 coarse xcorr", "Q2 coarse scan (survivors)", "Q3 fine xcorr",
